@@ -1,0 +1,343 @@
+// K-means kernels for gfx950 (MI355X / CDNA4).
+//
+// Replaces the reference's K-means E-step + accumulate hot loop
+// (ml/java/.../kmeans/regroupallgather/CenCalcTask.java:67-100: per point, argmin
+// over all centroids of the squared L2 distance, then local[c] += (1, x)) and the
+// thread merge (CenMergeTask.java:36-54) and the owner-side average
+// (KMeansCollectiveMapper.java:170-183).
+//
+// Design (MI355X-first, not a translation):
+//  * distances are a GEMM: X[N,dp] (bf16) x (-2C)[Kp,dp]^T on v_mfma_f32_32x32x16_bf16,
+//    with ||c||^2 loaded as the MFMA's initial accumulator (row constant), so the
+//    accumulator IS the distance minus ||x||^2 and the epilogue is a pure argmin.
+//  * centroids sit on the MFMA row axis, points on the lane (column) axis: each lane
+//    owns one point and 16 candidate centroids per 32x32 tile, so the argmin is
+//    register-local (16 keyed fminf -> v_min3) plus one lane<->lane+32 exchange.
+//    The within-tile register index is packed into the 4 low mantissa bits of the
+//    distance (relative perturbation 2^-19, far below the bf16 operand rounding).
+//  * X fragments stay in VGPRs for the whole centroid sweep; centroid tiles stream
+//    through double-buffered LDS (row pitch = odd number of 16-B slots -> ds_read_b128
+//    conflict-free), one barrier per stage; next tile's global loads are issued
+//    before the MFMA block and written to LDS after it (async-STAGE split).
+//  * the padding column d of X holds 1.0 and the matching column of -2C holds 0,
+//    so the accumulation adds (x, 1) = (partial sum, count) in one row: the Harp
+//    centroid row layout (sum + count) falls out of the data layout.
+//  * accumulation: per assigned point, one 256-B contiguous f32 atomic row segment
+//    per wave-instruction (the full-rate atomic shape on gfx950).
+#include "common.h"
+
+namespace {
+
+constexpr float KM_BIG = 1.0e38f;
+
+__device__ __forceinline__ float keyed(float v, unsigned idx) {
+  return __uint_as_float((__float_as_uint(v) & ~0xFu) | idx);
+}
+
+template <int KS, int G, int WAVES, int RG>
+struct KMCfg {
+  static constexpr int DP = KS * 16;                 // padded feature dim (elements)
+  static constexpr int LROW = DP + 8;                // LDS row pitch (elements): (2KS+1) 16-B slots
+  static constexpr int TILE = RG * 32;               // centroids per stage
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int CHUNKS = TILE * KS * 2;       // 16-byte chunks per centroid tile
+  static constexpr int CPT = (CHUNKS + THREADS - 1) / THREADS;
+  static constexpr int A_BYTES = TILE * LROW * 2;
+  static constexpr int STAGE_BYTES = A_BYTES + TILE * 4;
+  static constexpr int PTS = WAVES * G * 32;         // points per workgroup
+};
+
+template <class C>
+__device__ __forceinline__ void stage_load(const bf16x8* __restrict__ cm2, const float* __restrict__ cn,
+                                           int tile, bf16x8 (&regs)[C::CPT], float& cnv) {
+  const int tid = threadIdx.x;
+  const bf16x8* base = cm2 + (size_t)tile * C::CHUNKS;
+#pragma unroll
+  for (int i = 0; i < C::CPT; ++i) {
+    const int ch = tid + i * C::THREADS;
+    if (C::CHUNKS % C::THREADS == 0 || ch < C::CHUNKS) regs[i] = base[ch];
+  }
+  if (tid < C::TILE) cnv = cn[tile * C::TILE + tid];
+}
+
+template <class C>
+__device__ __forceinline__ void stage_store(char* buf, const bf16x8 (&regs)[C::CPT], float cnv) {
+  const int tid = threadIdx.x;
+  constexpr int CPR = C::DP / 8;  // chunks per row
+#pragma unroll
+  for (int i = 0; i < C::CPT; ++i) {
+    const int ch = tid + i * C::THREADS;
+    if (C::CHUNKS % C::THREADS == 0 || ch < C::CHUNKS) {
+      const int row = ch / CPR, c = ch - row * CPR;
+      *(bf16x8*)(buf + (row * C::LROW + c * 8) * 2) = regs[i];
+    }
+  }
+  if (tid < C::TILE) ((float*)(buf + C::A_BYTES))[tid] = cnv;
+}
+
+template <int KS, int G, int WAVES, int RG>
+__global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
+    const __bf16* __restrict__ X, const __bf16* __restrict__ Cm2, const float* __restrict__ cn,
+    long N, int ntiles, int dcount, int* __restrict__ labels, float* __restrict__ mindist,
+    float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial) {
+  using C = KMCfg<KS, G, WAVES, RG>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::STAGE_BYTES + WAVES * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const long pbase = ((long)blockIdx.x * WAVES + wave) * (G * 32);
+
+  // ---- this wave's points: B-operand fragments, resident for the whole sweep
+  bf16x8 xf[G][KS];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    long p = pbase + g * 32 + r;
+    if (p > N - 1) p = N - 1;
+    const bf16x8* row = (const bf16x8*)(X + p * C::DP);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) xf[g][s] = row[2 * s + h];
+  }
+
+  float best[G];
+  int bestt[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) { best[g] = KM_BIG; bestt[g] = 0; }
+
+  bf16x8 sreg[C::CPT];
+  float scn = 0.f;
+  stage_load<C>((const bf16x8*)Cm2, cn, 0, sreg, scn);
+  stage_store<C>(smem, sreg, scn);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = (t + 1) < ntiles;
+    if (more) stage_load<C>((const bf16x8*)Cm2, cn, t + 1, sreg, scn);
+    const char* buf = smem + (t & 1) * C::STAGE_BYTES;
+    const float* cnt = (const float*)(buf + C::A_BYTES);
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+      bf16x8 af[KS];
+      const __bf16* arow = (const __bf16*)buf + (rg * 32 + r) * C::LROW + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) af[s] = *(const bf16x8*)(arow + 16 * s);
+      floatx16 ci;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 v = *(const floatx4*)(cnt + rg * 32 + 8 * q + 4 * h);
+        ci[4 * q + 0] = v[0];
+        ci[4 * q + 1] = v[1];
+        ci[4 * q + 2] = v[2];
+        ci[4 * q + 3] = v[3];
+      }
+      const int tg = t * RG + rg;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        floatx16 acc = ci;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], xf[g][s], acc, 0, 0, 0);
+        float m = keyed(acc[0], 0u);
+#pragma unroll
+        for (int i = 1; i < 16; ++i) m = fminf(m, keyed(acc[i], (unsigned)i));
+        if (m < best[g]) { best[g] = m; bestt[g] = tg; }
+      }
+    }
+    if (more) stage_store<C>(smem + ((t + 1) & 1) * C::STAGE_BYTES, sreg, scn);
+    __syncthreads();
+  }
+
+  // ---- resolve argmin across the two lane halves, write labels / distances
+  int lab[G];
+  float local_obj = 0.f;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float xs = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (float)xf[g][s][j];
+        xs = fmaf(v, v, xs);
+      }
+    xs += __shfl_xor(xs, 32, 64);
+    xs -= 1.0f;  // the count column of X holds 1.0
+    const float ob = __shfl_xor(best[g], 32, 64);
+    const int obt = __shfl_xor(bestt[g], 32, 64);
+    const bool take = h ? (ob <= best[g]) : (ob < best[g]);
+    const float bv = take ? ob : best[g];
+    const int bt = take ? obt : bestt[g];
+    const int hw = take ? (1 - h) : h;
+    const unsigned reg = __float_as_uint(bv) & 0xFu;
+    const int idx = bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
+    lab[g] = idx;
+    const long p = pbase + g * 32 + r;
+    const float dist = fmaxf(bv + xs, 0.f);
+    if (h == 0 && p < N) {
+      labels[p] = idx;
+      if (mindist) mindist[p] = dist;
+      local_obj += dist;
+    }
+  }
+  if (obj_partial) {
+    local_obj = wave_sum(local_obj);
+    float* red = (float*)(smem + 2 * C::STAGE_BYTES);
+    if (lane == 0) red[wave] = local_obj;
+    __syncthreads();
+    if (tid == 0) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) s += red[w];
+      obj_partial[blockIdx.x] = s;
+    }
+  }
+
+  // ---- accumulate (x, 1) rows into the per-centroid partial sums
+  if (sums) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      for (int i = 0; i < 32; ++i) {
+        const long p = pbase + g * 32 + i;
+        if (p >= N) break;
+        const int l = __shfl(lab[g], i, 64);
+        const __bf16* xr = X + p * C::DP;
+        float* sr = sums + (long)l * ld_sums;
+        for (int c = lane; c <= dcount; c += 64) atomicAdd(sr + c, (float)xr[c]);
+      }
+    }
+  }
+}
+
+// sums[Kr][ld] (column d = count) -> c[Kr][d]; empty clusters keep their old centroid.
+__global__ void kmeans_normalize_kernel(const float* __restrict__ sums, int ld, float* __restrict__ c,
+                                        int Kr, int d, float* __restrict__ counts) {
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= Kr) return;
+  const float cnt = sums[(long)row * ld + d];
+  if (counts && lane == 0) counts[row] = cnt;
+  if (cnt > 0.f) {
+    const float inv = 1.0f / cnt;
+    for (int j = lane; j < d; j += 64) c[(long)row * d + j] = sums[(long)row * ld + j] * inv;
+  }
+}
+
+// c[K][d] fp32 -> Cm2[Kp][dp] = -2*bf16(c) (cols >= d zero), cn[Kp] = ||bf16(c)||^2 (pad rows: +BIG)
+__global__ void kmeans_prepare_kernel(const float* __restrict__ c, int K, int d, int Kp, int dp,
+                                      __bf16* __restrict__ Cm2, float* __restrict__ cn) {
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= Kp) return;
+  float s = 0.f;
+  for (int j = lane; j < dp; j += 64) {
+    float v = 0.f;
+    if (row < K && j < d) v = c[(long)row * d + j];
+    const __bf16 b = (__bf16)v;
+    const float bf = (float)b;
+    s = fmaf(bf, bf, s);
+    Cm2[(long)row * dp + j] = (__bf16)(-2.0f * bf);
+  }
+  s = wave_sum(s);
+  if (lane == 0) cn[row] = row < K ? s : KM_BIG;
+}
+
+// Counter-based uniform generator (splitmix64 of the element index): device-side
+// synthetic points like the reference's DataGenRunnable (U[lo,hi)), no host copy.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, int dp, float lo,
+                                         float hi, unsigned long long seed, long row0, int one_col) {
+  const long total = N * (long)dp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / dp;
+    const int col = (int)(i - row * dp);
+    float v = 0.f;
+    if (col < d) {
+      const unsigned long long z = splitmix64(seed ^ ((unsigned long long)(row0 + row) * 0x100000001B3ull + col));
+      v = lo + (hi - lo) * (float)((z >> 40) * (1.0 / 16777216.0));
+    } else if (one_col && col == d) {
+      v = 1.0f;
+    }
+    X[i] = (__bf16)v;
+  }
+}
+
+template <int KS, int G, int WAVES, int RG>
+int launch_assign(const void* X, const void* Cm2, const float* cn, long N, int Kp, int d, int* labels,
+                  float* mindist, float* sums, int ld_sums, float* obj_partial, hipStream_t stream) {
+  using C = KMCfg<KS, G, WAVES, RG>;
+  if (Kp % C::TILE) return HARP_EBADARG;
+  const long nblk = (N + C::PTS - 1) / C::PTS;
+  kmeans_assign_kernel<KS, G, WAVES, RG><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
+      (const __bf16*)X, (const __bf16*)Cm2, cn, N, Kp / C::TILE, d, labels, mindist, sums, ld_sums,
+      obj_partial);
+  return harp_launch_status();
+}
+
+// variant -> (G, WAVES, RG). Kp must be a multiple of 128 for every variant.
+#define KM_VARIANTS(KS)                                                                              \
+  switch (variant) {                                                                               \
+    case 0: return launch_assign<KS, 2, 4, 2>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
+    case 1: return launch_assign<KS, 4, 4, 2>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
+    case 2: return launch_assign<KS, 2, 8, 2>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
+    case 3: return launch_assign<KS, 2, 4, 4>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
+    default: return HARP_EBADARG;                                                                  \
+  }
+
+}  // namespace
+
+HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
+  switch (variant) {
+    case 0: return 4 * 2 * 32;
+    case 1: return 4 * 4 * 32;
+    case 2: return 8 * 2 * 32;
+    case 3: return 4 * 2 * 32;
+    default: return -1;
+  }
+}
+
+HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, const float* cn, long N, int dp, int Kp,
+                                   int d, int* labels, float* mindist, float* sums, int ld, float* op,
+                                   int variant, hipStream_t s) {
+  if (N <= 0 || d + 1 > dp || dp % 16 || Kp <= 0 || Kp % 128) return HARP_EBADARG;
+  switch (dp / 16) {
+    case 1: KM_VARIANTS(1)
+    case 2: KM_VARIANTS(2)
+    case 3: KM_VARIANTS(3)
+    case 4: KM_VARIANTS(4)
+    case 5: KM_VARIANTS(5)
+    case 6: KM_VARIANTS(6)
+    case 7: KM_VARIANTS(7)
+    case 8: KM_VARIANTS(8)
+    default: return HARP_EUNSUPPORTED;
+  }
+}
+
+HARP_EXPORT int harp_kmeans_normalize(const float* sums, int ld, float* c, int Kr, int d, float* counts,
+                                      hipStream_t s) {
+  if (Kr <= 0) return HARP_OK;
+  const int wpb = 4;
+  kmeans_normalize_kernel<<<dim3((Kr + wpb - 1) / wpb), dim3(64 * wpb), 0, s>>>(sums, ld, c, Kr, d, counts);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_kmeans_prepare(const float* c, int K, int d, int Kp, int dp, void* Cm2, float* cn,
+                                    hipStream_t s) {
+  if (Kp < K || dp < d) return HARP_EBADARG;
+  const int wpb = 4;
+  kmeans_prepare_kernel<<<dim3((Kp + wpb - 1) / wpb), dim3(64 * wpb), 0, s>>>(c, K, d, Kp, dp, (__bf16*)Cm2, cn);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_uniform_rows_bf16(void* X, long N, int d, int dp, float lo, float hi,
+                                       unsigned long long seed, long row0, int one_col, hipStream_t s) {
+  if (N <= 0) return HARP_OK;
+  long blocks = (N * (long)dp + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  uniform_rows_bf16_kernel<<<dim3((unsigned)blocks), dim3(256), 0, s>>>((__bf16*)X, N, d, dp, lo, hi, seed, row0,
+                                                                       one_col);
+  return harp_launch_status();
+}

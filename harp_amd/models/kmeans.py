@@ -1,0 +1,264 @@
+"""K-means with Harp's four interchangeable model-synchronisation strategies.
+
+Reference workloads:
+  * ml/java kmeans/regroupallgather (headline): per iteration threads compute local
+    sums (CenCalcTask), merge them (CenMergeTask), then ``regroup`` -> average at the
+    owner -> ``allgather`` (KMeansCollectiveMapper.java:107-211);
+  * contrib kmeans {allreduce, regroup-allgather, broadcast-reduce, push-pull}
+    (contrib/.../kmeans/common/KmeansMapCollective.java:30-270) and the DAAL variant's
+    same four strategies (ml/daal/.../daal_kmeans/regroupallgather/
+    KMeansDaalCollectiveMapper.java:435-530);
+  * kmeans/rotation: centroid partitions rotate through the ring while each worker
+    keeps its points (ml/java/.../kmeans/rotation/KMeansCollectiveMapper.java:106-228).
+
+MI355X design: points live in HBM as padded bf16 rows (device-generated), one fused
+MFMA kernel does E-step + argmin + accumulation (``ops.kmeans.assign``), the centroid
+partial-sum table is a :class:`PackedTable` whose rows are the partitions, so each
+strategy's collectives are single RCCL calls: allreduce -> ncclAllReduce; regroup ->
+ncclReduceScatter (block partitioner = owner-contiguous slab), allgather ->
+ncclAllGather; reduce + broadcast -> ncclReduce + ncclBroadcast; push/pull -> owner
+all-to-all-v. Per-iteration phase times mirror the reference's Compute/Merge/Aggregate
+log (KMeansCollectiveMapper.java:191-193).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import asdict, dataclass, field
+from typing import List, Optional
+
+import torch
+
+from ..core.combiner import ArrCombiner, Operation
+from ..core.partition import Partitioner
+from ..core.table import PackedTable, Table
+from ..ops import kmeans as K
+from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
+
+STRATEGIES = ("allreduce", "regroup_allgather", "bcast_reduce", "push_pull", "rotation")
+
+
+@dataclass
+class KMeansConfig:
+    num_points: int = 1000            # points on THIS worker (weak split is the caller's choice)
+    num_centroids: int = 10
+    dim: int = 100
+    iterations: int = 10
+    strategy: str = "regroup_allgather"
+    seed: int = 1
+    data_lo: float = 0.0
+    data_hi: float = 1000.0
+    variant: int = K.DEFAULT_VARIANT   # HIP kernel tiling variant
+    objective_every: int = 1           # compute the objective every k iterations (0: never)
+
+
+class BlockPartitioner(Partitioner):
+    """Owner of row id = id // ceil(n/P): contiguous owner slabs, so a regroup of the
+    packed centroid table is a reduce-scatter with no permutation."""
+
+    def __init__(self, num_workers: int, n: int):
+        super().__init__(num_workers)
+        self.block = max(1, math.ceil(n / num_workers))
+
+    def get_worker_id(self, partition_id: int) -> int:
+        return min(int(partition_id) // self.block, self.num_workers - 1)
+
+
+class KMeansCollectiveMapper(CollectiveMapper):
+    """One K-means job on this worker. ``map_collective`` reads points from the input
+    split (text rows ``x1 .. xd``, like contrib Utils.generateData) or generates them on
+    the device when the split is empty."""
+
+    def __init__(self, comm=None, config: Optional[KMeansConfig] = None, points: Optional[torch.Tensor] = None,
+                 init_centroids: Optional[torch.Tensor] = None, metrics=None):
+        super().__init__(comm, metrics)
+        self.cfg = config or KMeansConfig()
+        self._points_in = points
+        self._init_c = init_centroids
+        self.history: List[dict] = []
+
+    # -- data -----------------------------------------------------------------------------
+    def load_points(self, reader: KeyValReader) -> torch.Tensor:
+        cfg = self.cfg
+        if self._points_in is not None:
+            return K.pack_points(self._points_in.float(), self.device)
+        files = [v for _, v in reader]
+        if files:
+            rows = []
+            for f in files:
+                with open(f) as fh:
+                    for line in fh:
+                        vals = line.split()
+                        if vals:
+                            rows.append([float(v) for v in vals])
+            return K.pack_points(torch.tensor(rows, dtype=torch.float32), self.device)
+        return K.generate_points(cfg.num_points, cfg.dim, cfg.data_lo, cfg.data_hi,
+                                 seed=cfg.seed * 7919 + 17, device=self.device,
+                                 row0=self.get_self_id() * cfg.num_points)
+
+    def initial_centroids(self) -> torch.Tensor:
+        cfg = self.cfg
+        if self._init_c is not None:
+            return self._init_c.float().to(self.device)
+        g = torch.Generator().manual_seed(cfg.seed)
+        return (torch.rand((cfg.num_centroids, cfg.dim), generator=g) * (cfg.data_hi - cfg.data_lo)
+                + cfg.data_lo).to(self.device)
+
+    # -- main ------------------------------------------------------------------------------
+    def map_collective(self, reader: KeyValReader, context: Context) -> None:
+        self.init_model(reader)
+        for it in range(self.cfg.iterations):
+            self.step(it)
+        self.finish()
+
+    def init_model(self, reader: KeyValReader) -> None:
+        """Load/generate points, create + broadcast the initial centroids."""
+        cfg = self.cfg
+        if cfg.strategy not in STRATEGIES:
+            raise ValueError(f"unknown strategy {cfg.strategy}")
+        dev = self.device
+        self.X = self.load_points(reader)
+        d, k = cfg.dim, cfg.num_centroids
+        self.dp = self.X.shape[1]
+        Kp = K.padded_k(k)
+        self.ids = list(range(Kp))
+        self.sumop = ArrCombiner(Operation.SUM)
+        # centroid table [Kp, d] fp32: master creates it, chain-broadcast to all
+        # (KMeansCollectiveMapper.java:295-313 broadcast("main","broadcast-centroids"))
+        if self.is_master():
+            c0 = torch.zeros((Kp, d), dtype=torch.float32, device=dev)
+            c0[:k] = self.initial_centroids()
+            cen = PackedTable(self.ids, c0, table_id=0, combiner=self.sumop)
+        else:
+            cen = PackedTable([], torch.zeros((0, d), dtype=torch.float32, device=dev), table_id=0,
+                              combiner=self.sumop)
+        if not self.broadcast("main", "broadcast-centroids", cen, 0, False):
+            raise IOError("Fail to bcast")
+        self.c = cen.buffer  # [Kp, d]
+        self.op = K.prepare(self.c[:k].contiguous(), self.dp)
+        self.sums = torch.zeros((Kp, self.dp), dtype=torch.float32, device=dev)
+        self.part = BlockPartitioner(self.get_num_workers(), Kp)
+        self.lab = torch.empty(self.X.shape[0], dtype=torch.int32, device=dev)
+        self.objective = []
+
+    def step(self, it: int) -> None:
+        """One Lloyd iteration: fused assign+accumulate, model sync, operand prepare."""
+        cfg = self.cfg
+        timer = self.metrics.timer
+        t_it = time.perf_counter()
+        want_obj = cfg.objective_every > 0 and (it % cfg.objective_every == 0 or it == cfg.iterations - 1)
+        with timer.phase("compute"):
+            self.sums.zero_()
+            _, obj = K.assign(self.X, self.op, sums=self.sums, labels=self.lab, want_objective=want_obj,
+                              variant=cfg.variant)
+        with timer.phase("sync"):
+            self.c = self._sync(it, self.sums, self.c, self.part, self.ids, self.sumop, cfg.dim, cfg.num_centroids)
+        with timer.phase("prepare"):
+            self.op = K.prepare(self.c[:cfg.num_centroids], self.dp, self.op)
+        if obj is not None:
+            ot = obj.reshape(1).to(torch.float64)
+            if self.get_num_workers() > 1:
+                self.comm.all_reduce(ot)
+            self.objective.append(float(ot.item()))
+        self.history.append({"iter": it, "s": time.perf_counter() - t_it})
+
+    def finish(self) -> None:
+        k = self.cfg.num_centroids
+        self.centroids = self.c[:k].clone()
+        self.labels = self.lab
+        self.result = {"objective": self.objective, "centroids": self.centroids.cpu() if self.is_master() else None}
+
+    # -- model synchronisation strategies ----------------------------------------------
+    def _sync(self, it, sums, c, part, ids, sumop, d, k):
+        s = self.cfg.strategy
+        Kp = sums.shape[0]
+        if s == "allreduce":
+            t = PackedTable(ids, sums, combiner=sumop)
+            t.static_layout = True
+            if not self.allreduce("main", f"allreduce-{it}", t):
+                raise IOError("allreduce failed")
+            return K.normalize(t.buffer, c, d)
+        if s == "regroup_allgather":
+            t = PackedTable(ids, sums, combiner=sumop)
+            t.static_layout = True
+            if not self.regroup("main", f"regroup-{it}", t, part):
+                raise IOError("regroup failed")
+            mine = t.ids
+            lo = mine[0] if mine else 0
+            cs = c[lo:lo + len(mine)]
+            K.normalize(t.buffer, cs, d)  # average at the owner (KMeansCollectiveMapper.java:170-183)
+            ct = PackedTable(mine, cs.clone(), combiner=sumop)
+            if not self.allgather("main", f"allgather-{it}", ct):
+                raise IOError("allgather failed")
+            return ct.buffer
+        if s == "bcast_reduce":
+            t = PackedTable(ids, sums, combiner=sumop)
+            t.static_layout = True
+            if not self.reduce("main", f"reduce-{it}", t, 0):
+                raise IOError("reduce failed")
+            if self.is_master():
+                K.normalize(t.buffer, c, d)
+                ct = PackedTable(ids, c, combiner=sumop)
+            else:
+                ct = PackedTable([], c[:0], combiner=sumop)
+            if not self.broadcast("main", f"bcast-{it}", ct, 0, True):
+                raise IOError("broadcast failed")
+            return ct.buffer
+        if s == "push_pull":
+            # global table: each worker owns a block of centroid ids (zeros each iteration)
+            P, me = self.get_num_workers(), self.get_self_id()
+            mine = [i for i in ids if part.get_worker_id(i) == me]
+            glob = Table(1, sumop)
+            for i in mine:
+                glob.add(i, torch.zeros(sums.shape[1], dtype=sums.dtype, device=sums.device))
+            local = Table(2, sumop)
+            for i in range(k):
+                local.add(i, sums[i])
+            if not self.push("main", f"push-{it}", local, glob, part):
+                raise IOError("push failed")
+            for p in glob.get_partitions():
+                row = p.get()
+                cnt = row[d]
+                if float(cnt) > 0:
+                    row[:d] /= cnt
+                    row[d] = 1.0
+                else:
+                    row[:d] = c[p.id()]
+                    row[d] = 1.0
+            pulled = Table(3, sumop)
+            for i in range(k):
+                pulled.add(i, torch.zeros(sums.shape[1], dtype=sums.dtype, device=sums.device))
+            if not self.pull("main", f"pull-{it}", pulled, glob, True):
+                raise IOError("pull failed")
+            newc = c.clone()
+            for i in range(k):
+                newc[i] = pulled[i][:d]
+            return newc
+        if s == "rotation":
+            # all-to-all of partial sums by owner, normalize, then rotate the centroid
+            # blocks around the ring P-1 times so every worker sees every block
+            t = PackedTable(ids, sums, combiner=sumop)
+            t.static_layout = True
+            if not self.regroup("main", f"regroup-{it}", t, part):
+                raise IOError("regroup failed")
+            mine = t.ids
+            lo = mine[0] if mine else 0
+            cs = c[lo:lo + len(mine)]
+            K.normalize(t.buffer, cs, d)
+            block = PackedTable(mine, cs.clone(), combiner=sumop)
+            newc = c.clone()
+            for step in range(self.get_num_workers()):
+                b_ids = block.ids
+                if b_ids:
+                    newc[b_ids[0]:b_ids[0] + len(b_ids)] = block.buffer
+                if step < self.get_num_workers() - 1 and not self.rotate("main", f"rotate-{it}-{step}", block):
+                    raise IOError("rotate failed")
+            return newc
+        raise ValueError(s)
+
+
+def run_kmeans(comm, cfg: KMeansConfig, points=None, init_centroids=None) -> dict:
+    """Launcher target: run one K-means job on this rank, return objective history."""
+    m = KMeansCollectiveMapper(comm, cfg, points, init_centroids)
+    m.run(KeyValReader([]))
+    return {"objective": m.objective, "centroids": m.centroids.cpu(), "phases": m.metrics.timer.flush()}

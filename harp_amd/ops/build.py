@@ -1,0 +1,92 @@
+"""In-tree build of the native libraries.
+
+* ``harp_amd/_native/libharp_kernels.so`` — every ``csrc/*.hip`` kernel family, compiled
+  by hipcc for gfx950 only (``--offload-arch=gfx950``), exporting ``extern "C"``
+  launchers that take raw device pointers + a ``hipStream_t``.
+* ``harp_amd/_native/libharp_runtime.so`` — host-side C++ runtime pieces
+  (``csrc/host/*.cpp``: partition-table checkpoint I/O, big-endian codec, 2-D block
+  scheduler), built with g++.
+
+Both are loaded with ctypes *after* ``import torch`` so the kernels launch through the
+HIP runtime torch already loaded (same soname ``libamdhip64.so.7``).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+from typing import List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "csrc")
+NATIVE = os.path.join(ROOT, "harp_amd", "_native")
+OBJ = os.path.join(ROOT, "build", "obj")
+KERNEL_LIB = os.path.join(NATIVE, "libharp_kernels.so")
+RUNTIME_LIB = os.path.join(NATIVE, "libharp_runtime.so")
+
+ARCH = os.environ.get("HARP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-I" + CSRC]
+CXX = os.environ.get("CXX", "g++")
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I" + CSRC]
+
+
+def _stale(target: str, deps: List[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+
+
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(NATIVE, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + headers):
+            todo.append([HIPCC] + HIP_FLAGS + ["-c", s, "-o", o])
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for fut in [ex.submit(_run, c) for c in todo]:
+                fut.result()
+        if verbose:
+            print(f"[harp build] compiled {len(todo)} HIP source(s)", file=sys.stderr)
+    if force or todo or _stale(KERNEL_LIB, objs):
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", KERNEL_LIB] + objs)
+    return KERNEL_LIB
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(NATIVE, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    headers = glob.glob(os.path.join(CSRC, "host", "*.h"))
+    if not srcs:
+        return ""
+    if force or _stale(RUNTIME_LIB, srcs + headers):
+        _run([CXX] + CXX_FLAGS + ["-shared", "-o", RUNTIME_LIB] + srcs)
+        if verbose:
+            print(f"[harp build] linked {RUNTIME_LIB}", file=sys.stderr)
+    return RUNTIME_LIB
+
+
+def build_all(force: bool = False, verbose: bool = True) -> None:
+    build_kernels(force=force, verbose=verbose)
+    build_runtime(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

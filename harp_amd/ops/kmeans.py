@@ -1,0 +1,156 @@
+"""K-means device ops: padded point layout, assign+accumulate, normalize, prepare.
+
+GPU tensors run the gfx950 kernels in ``csrc/kmeans.hip``; CPU tensors run the PyTorch
+fp32 reference of the same op (also the numerics oracle in the GPU tests).
+
+Layouts (chosen for the MFMA kernel):
+  * points  ``X  [n, dp]`` bf16 (GPU) / fp32 (CPU), ``dp = round_up(d + 1, 16)``;
+    column ``d`` holds 1.0 so the accumulated row carries the count, columns > d are 0;
+  * centroids (master copy) ``c [K, d]`` fp32;
+  * kernel operand ``Cm2 [Kp, dp]`` bf16 = -2*bf16(c) and ``cn [Kp]`` = ||bf16(c)||^2,
+    padded to ``Kp = round_up(K, 128)`` rows that can never win (cn = 1e38);
+  * partial sums ``S [K, dp]`` fp32: columns ``0..d-1`` = sum of x, column ``d`` = count
+    — the reference's centroid row (count + d values,
+    KMeansCollectiveMapper.java:213-237) in a device-friendly order.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+KP_ALIGN = 128
+DEFAULT_VARIANT = 2
+
+
+def padded_dim(d: int) -> int:
+    return max(16, (d + 1 + 15) // 16 * 16)
+
+
+def padded_k(k: int) -> int:
+    return (k + KP_ALIGN - 1) // KP_ALIGN * KP_ALIGN
+
+
+def pack_points(x: torch.Tensor, device: torch.device | str | None = None) -> torch.Tensor:
+    """[n, d] -> padded [n, dp] (bf16 on GPU, fp32 on CPU) with the count column."""
+    device = torch.device(device) if device is not None else x.device
+    n, d = x.shape
+    dp = padded_dim(d)
+    dt = torch.bfloat16 if device.type == "cuda" else torch.float32
+    out = torch.zeros((n, dp), dtype=dt, device=device)
+    out[:, :d] = x.to(device=device, dtype=dt)
+    out[:, d] = 1.0
+    return out
+
+
+def generate_points(n: int, d: int, lo: float = 0.0, hi: float = 1000.0, seed: int = 0,
+                    device: torch.device | str = "cpu", row0: int = 0) -> torch.Tensor:
+    """Synthetic U[lo, hi) points in the padded layout, generated on the device
+    (the reference's DataGenRunnable writes U[0,1000) doubles, KMUtil.java:112-178)."""
+    device = torch.device(device)
+    dp = padded_dim(d)
+    if device.type == "cuda" and _lib.use_native(torch.empty(0, device=device)):
+        X = torch.empty((n, dp), dtype=torch.bfloat16, device=device)
+        _lib.check(_lib.kernels().harp_uniform_rows_bf16(X.data_ptr(), n, d, dp, float(lo), float(hi),
+                                                         seed & 0xFFFFFFFFFFFFFFFF, row0, 1,
+                                                         _lib.stream_ptr(device)), "uniform_rows")
+        return X
+    g = torch.Generator().manual_seed(seed * 1000003 + row0)
+    x = torch.rand((n, d), generator=g, dtype=torch.float32) * (hi - lo) + lo
+    return pack_points(x, device)
+
+
+@dataclass
+class CentroidOperand:
+    Cm2: torch.Tensor  # [Kp, dp]
+    cn: torch.Tensor   # [Kp]
+    K: int
+    d: int
+
+
+def prepare(c: torch.Tensor, dp: int, out: Optional[CentroidOperand] = None) -> CentroidOperand:
+    """Build the kernel operand (-2*bf16(c), ||bf16(c)||^2) from fp32 centroids."""
+    K, d = c.shape
+    Kp = padded_k(K)
+    dev = c.device
+    if out is None:
+        dt = torch.bfloat16 if dev.type == "cuda" else torch.float32
+        out = CentroidOperand(torch.empty((Kp, dp), dtype=dt, device=dev), torch.empty(Kp, dtype=torch.float32, device=dev), K, d)
+    if _lib.use_native(c):
+        cc = c.contiguous().float()
+        _lib.check(_lib.kernels().harp_kmeans_prepare(cc.data_ptr(), K, d, Kp, dp, out.Cm2.data_ptr(),
+                                                      out.cn.data_ptr(), _lib.stream_ptr(dev)), "kmeans_prepare")
+        return out
+    out.Cm2.zero_()
+    out.Cm2[:K, :d] = -2.0 * c
+    out.cn.fill_(1e38)
+    out.cn[:K] = (c.double() ** 2).sum(1).float()
+    return out
+
+
+def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = None,
+           labels: Optional[torch.Tensor] = None, want_objective: bool = True, variant: int = DEFAULT_VARIANT,
+           obj_partial: Optional[torch.Tensor] = None):
+    """Assign every point to its nearest centroid; optionally accumulate (x, 1) into
+    ``sums`` [K, dp] and return the sum of squared distances (0-dim fp64 tensor).
+
+    Returns (labels, objective)."""
+    n, dp = X.shape
+    dev = X.device
+    if labels is None:
+        labels = torch.empty(n, dtype=torch.int32, device=dev)
+    if _lib.use_native(X):
+        lib = _lib.kernels()
+        ppb = lib.harp_kmeans_points_per_block(variant)
+        if ppb <= 0:
+            raise ValueError(f"unknown kmeans kernel variant {variant}")
+        nblk = (n + ppb - 1) // ppb
+        if want_objective and (obj_partial is None or obj_partial.numel() < nblk):
+            obj_partial = torch.empty(nblk, dtype=torch.float32, device=dev)
+        if sums is not None:
+            assert sums.dtype == torch.float32 and sums.shape[1] >= op.d + 1 and sums.is_contiguous()
+            assert sums.shape[0] >= op.Cm2.shape[0], "sums needs Kp (padded) rows"
+            assert sums.device == dev
+        assert X.dtype == torch.bfloat16 and X.is_contiguous() and op.Cm2.shape[1] == dp
+        st = lib.harp_kmeans_assign(X.data_ptr(), op.Cm2.data_ptr(), op.cn.data_ptr(), n, dp, op.Cm2.shape[0], op.d,
+                                    labels.data_ptr(), None, _lib.ptr(sums), sums.stride(0) if sums is not None else 0,
+                                    _lib.ptr(obj_partial) if want_objective else None, variant, _lib.stream_ptr(dev))
+        _lib.check(st, "kmeans_assign")
+        obj = obj_partial[:nblk].double().sum() if want_objective else None
+        return labels, obj
+    # CPU reference (fp32)
+    Xf = X.float()
+    d = op.d
+    x = Xf[:, :d]
+    C = -0.5 * op.Cm2[: op.K, :d].float()
+    dist = op.cn[: op.K].unsqueeze(0) - 2.0 * (x @ C.t())
+    lab = dist.argmin(1)
+    labels.copy_(lab.to(labels.dtype))
+    if sums is not None:
+        sums[:, : d + 1].index_add_(0, lab, Xf[:, : d + 1])
+    obj = None
+    if want_objective:
+        xs = (x.double() ** 2).sum(1)
+        obj = (dist.gather(1, lab[:, None])[:, 0].double() + xs).clamp_min(0).sum()
+    return labels, obj
+
+
+def normalize(sums: torch.Tensor, c: torch.Tensor, d: int, counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """c[k] = sums[k, :d] / sums[k, d] where the count is > 0 (empty clusters keep c)."""
+    Kr = c.shape[0]
+    if _lib.use_native(c):
+        assert sums.is_contiguous() and c.is_contiguous()
+        _lib.check(_lib.kernels().harp_kmeans_normalize(sums.data_ptr(), sums.stride(0), c.data_ptr(), Kr, d,
+                                                        _lib.ptr(counts), _lib.stream_ptr(c.device)),
+                   "kmeans_normalize")
+        return c
+    cnt = sums[:, d]
+    m = cnt > 0
+    c[m] = sums[m, :d] / cnt[m, None]
+    if counts is not None:
+        counts.copy_(cnt)
+    return c

@@ -1,0 +1,72 @@
+"""K-means on CPU/gloo: BASELINE config #1 and the reference's km.sh accuracy gate.
+
+km.sh (contrib/test_scripts/km.sh:47,58): 1000 points, K=10, d=10, U[0,10), 2 workers,
+100 iterations, every sync strategy; "MSE" (mean point->centroid Euclidean distance,
+contrib KmeansMapper calcEucDistSquare returns the sqrt) must land in (7.0, 7.8)."""
+import pytest
+import torch
+
+from harp_amd.models.kmeans import STRATEGIES, KMeansConfig, run_kmeans
+from harp_amd.runtime.launcher import launch
+
+
+def _data(n, d, k, hi, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand((n, d), generator=g, dtype=torch.float64) * hi
+    c0 = torch.rand((k, d), generator=g, dtype=torch.float64) * hi
+    return x.float(), c0.float()
+
+
+def _job(comm, cfg, x, c0):
+    P, r = comm.world_size, comm.rank
+    n = x.shape[0]
+    lo, hi = r * n // P, (r + 1) * n // P
+    return run_kmeans(comm, cfg, points=x[lo:hi], init_centroids=c0)
+
+
+def _mean_dist(x, c):
+    return torch.cdist(x.double(), c.double()).min(1).values.mean().item()
+
+
+def _lloyd(x, c, iters):
+    c = c.double().clone()
+    x = x.double()
+    for _ in range(iters):
+        lab = torch.cdist(x, c).argmin(1)
+        s = torch.zeros_like(c).index_add_(0, lab, x)
+        n = torch.bincount(lab, minlength=c.shape[0]).double()
+        m = n > 0
+        c[m] = s[m] / n[m, None]
+    return c
+
+
+@pytest.mark.parametrize("strategy", STRATEGIES)
+def test_kmeans_km_sh_gate(strategy):
+    x, c0 = _data(1000, 10, 10, 10.0, seed=3)
+    cfg = KMeansConfig(num_points=500, num_centroids=10, dim=10, iterations=100, strategy=strategy)
+    res = launch(_job, 2, args=(cfg, x, c0), timeout=300)
+    c = res[0]["centroids"]
+    assert torch.allclose(c, res[1]["centroids"], atol=1e-5)  # replicated model agrees
+    md = _mean_dist(x, c)
+    assert 7.0 < md < 7.8, md
+    ref = _lloyd(x, c0, 100)
+    assert torch.allclose(c.double(), ref, atol=1e-3), (c.double() - ref).abs().max()
+    obj = res[0]["objective"]
+    assert all(b <= a * (1 + 1e-6) for a, b in zip(obj, obj[1:]))  # Lloyd is monotone
+
+
+def test_kmeans_baseline_config1():
+    """BASELINE.json config #1: 1000 points, 10 centroids, d=100, 2 workers, gloo."""
+    x, c0 = _data(1000, 100, 10, 1000.0, seed=5)
+    cfg = KMeansConfig(num_points=500, num_centroids=10, dim=100, iterations=10, strategy="regroup_allgather")
+    res = launch(_job, 2, args=(cfg, x, c0), timeout=300)
+    ref = _lloyd(x, c0, 10)
+    assert torch.allclose(res[0]["centroids"].double(), ref, rtol=1e-4, atol=1e-2)
+
+
+def test_kmeans_single_worker_matches_multi():
+    x, c0 = _data(600, 8, 6, 10.0, seed=9)
+    cfg = KMeansConfig(num_points=600, num_centroids=6, dim=8, iterations=15, strategy="allreduce")
+    one = launch(_job, 1, args=(cfg, x, c0))[0]
+    three = launch(_job, 3, args=(cfg, x, c0), timeout=300)[0]
+    assert torch.allclose(one["centroids"], three["centroids"], atol=1e-4)

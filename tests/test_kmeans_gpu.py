@@ -1,0 +1,93 @@
+"""GPU numerics of the K-means HIP kernels vs a plain PyTorch fp32 reference of the same
+op on the same (bf16-rounded) operands. Runs only on a MI355X box."""
+import pytest
+import torch
+
+from harp_amd.ops import kmeans as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_assign(X, c_bf, d):
+    x = X[:, :d].float()
+    cn = (c_bf.double() ** 2).sum(1)
+    dist = cn[None, :] - 2.0 * (x.double() @ c_bf.double().t())
+    lab = dist.argmin(1)
+    best = dist.gather(1, lab[:, None])[:, 0]
+    return lab, dist, best + (x.double() ** 2).sum(1)
+
+
+def test_generate_points_layout(cuda):
+    X = K.generate_points(1000, 37, 2.0, 5.0, seed=3, device=cuda)
+    dp = K.padded_dim(37)
+    assert X.shape == (1000, dp) and X.dtype == torch.bfloat16
+    assert bool((X[:, 37] == 1).all()) and bool((X[:, 38:] == 0).all())
+    v = X[:, :37].float()
+    assert v.min() >= 2.0 and v.max() <= 5.0 and abs(v.mean().item() - 3.5) < 0.05
+    X2 = K.generate_points(1000, 37, 2.0, 5.0, seed=3, device=cuda)
+    assert torch.equal(X, X2)  # counter-based generator: deterministic
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000)])
+def test_assign_matches_torch(cuda, variant, n, d, k):
+    torch.manual_seed(0)
+    x = torch.rand(n, d, device=cuda) * 1000
+    X = K.pack_points(x, cuda)
+    c = torch.rand(k, d, device=cuda) * 1000
+    op = K.prepare(c, X.shape[1])
+    sums = torch.zeros((K.padded_k(k), X.shape[1]), dtype=torch.float32, device=cuda)
+    lab, obj = K.assign(X, op, sums=sums, variant=variant)
+    torch.cuda.synchronize()
+    c_bf = c.to(torch.bfloat16).float()
+    rlab, dist, rbest = _ref_assign(X, c_bf, d)
+    lab = lab.long()
+    assert int(lab.min()) >= 0 and int(lab.max()) < k
+    # near-ties may resolve differently; the chosen centroid must be (near-)optimal
+    chosen = dist.gather(1, lab[:, None])[:, 0]
+    best = dist.gather(1, rlab[:, None])[:, 0]
+    scale = (X[:, :d].double() ** 2).sum(1) + (c_bf.double() ** 2).sum(1).max()
+    assert bool(((chosen - best) <= 1e-5 * scale).all())
+    assert (lab == rlab).float().mean() > 0.99
+    assert abs(obj.item() - rbest.sum().item()) <= 1e-4 * abs(rbest.sum().item()) + 1e-3
+    # accumulated (sum x, count) rows match index_add with the kernel's own labels
+    ref = torch.zeros_like(sums, dtype=torch.float64)
+    ref[:, : d + 1].index_add_(0, lab, X[:, : d + 1].double())
+    assert torch.allclose(sums.double(), ref, rtol=1e-5, atol=1e-2)
+    assert int(sums[:, d].sum().item()) == n
+
+
+def test_prepare_and_normalize(cuda):
+    k, d = 300, 100
+    c = torch.rand(k, d, device=cuda) * 10
+    op = K.prepare(c, K.padded_dim(d))
+    c_bf = c.to(torch.bfloat16).float()
+    assert torch.equal(op.Cm2[:k, :d].float(), -2 * c_bf)
+    assert bool((op.Cm2[k:] == 0).all()) and bool((op.cn[k:] > 1e37).all())
+    assert torch.allclose(op.cn[:k], (c_bf.double() ** 2).sum(1).float(), rtol=1e-6)
+    sums = torch.rand(k, K.padded_dim(d), device=cuda) * 100
+    sums[::7, d] = 0  # empty clusters keep their centroid
+    sums[1::7, d] = 3.0
+    cn = c.clone()
+    K.normalize(sums, cn, d)
+    ref = c.clone()
+    m = sums[:, d] > 0
+    ref[m] = sums[m, :d] / sums[m, d:d + 1]
+    assert torch.allclose(cn, ref, rtol=1e-6)
+
+
+def test_kmeans_model_gpu_matches_cpu(cuda):
+    from harp_amd.models.kmeans import KMeansConfig, run_kmeans
+    from harp_amd.parallel.comm import Communicator
+
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(20000, 20, generator=g) * 10
+    c0 = torch.rand(16, 20, generator=g) * 10
+    cfg = KMeansConfig(num_points=20000, num_centroids=16, dim=20, iterations=20, strategy="allreduce")
+    gpu = run_kmeans(Communicator(None, cuda), cfg, points=x, init_centroids=c0)
+    cpu = run_kmeans(Communicator(None, torch.device("cpu")), cfg, points=x, init_centroids=c0)
+    md_g = torch.cdist(x, gpu["centroids"]).min(1).values.mean()
+    md_c = torch.cdist(x, cpu["centroids"]).min(1).values.mean()
+    assert abs(md_g - md_c) / md_c < 5e-3, (md_g, md_c)
+    obj = gpu["objective"]
+    assert obj[-1] <= obj[0]
