@@ -52,6 +52,8 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     os.makedirs(NATIVE, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h"))
+    if not force and not _stale(KERNEL_LIB, srcs + headers):
+        return KERNEL_LIB  # shipped/up-to-date library (object files need not exist)
     objs = []
     todo = []
     for s in srcs:
