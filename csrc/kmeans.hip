@@ -7,21 +7,25 @@
 // (KMeansCollectiveMapper.java:170-183).
 //
 // Design (MI355X-first, not a translation):
-//  * distances are a GEMM: X[N,dp] (bf16) x (-2C)[Kp,dp]^T on v_mfma_f32_32x32x16_bf16,
-//    with ||c||^2 loaded as the MFMA's initial accumulator (row constant), so the
-//    accumulator IS the distance minus ||x||^2 and the epilogue is a pure argmin.
+//  * distances are a GEMM: X[N,dp] (bf16) x (-2C)[Kp,dp]^T on v_mfma_f32_32x32x16_bf16.
+//    ||c||^2 is folded INTO the GEMM: X carries 1.0 in columns d..d+3 and -2C carries
+//    0, hi, mid, lo there (||c||^2 = hi + mid + lo in three bf16 terms, ~24-bit exact), so
+//    the zero-initialised accumulator IS the distance minus ||x||^2 and the epilogue is a
+//    pure argmin (no row-constant registers, no norm reads from LDS). d=100 pads to 112,
+//    the same K as without the fold.
 //  * centroids sit on the MFMA row axis, points on the lane (column) axis: each lane
 //    owns one point and 16 candidate centroids per 32x32 tile, so the argmin is
 //    register-local (16 keyed fminf -> v_min3) plus one lane<->lane+32 exchange.
 //    The within-tile register index is packed into the 4 low mantissa bits of the
 //    distance (relative perturbation 2^-19, far below the bf16 operand rounding).
 //  * X fragments stay in VGPRs for the whole centroid sweep; centroid tiles stream
-//    through double-buffered LDS (row pitch = odd number of 16-B slots -> ds_read_b128
-//    conflict-free), one barrier per stage; next tile's global loads are issued
-//    before the MFMA block and written to LDS after it (async-STAGE split).
-//  * the padding column d of X holds 1.0 and the matching column of -2C holds 0,
-//    so the accumulation adds (x, 1) = (partial sum, count) in one row: the Harp
-//    centroid row layout (sum + count) falls out of the data layout.
+//    through double-buffered LDS filled by global_load_lds (LDS-DMA, no staging VGPRs)
+//    with a per-row chunk rotation applied to the DMA source so ds_read_b128 stays
+//    conflict-free; A fragments are register double-buffered across 32-row groups; one
+//    barrier per stage.
+//  * column d of X (1.0) meets column d of -2C (0): the accumulation adds (x, 1) =
+//    (partial sum, count) in one row: the Harp centroid row layout (sum + count) falls out
+//    of the data layout.
 //  * accumulation: per assigned point, one 256-B contiguous f32 atomic row segment
 //    per wave-instruction (the full-rate atomic shape on gfx950).
 #include "common.h"
@@ -29,62 +33,59 @@
 namespace {
 
 constexpr float KM_BIG = 1.0e38f;
+constexpr int KM_ONES = 4;  // X columns d..d+3 hold 1.0: count + the 3 folded ||c||^2 terms
 
 __device__ __forceinline__ float keyed(float v, unsigned idx) {
   return __uint_as_float((__float_as_uint(v) & ~0xFu) | idx);
 }
 
-template <int KS, int G, int WAVES, int RG>
+template <int KS, int G, int WAVES_, int RG>
 struct KMCfg {
   static constexpr int DP = KS * 16;                 // padded feature dim (elements)
-  static constexpr int LROW = DP + 8;                // LDS row pitch (elements): (2KS+1) 16-B slots
+  static constexpr int CPR = KS * 2;                 // 16-byte chunks per row
   static constexpr int TILE = RG * 32;               // centroids per stage
-  static constexpr int THREADS = WAVES * 64;
-  static constexpr int CHUNKS = TILE * KS * 2;       // 16-byte chunks per centroid tile
-  static constexpr int CPT = (CHUNKS + THREADS - 1) / THREADS;
-  static constexpr int A_BYTES = TILE * LROW * 2;
-  static constexpr int STAGE_BYTES = A_BYTES + TILE * 4;
-  static constexpr int PTS = WAVES * G * 32;         // points per workgroup
+  static constexpr int WAVES = WAVES_;
+  static constexpr int THREADS = WAVES_ * 64;
+  static constexpr int TILE_BYTES = TILE * DP * 2;
+  static constexpr int DMA_INSTR = TILE * CPR / 64;  // 1-KiB LDS-DMA wave-instructions per tile
+  static constexpr int PTS = WAVES_ * G * 32;        // points per workgroup
+  static_assert((TILE * CPR) % 64 == 0, "tile must be whole 1-KiB DMA pieces");
 };
 
+// LDS image of a centroid tile: row-major [TILE][CPR] 16-B chunks, chunk c of row r stored at
+// position (c + s(r)) mod CPR with s(r) = (r >> 3) & 1. Rows r and r+8 then sit on different
+// 16-B bank slots, so every ds_read_b128 lane group (16 distinct rows) is conflict-free, while
+// the image stays lane-linear for global_load_lds (the swizzle is applied to the SOURCE).
 template <class C>
-__device__ __forceinline__ void stage_load(const bf16x8* __restrict__ cm2, const float* __restrict__ cn,
-                                           int tile, bf16x8 (&regs)[C::CPT], float& cnv) {
-  const int tid = threadIdx.x;
-  const bf16x8* base = cm2 + (size_t)tile * C::CHUNKS;
+__device__ __forceinline__ void stage_dma(const __bf16* __restrict__ cm2, int tile, char* lds, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < C::CPT; ++i) {
-    const int ch = tid + i * C::THREADS;
-    if (C::CHUNKS % C::THREADS == 0 || ch < C::CHUNKS) regs[i] = base[ch];
-  }
-  if (tid < C::TILE) cnv = cn[tile * C::TILE + tid];
-}
-
-template <class C>
-__device__ __forceinline__ void stage_store(char* buf, const bf16x8 (&regs)[C::CPT], float cnv) {
-  const int tid = threadIdx.x;
-  constexpr int CPR = C::DP / 8;  // chunks per row
-#pragma unroll
-  for (int i = 0; i < C::CPT; ++i) {
-    const int ch = tid + i * C::THREADS;
-    if (C::CHUNKS % C::THREADS == 0 || ch < C::CHUNKS) {
-      const int row = ch / CPR, c = ch - row * CPR;
-      *(bf16x8*)(buf + (row * C::LROW + c * 8) * 2) = regs[i];
+  for (int j0 = 0; j0 < C::DMA_INSTR; j0 += C::WAVES) {
+    const int j = j0 + wave;
+    if (C::DMA_INSTR % C::WAVES == 0 || j < C::DMA_INSTR) {
+      const int q = j * 64 + lane;
+      const int row = q / C::CPR;
+      int c = q - row * C::CPR - ((row >> 3) & 1);
+      if (c < 0) c += C::CPR;
+      const __bf16* src = cm2 + ((size_t)tile * C::TILE + row) * C::DP + c * 8;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
     }
   }
-  if (tid < C::TILE) ((float*)(buf + C::A_BYTES))[tid] = cnv;
 }
 
 template <int KS, int G, int WAVES, int RG>
 __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
-    const __bf16* __restrict__ X, const __bf16* __restrict__ Cm2, const float* __restrict__ cn,
-    long N, int ntiles, int dcount, int* __restrict__ labels, float* __restrict__ mindist,
-    float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial) {
+    const __bf16* __restrict__ X, const __bf16* __restrict__ Cm2, long N, int ntiles, int dcount,
+    int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial) {
   using C = KMCfg<KS, G, WAVES, RG>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * C::STAGE_BYTES + WAVES * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::TILE_BYTES + WAVES * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  const int srot = (r >> 3) & 1;
   const long pbase = ((long)blockIdx.x * WAVES + wave) * (G * 32);
+
+  // kick off the first centroid tile before loading this wave's points
+  stage_dma<C>(Cm2, 0, smem, wave, lane);
 
   // ---- this wave's points: B-operand fragments, resident for the whole sweep
   bf16x8 xf[G][KS];
@@ -102,50 +103,49 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
 #pragma unroll
   for (int g = 0; g < G; ++g) { best[g] = KM_BIG; bestt[g] = 0; }
 
-  bf16x8 sreg[C::CPT];
-  float scn = 0.f;
-  stage_load<C>((const bf16x8*)Cm2, cn, 0, sreg, scn);
-  stage_store<C>(smem, sreg, scn);
+  // per-lane byte offsets of its A-fragment chunks inside a 32-row group
+  int aoff[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    int cp = 2 * s + h + srot;
+    if (cp >= C::CPR) cp -= C::CPR;
+    aoff[s] = (r * C::CPR + cp) * 16;
+  }
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
-    const bool more = (t + 1) < ntiles;
-    if (more) stage_load<C>((const bf16x8*)Cm2, cn, t + 1, sreg, scn);
-    const char* buf = smem + (t & 1) * C::STAGE_BYTES;
-    const float* cnt = (const float*)(buf + C::A_BYTES);
+    if (t + 1 < ntiles) stage_dma<C>(Cm2, t + 1, smem + ((t + 1) & 1) * C::TILE_BYTES, wave, lane);
+    const char* buf = smem + (t & 1) * C::TILE_BYTES;
+    bf16x8 af[2][KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[0][s] = *(const bf16x8*)(buf + aoff[s]);
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg) {
-      bf16x8 af[KS];
-      const __bf16* arow = (const __bf16*)buf + (rg * 32 + r) * C::LROW + 8 * h;
+      if (rg + 1 < RG) {
+        const char* nb = buf + (rg + 1) * 32 * C::CPR * 16;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) af[s] = *(const bf16x8*)(arow + 16 * s);
-      floatx16 ci;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const floatx4 v = *(const floatx4*)(cnt + rg * 32 + 8 * q + 4 * h);
-        ci[4 * q + 0] = v[0];
-        ci[4 * q + 1] = v[1];
-        ci[4 * q + 2] = v[2];
-        ci[4 * q + 3] = v[3];
+        for (int s = 0; s < KS; ++s) af[(rg + 1) & 1][s] = *(const bf16x8*)(nb + aoff[s]);
       }
       const int tg = t * RG + rg;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        floatx16 acc = ci;
+        floatx16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], xf[g][s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][s], xf[g][s], acc, 0, 0, 0);
         float m = keyed(acc[0], 0u);
 #pragma unroll
         for (int i = 1; i < 16; ++i) m = fminf(m, keyed(acc[i], (unsigned)i));
         if (m < best[g]) { best[g] = m; bestt[g] = tg; }
       }
     }
-    if (more) stage_store<C>(smem + ((t + 1) & 1) * C::STAGE_BYTES, sreg, scn);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // ---- resolve argmin across the two lane halves, write labels / distances
+  // ---- resolve argmin across the two lane halves, write labels / objective partials
   int lab[G];
   float local_obj = 0.f;
 #pragma unroll
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
         xs = fmaf(v, v, xs);
       }
     xs += __shfl_xor(xs, 32, 64);
-    xs -= 1.0f;  // the count column of X holds 1.0
+    xs -= (float)KM_ONES;  // the 1.0 columns of X
     const float ob = __shfl_xor(best[g], 32, 64);
     const int obt = __shfl_xor(bestt[g], 32, 64);
     const bool take = h ? (ob <= best[g]) : (ob < best[g]);
@@ -170,23 +170,21 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     const int idx = bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
     lab[g] = idx;
     const long p = pbase + g * 32 + r;
-    const float dist = fmaxf(bv + xs, 0.f);
     if (h == 0 && p < N) {
       labels[p] = idx;
-      if (mindist) mindist[p] = dist;
-      local_obj += dist;
+      local_obj += fmaxf(bv + xs, 0.f);
     }
   }
   if (obj_partial) {
     local_obj = wave_sum(local_obj);
-    float* red = (float*)(smem + 2 * C::STAGE_BYTES);
+    float* red = (float*)(smem + 2 * C::TILE_BYTES);
     if (lane == 0) red[wave] = local_obj;
     __syncthreads();
     if (tid == 0) {
-      float s = 0.f;
+      float acc = 0.f;
 #pragma unroll
-      for (int w = 0; w < WAVES; ++w) s += red[w];
-      obj_partial[blockIdx.x] = s;
+      for (int w = 0; w < WAVES; ++w) acc += red[w];
+      obj_partial[blockIdx.x] = acc;
     }
   }
 
@@ -220,23 +218,35 @@ __global__ void kmeans_normalize_kernel(const float* __restrict__ sums, int ld, 
   }
 }
 
-// c[K][d] fp32 -> Cm2[Kp][dp] = -2*bf16(c) (cols >= d zero), cn[Kp] = ||bf16(c)||^2 (pad rows: +BIG)
+// c[K][d] fp32 -> Cm2[Kp][dp]: cols [0,d) = -2*bf16(c), col d = 0 (count column of X),
+// cols d+1..d+3 = ||bf16(c)||^2 split into three bf16 terms (hi + mid + lo ~ 24-bit exact),
+// rest 0; cn[Kp] = ||bf16(c)||^2 in fp32. Padding rows: distance +BIG.
 __global__ void kmeans_prepare_kernel(const float* __restrict__ c, int K, int d, int Kp, int dp,
                                       __bf16* __restrict__ Cm2, float* __restrict__ cn) {
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= Kp) return;
   float s = 0.f;
-  for (int j = lane; j < dp; j += 64) {
-    float v = 0.f;
-    if (row < K && j < d) v = c[(long)row * d + j];
-    const __bf16 b = (__bf16)v;
-    const float bf = (float)b;
+  for (int j = lane; j < d; j += 64) {
+    float v = row < K ? c[(long)row * d + j] : 0.f;
+    const float bf = (float)(__bf16)v;
     s = fmaf(bf, bf, s);
     Cm2[(long)row * dp + j] = (__bf16)(-2.0f * bf);
   }
   s = wave_sum(s);
-  if (lane == 0) cn[row] = row < K ? s : KM_BIG;
+  if (row >= K) s = KM_BIG;
+  const __bf16 hi = (__bf16)s;
+  const float r1 = s - (float)hi;
+  const __bf16 mid = (__bf16)r1;
+  const __bf16 lo = (__bf16)(r1 - (float)mid);
+  for (int j = d + lane; j < dp; j += 64) {
+    __bf16 v = (__bf16)0.f;
+    if (j == d + 1) v = hi;
+    else if (j == d + 2) v = mid;
+    else if (j == d + 3) v = lo;
+    Cm2[(long)row * dp + j] = v;
+  }
+  if (lane == 0) cn[row] = s;
 }
 
 // Counter-based uniform generator (splitmix64 of the element index): device-side
@@ -258,7 +268,7 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
     if (col < d) {
       const unsigned long long z = splitmix64(seed ^ ((unsigned long long)(row0 + row) * 0x100000001B3ull + col));
       v = lo + (hi - lo) * (float)((z >> 40) * (1.0 / 16777216.0));
-    } else if (one_col && col == d) {
+    } else if (one_col && col < d + KM_ONES) {
       v = 1.0f;
     }
     X[i] = (__bf16)v;
@@ -266,43 +276,43 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
 }
 
 template <int KS, int G, int WAVES, int RG>
-int launch_assign(const void* X, const void* Cm2, const float* cn, long N, int Kp, int d, int* labels,
-                  float* mindist, float* sums, int ld_sums, float* obj_partial, hipStream_t stream) {
+int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* labels, float* sums, int ld_sums,
+                  float* obj_partial, hipStream_t stream) {
   using C = KMCfg<KS, G, WAVES, RG>;
   if (Kp % C::TILE) return HARP_EBADARG;
   const long nblk = (N + C::PTS - 1) / C::PTS;
   kmeans_assign_kernel<KS, G, WAVES, RG><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
-      (const __bf16*)X, (const __bf16*)Cm2, cn, N, Kp / C::TILE, d, labels, mindist, sums, ld_sums,
-      obj_partial);
+      (const __bf16*)X, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial);
   return harp_launch_status();
 }
 
 // variant -> (G, WAVES, RG). Kp must be a multiple of 128 for every variant.
-#define KM_VARIANTS(KS)                                                                              \
-  switch (variant) {                                                                               \
-    case 0: return launch_assign<KS, 2, 4, 2>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
-    case 1: return launch_assign<KS, 4, 4, 2>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
-    case 2: return launch_assign<KS, 2, 8, 2>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
-    case 3: return launch_assign<KS, 2, 4, 4>(X, Cm2, cn, N, Kp, d, labels, mindist, sums, ld, op, s); \
-    default: return HARP_EBADARG;                                                                  \
+#define KM_VARIANTS(KS)                                                                       \
+  switch (variant) {                                                                        \
+    case 0: return launch_assign<KS, 2, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
+    case 1: return launch_assign<KS, 2, 8, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
+    case 2: return launch_assign<KS, 2, 4, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
+    case 3: return launch_assign<KS, 3, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
+    case 4: return launch_assign<KS, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s); \
+    default: return HARP_EBADARG;                                                           \
   }
 
 }  // namespace
 
 HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
   switch (variant) {
-    case 0: return 4 * 2 * 32;
-    case 1: return 4 * 4 * 32;
-    case 2: return 8 * 2 * 32;
-    case 3: return 4 * 2 * 32;
+    case 0: return 8 * 2 * 32;
+    case 1: return 8 * 2 * 32;
+    case 2: return 4 * 2 * 32;
+    case 3: return 8 * 3 * 32;
+    case 4: return 16 * 1 * 32;
     default: return -1;
   }
 }
 
-HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, const float* cn, long N, int dp, int Kp,
-                                   int d, int* labels, float* mindist, float* sums, int ld, float* op,
-                                   int variant, hipStream_t s) {
-  if (N <= 0 || d + 1 > dp || dp % 16 || Kp <= 0 || Kp % 128) return HARP_EBADARG;
+HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, long N, int dp, int Kp, int d, int* labels,
+                                   float* sums, int ld, float* op, int variant, hipStream_t s) {
+  if (N <= 0 || d + KM_ONES > dp || dp % 16 || Kp <= 0 || Kp % 128) return HARP_EBADARG;
   switch (dp / 16) {
     case 1: KM_VARIANTS(1)
     case 2: KM_VARIANTS(2)

@@ -4,11 +4,13 @@ GPU tensors run the gfx950 kernels in ``csrc/kmeans.hip``; CPU tensors run the P
 fp32 reference of the same op (also the numerics oracle in the GPU tests).
 
 Layouts (chosen for the MFMA kernel):
-  * points  ``X  [n, dp]`` bf16 (GPU) / fp32 (CPU), ``dp = round_up(d + 1, 16)``;
-    column ``d`` holds 1.0 so the accumulated row carries the count, columns > d are 0;
+  * points  ``X  [n, dp]`` bf16 (GPU) / fp32 (CPU), ``dp = round_up(d + 4, 16)``;
+    columns ``d..d+3`` hold 1.0 (column d makes the accumulated row carry the count,
+    d+1..d+3 pick up the three bf16 terms of ||c||^2 folded into the GEMM), rest 0;
   * centroids (master copy) ``c [K, d]`` fp32;
-  * kernel operand ``Cm2 [Kp, dp]`` bf16 = -2*bf16(c) and ``cn [Kp]`` = ||bf16(c)||^2,
-    padded to ``Kp = round_up(K, 128)`` rows that can never win (cn = 1e38);
+  * kernel operand ``Cm2 [Kp, dp]`` bf16: cols [0,d) = -2*bf16(c), col d = 0, cols
+    d+1..d+3 = hi/mid/lo bf16 split of ||bf16(c)||^2; ``cn [Kp]`` the same norm in fp32;
+    padded to ``Kp = round_up(K, 128)`` rows that can never win (norm = 1e38);
   * partial sums ``S [K, dp]`` fp32: columns ``0..d-1`` = sum of x, column ``d`` = count
     — the reference's centroid row (count + d values,
     KMeansCollectiveMapper.java:213-237) in a device-friendly order.
@@ -24,11 +26,12 @@ import torch
 from . import _lib
 
 KP_ALIGN = 128
-DEFAULT_VARIANT = 2
+ONES = 4  # X columns d..d+3 hold 1.0
+DEFAULT_VARIANT = 0
 
 
 def padded_dim(d: int) -> int:
-    return max(16, (d + 1 + 15) // 16 * 16)
+    return (d + ONES + 15) // 16 * 16
 
 
 def padded_k(k: int) -> int:
@@ -43,7 +46,7 @@ def pack_points(x: torch.Tensor, device: torch.device | str | None = None) -> to
     dt = torch.bfloat16 if device.type == "cuda" else torch.float32
     out = torch.zeros((n, dp), dtype=dt, device=device)
     out[:, :d] = x.to(device=device, dtype=dt)
-    out[:, d] = 1.0
+    out[:, d:d + ONES] = 1.0
     return out
 
 
@@ -116,8 +119,8 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             assert sums.shape[0] >= op.Cm2.shape[0], "sums needs Kp (padded) rows"
             assert sums.device == dev
         assert X.dtype == torch.bfloat16 and X.is_contiguous() and op.Cm2.shape[1] == dp
-        st = lib.harp_kmeans_assign(X.data_ptr(), op.Cm2.data_ptr(), op.cn.data_ptr(), n, dp, op.Cm2.shape[0], op.d,
-                                    labels.data_ptr(), None, _lib.ptr(sums), sums.stride(0) if sums is not None else 0,
+        st = lib.harp_kmeans_assign(X.data_ptr(), op.Cm2.data_ptr(), n, dp, op.Cm2.shape[0], op.d,
+                                    labels.data_ptr(), _lib.ptr(sums), sums.stride(0) if sums is not None else 0,
                                     _lib.ptr(obj_partial) if want_objective else None, variant, _lib.stream_ptr(dev))
         _lib.check(st, "kmeans_assign")
         obj = obj_partial[:nblk].double().sum() if want_objective else None

@@ -21,14 +21,14 @@ def test_generate_points_layout(cuda):
     X = K.generate_points(1000, 37, 2.0, 5.0, seed=3, device=cuda)
     dp = K.padded_dim(37)
     assert X.shape == (1000, dp) and X.dtype == torch.bfloat16
-    assert bool((X[:, 37] == 1).all()) and bool((X[:, 38:] == 0).all())
+    assert bool((X[:, 37:41] == 1).all()) and bool((X[:, 41:] == 0).all())
     v = X[:, :37].float()
     assert v.min() >= 2.0 and v.max() <= 5.0 and abs(v.mean().item() - 3.5) < 0.05
     X2 = K.generate_points(1000, 37, 2.0, 5.0, seed=3, device=cuda)
     assert torch.equal(X, X2)  # counter-based generator: deterministic
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000)])
 def test_assign_matches_torch(cuda, variant, n, d, k):
     torch.manual_seed(0)
@@ -63,7 +63,10 @@ def test_prepare_and_normalize(cuda):
     op = K.prepare(c, K.padded_dim(d))
     c_bf = c.to(torch.bfloat16).float()
     assert torch.equal(op.Cm2[:k, :d].float(), -2 * c_bf)
-    assert bool((op.Cm2[k:] == 0).all()) and bool((op.cn[k:] > 1e37).all())
+    assert bool((op.Cm2[k:, :d] == 0).all()) and bool((op.cn[k:] > 1e37).all())
+    folded = op.Cm2[:k, d + 1:d + 4].double().sum(1)  # hi + mid + lo == ||c||^2 (~24 bits)
+    assert torch.allclose(folded, op.cn[:k].double(), rtol=1e-6)
+    assert bool((op.Cm2[:, d] == 0).all()) and bool((op.Cm2[:, d + 4:] == 0).all())
     assert torch.allclose(op.cn[:k], (c_bf.double() ** 2).sum(1).float(), rtol=1e-6)
     sums = torch.rand(k, K.padded_dim(d), device=cuda) * 100
     sums[::7, d] = 0  # empty clusters keep their centroid
