@@ -322,6 +322,10 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, long N, int d
     case 6: KM_VARIANTS(6)
     case 7: KM_VARIANTS(7)
     case 8: KM_VARIANTS(8)
+    // wide rows: one 32-point group per wave keeps the X fragments within budget
+#define KM_WIDE(KSV) case KSV: return launch_assign<KSV, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);
+    KM_WIDE(9) KM_WIDE(10) KM_WIDE(11) KM_WIDE(12) KM_WIDE(13) KM_WIDE(14) KM_WIDE(15) KM_WIDE(16)
+#undef KM_WIDE
     default: return HARP_EUNSUPPORTED;
   }
 }

@@ -108,6 +108,10 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
         labels = torch.empty(n, dtype=torch.int32, device=dev)
     if _lib.use_native(X):
         lib = _lib.kernels()
+        if dp > 256:
+            raise NotImplementedError(f"native K-means supports d <= {256 - ONES} (got d={op.d})")
+        if dp > 128:
+            variant = 4  # the only instantiation for 9..16 k-steps
         ppb = lib.harp_kmeans_points_per_block(variant)
         if ppb <= 0:
             raise ValueError(f"unknown kmeans kernel variant {variant}")

@@ -29,7 +29,7 @@ def test_generate_points_layout(cuda):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000)])
+@pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000), (1500, 250, 200)])
 def test_assign_matches_torch(cuda, variant, n, d, k):
     torch.manual_seed(0)
     x = torch.rand(n, d, device=cuda) * 1000
