@@ -1,0 +1,234 @@
+"""MF-SGD with model rotation (Harp's second headline workload).
+
+Reference: ml/java/.../sgd/SGDCollectiveMapper.java:183-326 — W (user factors) is
+row-partitioned and stays local (ratings are regrouped by a random row owner, :384); H
+(item factors) is column-partitioned into ``P x numModelSlices`` slices (numModelSlices =
+2, :120) that rotate around the workers (dymoro Rotator); per iteration, P steps x 2
+slices of {compute on slice k, rotate slice k}; test RMSE every 5 iterations with an
+allreduce of (SSE, count) (:670-735). Update rule SGDMPTask.java:46-77.
+
+MI355X design: ratings on each worker are bucketed once by H slice and sorted by user;
+each (user-block x resident slice) pass is one HIP kernel (``ops.mf.sgd_update``); the
+two slices of a worker rotate on two private RCCL channels so slice k's transfer
+overlaps the kernel on slice k+1 (:class:`~harp_amd.runtime.dymoro.DeviceRotator`);
+no host synchronisation inside an epoch.
+"""
+from __future__ import annotations
+
+import math
+import random
+import time
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+
+from ..ops import mf as MF
+from ..runtime.dymoro import DeviceRotator, RotationSchedule, create_rotation_order, get_rotation_sequences
+from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
+
+
+@dataclass
+class SGDConfig:
+    rank: int = 128            # r
+    lam: float = 0.05          # lambda
+    lr: float = 0.002          # epsilon
+    epochs: int = 10
+    num_slices: int = 2        # model slices per worker (numModelSlices)
+    chunk: int = 64            # ratings per GPU update stream
+    random_order: bool = False  # random rotation orders (RotationUtil) vs ring
+    test_every: int = 5        # rmseIteInterval
+    seed: int = 0
+    init_scale: float = -1.0   # <0: sqrt(mean_rating / r) (E[w.h] = mean rating)
+
+
+def load_mm(path: str) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Read ``row col value`` text (Matrix Market body, optionally .bz2), 1-based ids."""
+    import bz2
+    import numpy as np
+
+    opener = bz2.open if path.endswith(".bz2") else open
+    with opener(path, "rt") as f:
+        lines = [ln for ln in f if ln.strip() and not ln.startswith("%")]
+    arr = np.loadtxt(lines, dtype=np.float64, ndmin=2)
+    return (torch.from_numpy(arr[:, 0].astype("int64") - 1), torch.from_numpy(arr[:, 1].astype("int64") - 1),
+            torch.from_numpy(arr[:, 2].astype("float32")))
+
+
+def synthetic_ratings(n_users: int, n_items: int, n_ratings: int, seed: int = 0, device="cpu", true_rank: int = 8):
+    """Netflix-shaped synthetic ratings: uniform users, Zipf-like item popularity, values
+    from a hidden rank-``true_rank`` model + noise clipped to [1, 5]."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    u = torch.randint(0, n_users, (n_ratings,), generator=g, device=device)
+    pop = torch.rand(n_ratings, generator=g, device=device) ** 2.0
+    perm = torch.randperm(n_items, generator=g, device=device)
+    it = perm[(pop * n_items).long().clamp_max(n_items - 1)]
+    Ut = torch.randn((n_users, true_rank), generator=g, device=device) / math.sqrt(true_rank)
+    Vt = torch.randn((n_items, true_rank), generator=g, device=device) / math.sqrt(true_rank)
+    val = torch.empty(n_ratings, device=device)
+    step = 1 << 24
+    for s in range(0, n_ratings, step):
+        e = min(s + step, n_ratings)
+        val[s:e] = (3.6 + (Ut[u[s:e]] * Vt[it[s:e]]).sum(1) + 0.3 * torch.randn(e - s, generator=g, device=device))
+    return u, it, val.clamp_(1.0, 5.0)
+
+
+class _Buckets:
+    """Ratings of this worker bucketed by global H slice, user-sorted inside a bucket."""
+
+    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device):
+        g = slice_of_item[cols]
+        key = g * (int(rows.max().item()) + 1 if rows.numel() else 1) + rows
+        order = torch.argsort(key)
+        self.rows = rows[order].to(torch.int32).contiguous().to(device)
+        self.cols = local_of_item[cols[order]].to(torch.int32).contiguous().to(device)
+        self.vals = vals[order].to(torch.float32).contiguous().to(device)
+        counts = torch.bincount(g, minlength=n_slices).cpu()
+        self.offsets = [0] + torch.cumsum(counts, 0).tolist()
+        self.n = rows.numel()
+
+    def get(self, s: int):
+        a, b = self.offsets[s], self.offsets[s + 1]
+        return self.rows[a:b], self.cols[a:b], self.vals[a:b]
+
+
+class SGDCollectiveMapper(CollectiveMapper):
+    def __init__(self, comm=None, config: Optional[SGDConfig] = None, n_users: int = 0, n_items: int = 0,
+                 train=None, test=None, metrics=None):
+        super().__init__(comm, metrics)
+        self.cfg = config or SGDConfig()
+        self.n_users, self.n_items = n_users, n_items
+        self._train, self._test = train, test
+        self.rmse_history: List[Tuple[int, float, float]] = []
+        self.epoch_times: List[float] = []
+
+    # -- partitioning -------------------------------------------------------------------
+    def _owner(self, users: torch.Tensor) -> torch.Tensor:
+        # random-but-shared row owner (RandomPartitioner seeded from an allreduced seed)
+        P = self.get_num_workers()
+        h = (users * 2654435761 + self.cfg.seed) % 4294967296
+        return h % P
+
+    def init_model(self, reader: KeyValReader) -> None:
+        cfg = self.cfg
+        P, me, dev = self.get_num_workers(), self.get_self_id(), self.device
+        S = cfg.num_slices
+        n_slices = P * S
+        u, i, v = self._train
+        mine = self._owner(u) == me
+        u, i, v = u[mine], i[mine], v[mine]
+        # local dense user index
+        self.users = torch.unique(self._all_users_of(me))
+        lut = torch.full((self.n_users,), -1, dtype=torch.int64, device=u.device)
+        lut[self.users.to(u.device)] = torch.arange(self.users.numel(), device=u.device)
+        rows = lut[u]
+        # item -> (slice, local index): seeded permutation, equal slice sizes
+        g = torch.Generator().manual_seed(cfg.seed + 12345)
+        perm = torch.randperm(self.n_items, generator=g)
+        self.ips = math.ceil(self.n_items / n_slices)
+        pos = torch.empty(self.n_items, dtype=torch.int64)
+        pos[perm] = torch.arange(self.n_items)
+        self.slice_of_item = (pos // self.ips).to(u.device)
+        self.local_of_item = (pos % self.ips).to(u.device)
+        self.item_perm = perm  # slice s holds items perm[s*ips:(s+1)*ips]
+        self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev)
+        if self._test is not None:
+            tu, ti, tv = self._test
+            m = self._owner(tu) == me
+            tr = lut[tu[m]]
+            ok = tr >= 0  # test users never seen in training are skipped (no W row)
+            self.test = _Buckets(tr[ok], ti[m][ok], tv[m][ok], self.slice_of_item, self.local_of_item, n_slices, dev)
+        else:
+            self.test = None
+        # model: W local, H slices of the blocks initially placed here
+        r = cfg.rank
+        mean = float(v.mean().item()) if v.numel() else 3.0
+        tot = torch.tensor([mean * v.numel(), float(v.numel())], dtype=torch.float64, device=dev)
+        if P > 1:
+            self.comm.all_reduce(tot)
+        mean = float(tot[0] / max(tot[1], 1))
+        scale = cfg.init_scale if cfg.init_scale > 0 else math.sqrt(mean / r)
+        gw = torch.Generator().manual_seed(cfg.seed * 31 + 7 + me)
+        self.W = (torch.rand((self.users.numel(), r), generator=gw) * 2 * scale).to(dev)
+        orders = get_rotation_sequences(self, cfg.epochs + 2, cfg.seed) if cfg.random_order else None
+        self.schedule = RotationSchedule(P, orders)
+        block = self.schedule.block_at(me, 0, 0)
+        slabs = []
+        for k in range(S):
+            gs = block * S + k
+            gh = torch.Generator().manual_seed(cfg.seed * 1009 + gs)
+            slabs.append((torch.rand((self.ips, r), generator=gh) * 2 * scale).to(dev))
+        self.rot = DeviceRotator(self.comm, slabs, name="sgd-h")
+        self.trained = 0
+
+    def _all_users_of(self, me: int) -> torch.Tensor:
+        allu = torch.arange(self.n_users, device=self._train[0].device)
+        return allu[self._owner(allu) == me]
+
+    # -- training -------------------------------------------------------------------------
+    def train_epoch(self, epoch: int, evaluate: bool = False) -> int:
+        cfg = self.cfg
+        P, me = self.get_num_workers(), self.get_self_id()
+        S = cfg.num_slices
+        n = 0
+        timer = self.metrics.timer
+        for s in range(P):
+            block = self.schedule.block_at(me, epoch, s)
+            for k in range(S):
+                slab = self.rot.get(k)
+                gs = block * S + k
+                with timer.phase("compute"):
+                    n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
+                with timer.phase("rotate"):
+                    self.rot.start(k, self.schedule.rotation_map(epoch, s))
+        self.trained += n
+        return n
+
+    def map_collective(self, reader: KeyValReader, context: Context) -> None:
+        self.init_model(reader)
+        for ep in range(self.cfg.epochs):
+            t0 = time.perf_counter()
+            self.train_epoch(ep)
+            self.rot.wait_all()
+            if torch.cuda.is_available() and self.device.type == "cuda":
+                torch.cuda.synchronize()
+            self.epoch_times.append(time.perf_counter() - t0)
+            if self.cfg.test_every and ((ep + 1) % self.cfg.test_every == 0 or ep == self.cfg.epochs - 1):
+                self.rmse_history.append((ep + 1, *self._eval_ring(ep)))
+        self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained}
+
+    def _eval_ring(self, epoch: int) -> Tuple[float, float]:
+        """RMSE with a ring tour (P steps, every slice visits every worker, slices end where
+        they started, so the training schedule is unaffected)."""
+        P, me, S = self.get_num_workers(), self.get_self_id(), self.cfg.num_slices
+        dev = self.device
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        start = self.schedule.placement(epoch + 1, 0)  # placement the next epoch starts from
+        ring = [(w + 1) % P for w in range(P)]
+        for s in range(P):
+            # block held by me after s ring steps from `start`
+            holder = [(start[i] + s) % P for i in range(P)]
+            block = holder.index(me)
+            for k in range(S):
+                slab = self.rot.get(k)
+                gs = block * S + k
+                tr = self.train.get(gs)
+                acc[0] += MF.sse(*tr, self.W, slab)
+                acc[1] += tr[0].numel()
+                if self.test is not None:
+                    te = self.test.get(gs)
+                    acc[2] += MF.sse(*te, self.W, slab)
+                    acc[3] += te[0].numel()
+                if P > 1:
+                    self.rot.start(k, ring)
+        self.rot.wait_all()
+        if P > 1:
+            self.comm.all_reduce(acc)
+        a = acc.cpu().tolist()
+        return math.sqrt(a[0] / max(a[1], 1)), (math.sqrt(a[2] / a[3]) if a[3] else float("nan"))
+
+
+def run_sgd(comm, cfg: SGDConfig, n_users: int, n_items: int, train, test=None) -> dict:
+    m = SGDCollectiveMapper(comm, cfg, n_users, n_items, train, test)
+    m.run(KeyValReader([]))
+    return m.result

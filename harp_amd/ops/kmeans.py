@@ -27,7 +27,7 @@ from . import _lib
 
 KP_ALIGN = 128
 ONES = 4  # X columns d..d+3 hold 1.0
-DEFAULT_VARIANT = 0
+DEFAULT_VARIANT = 1
 
 
 def padded_dim(d: int) -> int:

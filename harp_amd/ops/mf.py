@@ -1,0 +1,88 @@
+"""Matrix-factorisation device ops (SGD update, squared-error sum).
+
+GPU: ``csrc/mf_sgd.hip`` (subgroup-per-stream Hogwild SGD over user-sorted ratings).
+CPU: the native sequential loop in ``csrc/host/mf_cpu.cpp`` (exact reference order).
+Ratings are three parallel arrays ``rows`` (local user index, int32), ``cols`` (item index
+within the resident H slice, int32), ``vals`` (float32).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+SUPPORTED_RANKS = (16, 32, 48, 64, 128, 256)
+
+_lib.register({
+    "harp_mf_sgd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
+                    _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_void_p],
+    "harp_mf_rmse_blocks": [],
+    "harp_mf_rmse": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int,
+                     _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
+})
+
+
+def _rt():
+    rt = _lib.runtime()
+    if rt is None:
+        raise _lib.NativeUnavailable("libharp_runtime.so not built (python -m harp_amd.ops.build)")
+    if not getattr(rt, "_mf_bound", False):
+        rt.harp_mf_sgd_cpu.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
+                                       ctypes.c_float]
+        rt.harp_mf_sgd_cpu.restype = None
+        rt.harp_mf_sse_cpu.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        rt.harp_mf_sse_cpu.restype = ctypes.c_double
+        rt._mf_bound = True
+    return rt
+
+
+def _check(rows, cols, vals, W, H):
+    assert rows.dtype == torch.int32 and cols.dtype == torch.int32 and vals.dtype == torch.float32
+    assert rows.is_contiguous() and cols.is_contiguous() and vals.is_contiguous()
+    assert W.dtype == torch.float32 and H.dtype == torch.float32 and W.stride(1) == 1 and H.stride(1) == 1
+    assert W.shape[1] == H.shape[1]
+
+
+def sgd_update(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: torch.Tensor, H: torch.Tensor,
+               lr: float, lam: float, chunk: int = 64) -> int:
+    """One pass of SGD over the given ratings, updating W and H in place. Returns n."""
+    _check(rows, cols, vals, W, H)
+    n = rows.numel()
+    if n == 0:
+        return 0
+    r = W.shape[1]
+    if _lib.use_native(W):
+        if r not in SUPPORTED_RANKS:
+            raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS}, got {r}")
+        st = _lib.kernels().harp_mf_sgd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, chunk, W.data_ptr(),
+                                        W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam),
+                                        _lib.stream_ptr(W.device))
+        _lib.check(st, "mf_sgd")
+        return n
+    _rt().harp_mf_sgd_cpu(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, W.data_ptr(), W.stride(0),
+                          H.data_ptr(), H.stride(0), float(lr), float(lam))
+    return n
+
+
+def sse(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: torch.Tensor, H: torch.Tensor):
+    """Sum of squared errors (0-dim float64 tensor on W's device)."""
+    _check(rows, cols, vals, W, H)
+    n = rows.numel()
+    if n == 0:
+        return torch.zeros((), dtype=torch.float64, device=W.device)
+    r = W.shape[1]
+    if _lib.use_native(W):
+        lib = _lib.kernels()
+        nb = lib.harp_mf_rmse_blocks()
+        part = torch.empty(nb, dtype=torch.float64, device=W.device)
+        st = lib.harp_mf_rmse(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, W.data_ptr(), W.stride(0),
+                              H.data_ptr(), H.stride(0), part.data_ptr(), _lib.stream_ptr(W.device))
+        _lib.check(st, "mf_rmse")
+        return part.sum()
+    v = _rt().harp_mf_sse_cpu(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, W.data_ptr(), W.stride(0),
+                              H.data_ptr(), H.stride(0))
+    return torch.tensor(v, dtype=torch.float64)

@@ -1,0 +1,278 @@
+"""Dynamic model rotation ("dymoro", Harp computation model B).
+
+Reference (ml/java/.../dymoro/):
+  * ``Rotator`` wraps K model slices (tables), one ``RotateTask`` per slice on its own
+    thread, so slice k rotates while compute runs on slice k+-1; ``getSplitMap(k)`` blocks
+    until slice k's rotation finished (Rotator.java:30-86);
+  * ``RotateTask.run``: compute the next rotation map, ``mapper.rotate(ctx,
+    "rotate-<table>-<opID>", table, map)``, re-split the received table into column
+    blocks (RotateTask.java:107-150); ``updateRotationMap`` follows a random order table
+    (:158-210);
+  * ``RotationUtil``: the master builds a (2P-1)*iters order table (per iteration a
+    random placement permutation then P-1 distinct random shifts) and broadcasts it
+    (RotationUtil.java:34-90);
+  * ``Scheduler``: 2-D (row-split x col-split) conflict-free block scheduler with a timer
+    budget (Scheduler.java:54-237); ``MPTask.doRun(cData, rData)`` (MPTask.java:56).
+
+MI355X design: a rotation is a grouped ``ncclSend/ncclRecv`` of a device slab; the
+:class:`DeviceRotator` keeps a spare receive buffer per slice and issues each slice's
+rotation on its OWN communicator (its own RCCL stream) asynchronously, so the comm stream
+overlaps the compute kernels on the current stream; completion is a device-side stream
+wait, never a host sync (slice shapes are static, slice ids are derived from the order
+table on the host). :class:`Rotator` provides the reference's table-level API on top of
+the generic ``rotate`` collective for non-dense models.
+"""
+from __future__ import annotations
+
+import random
+import threading
+import time
+from concurrent.futures import Future, ThreadPoolExecutor
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..core.combiner import ArrCombiner, Operation
+from ..core.table import PackedTable, Table
+from ..parallel import collectives as C
+from ..parallel.comm import Communicator
+
+
+# ---------------------------------------------------------------- rotation orders
+def create_rotation_order(rng: random.Random, num_iterations: int, num_workers: int) -> List[int]:
+    """Order table of length (2P-1)*iters: per iteration a placement permutation of the P
+    data blocks (identity in iteration 0), then the P-1 shifts 1..P-1 in random order."""
+    P = num_workers
+    orders: List[int] = []
+    for it in range(num_iterations):
+        if it == 0:
+            orders += list(range(P))
+        else:
+            ids = list(range(P))
+            while ids:
+                orders.append(ids.pop(rng.randrange(len(ids))))
+        ids = list(range(1, P))
+        while ids:
+            orders.append(ids.pop(rng.randrange(len(ids))))
+    return orders
+
+
+def get_rotation_sequences(mapper, num_iterations: int, seed: int = 0, ctx: str = "sgd") -> List[int]:
+    """Master creates the order table and broadcasts it (RotationUtil.getRotationSequences)."""
+    P = mapper.get_num_workers()
+    n = (2 * P - 1) * num_iterations
+    if mapper.is_master():
+        orders = create_rotation_order(random.Random(seed), num_iterations, P)
+        t = PackedTable([0], torch.tensor([orders], dtype=torch.int64, device=mapper.device),
+                        combiner=ArrCombiner(Operation.SUM))
+    else:
+        t = PackedTable([], torch.zeros((0, n), dtype=torch.int64, device=mapper.device),
+                        combiner=ArrCombiner(Operation.SUM))
+    if not mapper.broadcast(ctx, "bcast-rotate-orders", t, mapper.get_master_id(), False):
+        raise IOError("broadcast of rotation orders failed")
+    return t.buffer[0].cpu().tolist()
+
+
+class RotationSchedule:
+    """Placement of P data blocks over P workers for every (iteration, step).
+
+    ``placement(it, s)[i]`` = worker holding data block i at step s of iteration it. With
+    ``orders=None`` the schedule is the ring: block i sits on (i + s) mod P, and every
+    rotation sends to next = self+1."""
+
+    def __init__(self, num_workers: int, orders: Optional[Sequence[int]] = None):
+        self.P = num_workers
+        self.orders = list(orders) if orders is not None else None
+
+    def placement(self, it: int, s: int) -> List[int]:
+        P = self.P
+        if self.orders is None:
+            return [(i + s + it * P) % P for i in range(P)]
+        row = self.orders[(2 * P - 1) * it:(2 * P - 1) * (it + 1)]
+        if len(row) < 2 * P - 1:
+            raise IndexError("rotation order table exhausted")
+        base = row[:P]
+        shift = 0 if s == 0 else row[P + s - 1]
+        return [(base[i] + shift) % P for i in range(P)]
+
+    def block_at(self, worker: int, it: int, s: int) -> int:
+        return self.placement(it, s).index(worker)
+
+    def rotation_map(self, it: int, s: int) -> List[int]:
+        """Worker->worker map moving step (it, s) to the next step."""
+        cur = self.placement(it, s)
+        nxt = self.placement(it, s + 1) if s + 1 < self.P else self.placement(it + 1, 0)
+        m = [0] * self.P
+        for i in range(self.P):
+            m[cur[i]] = nxt[i]
+        return m
+
+
+# ---------------------------------------------------------------- device rotation engine
+class DeviceRotator:
+    """Asynchronous rotation of equally-shaped device slabs (one per model slice).
+
+    ``start(k, rmap)`` sends slab k to ``rmap[self]`` and receives the slab of the worker
+    mapping to self into a spare buffer, on slice k's private communicator; ``get(k)``
+    makes the current stream wait for it (no host sync) and returns the new slab."""
+
+    def __init__(self, comm: Communicator, slabs: Sequence[torch.Tensor], name: str = "rot"):
+        self.comm = comm
+        self.slabs = list(slabs)
+        self.spare = [torch.empty_like(s) for s in self.slabs]
+        self.channels = [comm.channel(f"{name}-{k}") for k in range(len(self.slabs))]
+        self._work: Dict[int, list] = {}
+        self.comm_time = 0.0
+
+    def start(self, k: int, rmap: Sequence[int]) -> None:
+        me = self.comm.rank
+        dst = rmap[me]
+        src = list(rmap).index(me)
+        if dst == me:
+            return
+        ch = self.channels[k]
+        self._work[k] = ch.sendrecv({dst: self.slabs[k]}, {src: self.spare[k]}, async_op=True)
+
+    def get(self, k: int) -> torch.Tensor:
+        works = self._work.pop(k, None)
+        if works is not None:
+            for w in works:
+                w.wait()  # stream-level wait on GPU (RCCL), blocking on gloo
+            self.slabs[k], self.spare[k] = self.spare[k], self.slabs[k]
+        return self.slabs[k]
+
+    def wait_all(self) -> None:
+        for k in list(self._work):
+            self.get(k)
+
+
+# ---------------------------------------------------------------- table-level Rotator
+class Rotator:
+    """Reference-style rotator over generic tables (one rotation thread per slice).
+
+    Each slice's rotations are issued from its own thread on its own communicator
+    channel, so concurrent rotations of different slices keep a per-communicator issue
+    order (the RCCL requirement; SURVEY §2.0 concurrency contract)."""
+
+    def __init__(self, tables: Sequence[Table], mapper, orders: Optional[Sequence[int]] = None, ctx: str = "rotate"):
+        self.tables = list(tables)
+        self.mapper = mapper
+        P = mapper.get_num_workers()
+        self.schedule = RotationSchedule(P, orders)
+        self.channels = [mapper.comm.channel(f"{ctx}-table-{k}") for k in range(len(tables))]
+        self._pool = ThreadPoolExecutor(max_workers=max(1, len(tables)))
+        self._fut: Dict[int, Future] = {}
+        self._step = [0] * len(tables)
+        self.comm_time = 0.0
+
+    def get_split_map(self, k: int) -> Table:
+        f = self._fut.pop(k, None)
+        if f is not None:
+            f.result()
+        return self.tables[k]
+
+    def rotate(self, k: int) -> None:
+        step = self._step[k]
+        P = self.schedule.P
+        it, s = divmod(step, P)
+        rmap = self.schedule.rotation_map(it, s) if self.schedule.orders is not None else None
+        self._step[k] += 1
+
+        def work():
+            t0 = time.perf_counter()
+            ok = C.rotate(self.channels[k], self.tables[k], rmap)
+            self.comm_time += time.perf_counter() - t0
+            if not ok:
+                raise IOError(f"rotate of slice {k} failed")
+
+        self._fut[k] = self._pool.submit(work)
+
+    def start(self) -> None:
+        pass
+
+    def pause(self) -> None:
+        for k in list(self._fut):
+            self.get_split_map(k)
+
+    def stop(self) -> None:
+        self.pause()
+        self._pool.shutdown(wait=True)
+
+
+# ---------------------------------------------------------------- 2-D block scheduler
+class BlockScheduler:
+    """Conflict-free 2-D (row split x column split) block scheduler.
+
+    Never runs two blocks sharing a row split or a column split at the same time
+    (Scheduler.java:104-116,150-213), refills as blocks finish, and optionally stops
+    submitting when ``time_budget`` seconds have elapsed (the reference's timer that keeps
+    all workers rotating in lockstep, :118-137). ``task(row, col) -> items`` runs on a
+    host thread pool; native (ctypes) tasks release the GIL and run in parallel."""
+
+    def __init__(self, num_rows: int, num_cols: int, task: Callable[[int, int], int], num_threads: int = 4):
+        self.R, self.C = num_rows, num_cols
+        self.task = task
+        self.num_threads = max(1, num_threads)
+
+    def schedule(self, time_budget: Optional[float] = None, blocks: Optional[Sequence[Tuple[int, int]]] = None) -> dict:
+        todo = set(blocks) if blocks is not None else {(r, c) for r in range(self.R) for c in range(self.C)}
+        busy_r, busy_c = set(), set()
+        lock = threading.Condition()
+        done_items = [0]
+        done_blocks = []
+        t0 = time.perf_counter()
+        inflight = [0]
+
+        def run(r, c):
+            try:
+                n = self.task(r, c)
+            finally:
+                with lock:
+                    busy_r.discard(r)
+                    busy_c.discard(c)
+                    done_items[0] += int(n or 0)
+                    done_blocks.append((r, c))
+                    inflight[0] -= 1
+                    lock.notify_all()
+
+        with ThreadPoolExecutor(max_workers=self.num_threads) as ex:
+            with lock:
+                while todo or inflight[0]:
+                    timed_out = time_budget is not None and time.perf_counter() - t0 > time_budget
+                    launched = False
+                    if not timed_out:
+                        for (r, c) in sorted(todo):
+                            if inflight[0] >= self.num_threads:
+                                break
+                            if r not in busy_r and c not in busy_c:
+                                todo.discard((r, c))
+                                busy_r.add(r)
+                                busy_c.add(c)
+                                inflight[0] += 1
+                                ex.submit(run, r, c)
+                                launched = True
+                    if timed_out and not inflight[0]:
+                        break
+                    if not launched:
+                        lock.wait(timeout=0.05)
+        return {"items": done_items[0], "blocks": done_blocks, "remaining": sorted(todo),
+                "seconds": time.perf_counter() - t0}
+
+
+class MPTask:
+    """Base of a model-parallel task: ``do_run(col_data, row_data) -> items`` with timing
+    records (MPTask.java:27-80)."""
+
+    def __init__(self):
+        self.items = 0
+        self.seconds = 0.0
+
+    def do_run(self, col_data, row_data) -> int:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def __call__(self, col_data, row_data) -> int:
+        t0 = time.perf_counter()
+        n = self.do_run(col_data, row_data)
+        self.seconds += time.perf_counter() - t0
+        self.items += int(n or 0)
+        return n
