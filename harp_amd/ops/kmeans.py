@@ -97,10 +97,12 @@ def prepare(c: torch.Tensor, dp: int, out: Optional[CentroidOperand] = None) -> 
 
 def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = None,
            labels: Optional[torch.Tensor] = None, want_objective: bool = True, variant: int = DEFAULT_VARIANT,
-           obj_partial: Optional[torch.Tensor] = None):
+           obj_partial: Optional[torch.Tensor] = None, accumulate: str = "bucket"):
     """Assign every point to its nearest centroid; optionally accumulate (x, 1) into
-    ``sums`` [K, dp] and return the sum of squared distances (0-dim fp64 tensor).
+    ``sums`` [Kp, dp] and return the sum of squared distances (0-dim fp64 tensor).
 
+    ``accumulate``: "bucket" (labels -> counting sort -> per-centroid row gather-sum,
+    deterministic) or "atomic" (fused fp32 atomics in the assign kernel).
     Returns (labels, objective)."""
     n, dp = X.shape
     dev = X.device
@@ -123,10 +125,16 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             assert sums.shape[0] >= op.Cm2.shape[0], "sums needs Kp (padded) rows"
             assert sums.device == dev
         assert X.dtype == torch.bfloat16 and X.is_contiguous() and op.Cm2.shape[1] == dp
+        fused = sums if accumulate == "atomic" else None
         st = lib.harp_kmeans_assign(X.data_ptr(), op.Cm2.data_ptr(), n, dp, op.Cm2.shape[0], op.d,
-                                    labels.data_ptr(), _lib.ptr(sums), sums.stride(0) if sums is not None else 0,
+                                    labels.data_ptr(), _lib.ptr(fused), fused.stride(0) if fused is not None else 0,
                                     _lib.ptr(obj_partial) if want_objective else None, variant, _lib.stream_ptr(dev))
         _lib.check(st, "kmeans_assign")
+        if sums is not None and fused is None:
+            from . import segment
+
+            perm, start = segment.bucket_labels(labels, op.Cm2.shape[0])
+            segment.bucket_rowsum(X, perm, start, sums)
         obj = obj_partial[:nblk].double().sum() if want_objective else None
         return labels, obj
     # CPU reference (fp32)

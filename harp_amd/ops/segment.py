@@ -1,0 +1,67 @@
+"""Label bucketing (counting sort) and per-bucket row sums on the GPU.
+
+``bucket_labels(labels, K)`` -> (perm, start): indices grouped by label, bucket offsets.
+``bucket_rowsum(X, perm, start, out)``: out[k] = sum of bf16 rows X[perm[start[k]:start[k+1]]].
+See csrc/segsum.hip for why this beats float atomics on gfx950.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Tuple
+
+import torch
+
+from . import _lib
+
+_lib.register({
+    "harp_bucket_chunk": [],
+    "harp_bucket_workspace_ints": [_lib.c_long, _lib.c_int],
+    "harp_bucket_labels": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                           _lib.c_void_p],
+    "harp_bucket_rowsum_bf16": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                                _lib.c_int, _lib.c_void_p],
+})
+_WS: Dict[Tuple, torch.Tensor] = {}
+
+
+def _lib_ret_long(fn):
+    fn.restype = ctypes.c_long
+    return fn
+
+
+def bucket_labels(labels: torch.Tensor, K: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    n = labels.numel()
+    if not _lib.use_native(labels):
+        order = torch.argsort(labels.long(), stable=True)
+        counts = torch.bincount(labels.long(), minlength=K)
+        start = torch.zeros(K + 1, dtype=torch.int64)
+        start[1:] = torch.cumsum(counts, 0)
+        return order.to(torch.int32), start.to(torch.int32)
+    lib = _lib.kernels()
+    _lib_ret_long(lib.harp_bucket_workspace_ints)
+    need = lib.harp_bucket_workspace_ints(n, K)
+    key = (labels.device, n, K)
+    ws = _WS.get(key)
+    if ws is None:
+        _WS.clear()  # keep one workspace alive
+        ws = torch.empty(need, dtype=torch.int32, device=labels.device)
+        _WS[key] = ws
+    so, po = ctypes.c_long(0), ctypes.c_long(0)
+    st = lib.harp_bucket_labels(labels.data_ptr(), n, K, ws.data_ptr(), ctypes.byref(so), ctypes.byref(po),
+                                _lib.stream_ptr(labels.device))
+    _lib.check(st, "bucket_labels")
+    return ws[po.value:po.value + n], ws[so.value:so.value + K + 1]
+
+
+def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    K = start.numel() - 1
+    if not _lib.use_native(X):
+        idx = torch.repeat_interleave(torch.arange(K), (start[1:] - start[:-1]).long())
+        out[:K, : X.shape[1]] = 0
+        out[:K, : X.shape[1]].index_add_(0, idx, X[perm.long()].float())
+        return out
+    assert X.dtype == torch.bfloat16 and X.is_contiguous() and out.dtype == torch.float32 and out.is_contiguous()
+    st = _lib.kernels().harp_bucket_rowsum_bf16(X.data_ptr(), X.shape[1], perm.data_ptr(), start.data_ptr(), K,
+                                                out.data_ptr(), out.stride(0), _lib.stream_ptr(X.device))
+    _lib.check(st, "bucket_rowsum")
+    return out

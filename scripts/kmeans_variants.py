@@ -33,14 +33,16 @@ def main():
     res = {}
     for _ in range(a.rounds):
         for v in variants:
-            for acc in (False, True):
-                K.assign(X, op, sums=sums if acc else None, labels=lab, want_objective=False, variant=v)
+            for acc in ("none", "atomic", "bucket"):
+                kw = dict(sums=None if acc == "none" else sums, labels=lab, want_objective=False, variant=v,
+                          accumulate=acc if acc != "none" else "bucket")
+                K.assign(X, op, **kw)
                 s, e = torch.cuda.Event(True), torch.cuda.Event(True)
                 s.record()
-                K.assign(X, op, sums=sums if acc else None, labels=lab, want_objective=False, variant=v)
+                K.assign(X, op, **kw)
                 e.record()
                 e.synchronize()
-                res.setdefault(f"v{v}{'+acc' if acc else ''}", []).append(s.elapsed_time(e))
+                res.setdefault(f"v{v}+{acc}", []).append(s.elapsed_time(e))
     flops = 2.0 * n * a.k * a.d
     out = {k: {"ms_min": min(v), "ms_med": sorted(v)[len(v) // 2], "tflops": flops / (min(v) / 1e3) / 1e12}
            for k, v in res.items()}

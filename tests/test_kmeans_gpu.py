@@ -28,16 +28,18 @@ def test_generate_points_layout(cuda):
     assert torch.equal(X, X2)  # counter-based generator: deterministic
 
 
+@pytest.mark.parametrize("accumulate", ["bucket", "atomic"])
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000), (1500, 250, 200)])
-def test_assign_matches_torch(cuda, variant, n, d, k):
+@pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000), (1500, 250, 200),
+                                   (200000, 100, 2000)])
+def test_assign_matches_torch(cuda, variant, n, d, k, accumulate):
     torch.manual_seed(0)
     x = torch.rand(n, d, device=cuda) * 1000
     X = K.pack_points(x, cuda)
     c = torch.rand(k, d, device=cuda) * 1000
     op = K.prepare(c, X.shape[1])
     sums = torch.zeros((K.padded_k(k), X.shape[1]), dtype=torch.float32, device=cuda)
-    lab, obj = K.assign(X, op, sums=sums, variant=variant)
+    lab, obj = K.assign(X, op, sums=sums, variant=variant, accumulate=accumulate)
     torch.cuda.synchronize()
     c_bf = c.to(torch.bfloat16).float()
     rlab, dist, rbest = _ref_assign(X, c_bf, d)
@@ -94,3 +96,21 @@ def test_kmeans_model_gpu_matches_cpu(cuda):
     assert abs(md_g - md_c) / md_c < 5e-3, (md_g, md_c)
     obj = gpu["objective"]
     assert obj[-1] <= obj[0]
+
+
+def test_bucket_labels_and_rowsum(cuda):
+    from harp_amd.ops import segment
+
+    n, K, dp = 300000, 5000, 112
+    lab = torch.randint(0, K, (n,), device=cuda, dtype=torch.int32)
+    lab[:1000] = 7  # one heavy bucket
+    perm, start = segment.bucket_labels(lab, K)
+    cnt = torch.bincount(lab.long(), minlength=K)
+    assert torch.equal((start[1:] - start[:-1]).long(), cnt)
+    assert torch.equal(torch.sort(perm.long()).values, torch.arange(n, device=cuda))
+    assert torch.equal(lab[perm.long()].long(), torch.repeat_interleave(torch.arange(K, device=cuda), cnt))
+    X = (torch.rand(n, dp, device=cuda) * 10).to(torch.bfloat16)
+    out = torch.zeros(K, dp, device=cuda)
+    segment.bucket_rowsum(X, perm, start, out)
+    ref = torch.zeros(K, dp, dtype=torch.float64, device=cuda).index_add_(0, lab.long(), X.double())
+    assert torch.allclose(out.double(), ref, rtol=1e-5, atol=1e-2)
