@@ -15,7 +15,8 @@
 //   2. colscan: per-bucket exclusive scan over chunks (two levels: 64-chunk segments)
 //   3. segscan: exclusive scan of bucket totals -> seg_start[K+1]
 //   4. bucket:  per chunk, LDS cursors = global base; perm[pos] = i
-//   5. rowsum:  one workgroup per bucket gathers its rows (16 B per lane, fp32 registers)
+//   5. rowsum:  each 16-lane slot sums a fixed run of the sorted permutation (balanced for any
+//               bucket skew) in fp32 registers, flushing at bucket boundaries
 #include "common.h"
 
 namespace {
@@ -108,44 +109,72 @@ __global__ __launch_bounds__(256) void bucket_kernel(const int* __restrict__ lab
   }
 }
 
-// one workgroup per bucket; LPR lanes cover one row (16 B each), 64/LPR rows per wave-load
-template <int LPR, int UNROLL>
+// Skew-proof gather-sum: every LPR-lane slot owns RUN consecutive entries of the
+// bucket-sorted permutation (so work is balanced whatever the bucket sizes), keeps the
+// running row sum in registers, and flushes it with one contiguous fp32 atomic row segment
+// whenever it crosses a bucket boundary (~1 flush per slot for buckets >> RUN).
+template <int LPR, int RUN>
 __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restrict__ X, int dp, const int* __restrict__ perm,
-                                                          const int* __restrict__ start, float* __restrict__ sums, int ld) {
-  constexpr int RPW = 64 / LPR;  // rows per wave-instruction
-  const int k = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int slot = lane / LPR, sl = lane % LPR;
-  const int a = start[k], b = start[k + 1];
+                                                          const int* __restrict__ start, int K, long n,
+                                                          float* __restrict__ sums, int ld) {
+  constexpr int SPW = 64 / LPR;  // slots per wave
+  const int lane = threadIdx.x & 63;
+  const int sl = lane % LPR;
+  const long slot = ((long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const long j0 = slot * RUN;
+  if (j0 >= n) return;
+  long j1 = j0 + RUN;
+  if (j1 > n) j1 = n;
   const bool active = sl * 8 < dp;
+  // bucket containing j0: last k with start[k] <= j0
+  int lo = 0, hi = K;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (start[mid] <= j0) lo = mid; else hi = mid;
+  }
+  int k = lo;
+  long kend = start[k + 1];
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int step = 4 * RPW;  // rows per workgroup iteration (4 waves)
-  for (int j0 = a + wave * RPW + slot; j0 < b; j0 += step * UNROLL) {
-    bf16x8 v[UNROLL];
+  auto flush = [&](int kk) {
+    if (active) {
+      float* o = sums + (long)kk * ld + sl * 8;
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int j = j0 + u * step;
-      if (j < b && active) v[u] = *(const bf16x8*)(X + (long)perm[j] * dp + sl * 8);
-      else v[u] = bf16x8{};
+      for (int e = 0; e < 8; ++e) {
+        if (acc[e] != 0.f) atomicAdd(o + e, acc[e]);
+        acc[e] = 0.f;
+      }
     }
+  };
+  long j = j0;
+  while (j < j1) {
+    while (j >= kend) {  // crossed into the next non-empty bucket
+      flush(k);
+      ++k;
+      kend = start[k + 1];
+    }
+    long stop = kend < j1 ? kend : j1;
+    // 4 rows in flight per slot inside one bucket
+    for (; j + 4 <= stop; j += 4) {
+      bf16x8 v0{}, v1{}, v2{}, v3{};
+      if (active) {
+        v0 = *(const bf16x8*)(X + (long)perm[j] * dp + sl * 8);
+        v1 = *(const bf16x8*)(X + (long)perm[j + 1] * dp + sl * 8);
+        v2 = *(const bf16x8*)(X + (long)perm[j + 2] * dp + sl * 8);
+        v3 = *(const bf16x8*)(X + (long)perm[j + 3] * dp + sl * 8);
+      }
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u)
+      for (int e = 0; e < 8; ++e) acc[e] += ((float)v0[e] + (float)v1[e]) + ((float)v2[e] + (float)v3[e]);
+    }
+    for (; j < stop; ++j) {
+      if (active) {
+        const bf16x8 v = *(const bf16x8*)(X + (long)perm[j] * dp + sl * 8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += (float)v[u][e];
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+      }
+    }
   }
-  // reduce the RPW row slots of the wave (lanes sl, sl+LPR, ...)
-#pragma unroll
-  for (int off = LPR; off < 64; off <<= 1)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], off, 64);
-  __shared__ float red[4][LPR * 8];
-  if (slot == 0 && active)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[wave][sl * 8 + e] = acc[e];
-  __syncthreads();
-  for (int c = threadIdx.x; c < dp; c += blockDim.x) {
-    sums[(long)k * ld + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-  }
+  flush(k);
+  (void)SPW;
 }
 
 }  // namespace
@@ -184,14 +213,17 @@ HARP_EXPORT int harp_bucket_labels(const int* lab, long n, int K, int* ws, long*
   return harp_launch_status();
 }
 
-// sums[k][0..dp) = sum of bf16 rows X[perm[j]] for j in [start[k], start[k+1])
-HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, const int* perm, const int* start, int K, float* sums,
-                                        int ld, hipStream_t s) {
-  if (dp % 8 || dp > 256 || ld < dp) return HARP_EBADARG;
+// sums[k][0..dp) += sum of bf16 rows X[perm[j]] for j in [start[k], start[k+1]) (sums must be
+// zeroed by the caller: partial rows are added with fp32 atomics at bucket boundaries)
+HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, const int* perm, const int* start, int K, long n,
+                                        float* sums, int ld, hipStream_t s) {
+  if (dp % 8 || dp > 256 || ld < dp || n <= 0) return n == 0 ? HARP_OK : HARP_EBADARG;
   const int lpr_min = dp / 8;
   const __bf16* Xb = (const __bf16*)X;
-  if (lpr_min <= 8) rowsum_bf16_kernel<8, 4><<<dim3(K), dim3(256), 0, s>>>(Xb, dp, perm, start, sums, ld);
-  else if (lpr_min <= 16) rowsum_bf16_kernel<16, 4><<<dim3(K), dim3(256), 0, s>>>(Xb, dp, perm, start, sums, ld);
-  else rowsum_bf16_kernel<32, 4><<<dim3(K), dim3(256), 0, s>>>(Xb, dp, perm, start, sums, ld);
+  constexpr int RUN = 256;
+  auto grid = [&](int lpr) { return dim3((unsigned)(((n + RUN - 1) / RUN * lpr + 255) / 256)); };
+  if (lpr_min <= 8) rowsum_bf16_kernel<8, RUN><<<grid(8), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
+  else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN><<<grid(16), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
+  else rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
   return harp_launch_status();
 }

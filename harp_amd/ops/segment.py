@@ -18,8 +18,8 @@ _lib.register({
     "harp_bucket_workspace_ints": [_lib.c_long, _lib.c_int],
     "harp_bucket_labels": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                            _lib.c_void_p],
-    "harp_bucket_rowsum_bf16": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
-                                _lib.c_int, _lib.c_void_p],
+    "harp_bucket_rowsum_bf16": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long,
+                                _lib.c_void_p, _lib.c_int, _lib.c_void_p],
 })
 _WS: Dict[Tuple, torch.Tensor] = {}
 
@@ -54,14 +54,14 @@ def bucket_labels(labels: torch.Tensor, K: int) -> Tuple[torch.Tensor, torch.Ten
 
 
 def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[k] += sum of the bucket's rows (zero ``out`` first for a plain sum)."""
     K = start.numel() - 1
     if not _lib.use_native(X):
         idx = torch.repeat_interleave(torch.arange(K), (start[1:] - start[:-1]).long())
-        out[:K, : X.shape[1]] = 0
         out[:K, : X.shape[1]].index_add_(0, idx, X[perm.long()].float())
         return out
     assert X.dtype == torch.bfloat16 and X.is_contiguous() and out.dtype == torch.float32 and out.is_contiguous()
     st = _lib.kernels().harp_bucket_rowsum_bf16(X.data_ptr(), X.shape[1], perm.data_ptr(), start.data_ptr(), K,
-                                                out.data_ptr(), out.stride(0), _lib.stream_ptr(X.device))
+                                                perm.numel(), out.data_ptr(), out.stride(0), _lib.stream_ptr(X.device))
     _lib.check(st, "bucket_rowsum")
     return out

@@ -104,7 +104,8 @@ def test_bucket_labels_and_rowsum(cuda):
 
     n, K, dp = 300000, 5000, 112
     lab = torch.randint(0, K, (n,), device=cuda, dtype=torch.int32)
-    lab[:1000] = 7  # one heavy bucket
+    lab[:100000] = 7  # one heavy bucket (skew)
+    lab[lab == 11] = 12  # an empty bucket
     perm, start = segment.bucket_labels(lab, K)
     cnt = torch.bincount(lab.long(), minlength=K)
     assert torch.equal((start[1:] - start[:-1]).long(), cnt)
