@@ -39,9 +39,9 @@ def main() -> int:
 
     import torch
 
-    from harp_amd.ops.build import build_kernels
+    from harp_amd.ops.build import KERNEL_LIB, build_kernels
 
-    if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+    if int(os.environ.get("LOCAL_RANK", "0")) == 0 and not os.path.exists(KERNEL_LIB):
         build_kernels()
     from harp_amd.models.kmeans import KMeansCollectiveMapper, KMeansConfig
     from harp_amd.ops import kmeans as K
@@ -49,12 +49,9 @@ def main() -> int:
     from harp_amd.runtime.mapper import KeyValReader
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        # the rank-0 build must finish before other ranks dlopen the library
-        pass
     comm = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
     if world > 1:
-        comm.barrier()
+        comm.barrier()  # rank 0's (rare) build finishes before any rank loads the library
     P, rank = comm.world_size, comm.rank
     N = int(args.points)
     n_local = N // P + (1 if rank < N % P else 0)

@@ -68,7 +68,9 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
         if verbose:
             print(f"[harp build] compiled {len(todo)} HIP source(s)", file=sys.stderr)
     if force or todo or _stale(KERNEL_LIB, objs):
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", KERNEL_LIB] + objs)
+        tmp = f"{KERNEL_LIB}.{os.getpid()}.tmp"
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs)
+        os.replace(tmp, KERNEL_LIB)  # atomic: concurrent loaders never see a partial file
     return KERNEL_LIB
 
 
@@ -79,7 +81,9 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     if not srcs:
         return ""
     if force or _stale(RUNTIME_LIB, srcs + headers):
-        _run([CXX] + CXX_FLAGS + ["-shared", "-o", RUNTIME_LIB] + srcs)
+        tmp = f"{RUNTIME_LIB}.{os.getpid()}.tmp"
+        _run([CXX] + CXX_FLAGS + ["-shared", "-o", tmp] + srcs)
+        os.replace(tmp, RUNTIME_LIB)
         if verbose:
             print(f"[harp build] linked {RUNTIME_LIB}", file=sys.stderr)
     return RUNTIME_LIB
