@@ -226,3 +226,85 @@ def collective_battery(comm):
     comm.fault_hook = None
     res["barrier_after_fault"] = C.barrier(comm)
     return res
+
+
+def runtime_battery(comm):
+    """KV/groupByKey, partition utilities, object comm, table-level Rotator, checkpoint."""
+    import os
+    import tempfile
+
+    from harp_amd.core.examples import IntCount, StringKey, WordAvgFunction, WordCountTable
+    from harp_amd.core.keyval import TensorKVCombiner, TensorKVPartition
+    from harp_amd.parallel import partition_util as PU
+    from harp_amd.runtime.dymoro import Rotator
+    from harp_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    P, r = comm.world_size, comm.rank
+    res = {}
+    # word count: every worker counts its words, groupByKey at owners, average, allgather
+    words = ["apple", "banana", "cherry", "apple", "durian"][: 3 + r % 3]
+    wc = WordCountTable(0, num_partitions=7)
+    for w in words:
+        wc.add_word(w, val=10)
+    C.aggregate(comm, wc, Partitioner(P), WordAvgFunction())
+    total = {}
+    for q in range(P):
+        for w in ["apple", "banana", "cherry", "apple", "durian"][: 3 + q % 3]:
+            total[w] = total.get(w, 0) + 1
+    got = {k.str: (v.val, v.count) for k, v in wc.items()}
+    res["wordcount_aggregate"] = set(got) == set(total) and all(got[w] == (10, 1) for w in total)
+    wc2 = WordCountTable(0, num_partitions=5)
+    for w in words:
+        wc2.add_word(w)
+    C.group_by_key(comm, wc2, Partitioner(P))
+    mine = {k.str: v.count for k, v in wc2.items()}
+    allm = PU.allgather_objects(comm, [IntCount(sum(mine.values()), len(mine))])
+    res["group_by_key"] = sum(x.val for x in allm) == sum(total.values()) and sum(x.count for x in allm) == len(total)
+    # device KV allreduce (generic path, combine = reduce-by-key)
+    t = Table(0, TensorKVCombiner())
+    t.add(0, TensorKVPartition(torch.tensor([r, 100]), torch.tensor([1.0, float(r)])))
+    C.allreduce(comm, t)
+    kv = t[0]
+    res["tensor_kv_allreduce"] = kv.keys.tolist() == list(range(P)) + [100] and kv.vals.tolist() == [1.0] * P + [
+        float(sum(range(P)))]
+    # partition utilities
+    tab = Table(0)
+    for i in range(r + 1):
+        tab.add(i, torch.zeros(1))
+    cnt = PU.regroup_partition_count(comm, tab, Partitioner(P))
+    res["regroup_partition_count"] = int(cnt.sum()) == sum(q + 1 for q in range(P)) and int(cnt[r].sum()) == r + 1
+    sets = PU.allgather_partition_set(comm, tab)
+    res["allgather_partition_set"] = [s.par_set for s in sets] == [list(range(q + 1)) for q in range(P)]
+    g = PU.gather_partition_set(comm, tab, 0)
+    res["gather_partition_set"] = (g is not None and len(g) == P) if r == 0 else g is None
+    order = PU.create_send_order(P, r)
+    res["send_order"] = sorted(order) == [q for q in range(P) if q != r]
+    objs = PU.broadcast_objects(comm, [IntCount(7, 8)] if r == 0 else None, 0)
+    res["broadcast_objects"] = len(objs) == 1 and objs[0].val == 7
+    gathered = PU.gather_objects(comm, [IntCount(r, 1)], 0)
+    res["gather_objects"] = ([o.val for o in gathered] == list(range(P))) if r == 0 else gathered is None
+    # table-level rotator: 2 slices rotating on their own channels, concurrently
+    class _M:
+        pass
+
+    mp = _M()
+    mp.comm, mp.get_num_workers = comm, (lambda: P)
+    t0, t1 = Table(0), Table(1)
+    t0.add(r, torch.tensor([float(r)]))
+    t1.add(100 + r, torch.tensor([float(r)]))
+    rot = Rotator([t0, t1], mp)
+    for step in range(P):
+        rot.rotate(0)
+        rot.rotate(1)
+        a, b = rot.get_split_map(0), rot.get_split_map(1)
+    rot.stop()
+    res["rotator_full_tour"] = a.get_partition_ids() == [r] and b.get_partition_ids() == [100 + r]
+    # checkpoint / resume across ranks
+    d = os.path.join(tempfile.gettempdir(), f"harp_ck_{os.environ.get('MASTER_PORT', '0')}")
+    ct = Table(0)
+    ct.add(r, torch.full((3,), float(r)))
+    save_checkpoint(d, {"m": ct}, r, P, iteration=3, comm=comm)
+    C.barrier(comm)
+    man, tabs = load_checkpoint(d, r, P)
+    res["checkpoint_resume"] = man["iteration"] == 3 and torch.equal(tabs["m"][r], torch.full((3,), float(r)))
+    return res
