@@ -1,0 +1,172 @@
+// SYRK partial G += X^T X on MFMA (bf16 in, fp32 accumulate/out) for gfx950.
+//
+// The step-1 partial of covariance / low-order moments / correlation PCA / normal-equation
+// regression (DAAL DistributedStep1Local: ml/daal/.../daal_cov/densedistri/
+// COVDaalCollectiveMapper.java:146-175, daal_pca/cordensedistr/PCADaalCollectiveMapper.java:
+// 121-147, daal_linreg/normaleq). N = 1e8 x d = 1000 is ~1e14 MFMA FLOP per pass.
+//
+// Design (MI355X-first):
+//  * data is stored FEATURE-MAJOR, XT[d_pad][ld] (samples contiguous): for G = XT XT^T both
+//    MFMA operands want 8 consecutive samples of one feature per lane, which is then a
+//    plain 16-B read — no transposes anywhere. A row of ones in XT makes G's last column
+//    the column sums and G[ones][ones] = n, so moments come out of the same pass.
+//  * only upper-triangular 128x128 output tiles are computed (diagonal tiles in full);
+//    the sample dimension is split over workgroups (split-K) for >= 1000 workgroups, each
+//    workgroup adds its fp32 tile into G with contiguous 128-B atomic row segments.
+//  * per 64-sample step both 128-feature operand panels stream through double-buffered LDS
+//    by global_load_lds (LDS-DMA); a 16-B chunk XOR swizzle c ^ ((row >> 1) & 7), applied
+//    to the DMA source and the ds_read_b128 address, keeps every read lane group
+//    conflict-free. 4 waves, each a 64x64 sub-tile = 2x2 accumulators of
+//    v_mfma_f32_32x32x16_bf16.
+#include "common.h"
+
+namespace {
+
+constexpr int MT = 128;       // macro tile (features)
+constexpr int KT = 64;        // samples per stage
+constexpr int CPR = KT / 8;   // 16-B chunks per LDS row (8)
+constexpr int PANEL_BYTES = MT * KT * 2;  // 16 KiB
+
+__device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+// one 128 x 64 panel of XT (rows r0.., samples k0..) -> LDS, 16 DMA wave-instructions
+__device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long ld, int r0, long k0, char* lds,
+                                            int wave, int lane) {
+#pragma unroll
+  for (int j = wave; j < PANEL_BYTES / 1024; j += 4) {
+    const int q = j * 64 + lane;          // chunk position in the LDS image
+    const int row = q / CPR, cp = q % CPR;
+    const int c = swz(row, cp);           // involution: source chunk for this position
+    const __bf16* src = XT + (long)(r0 + row) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void syrk_kernel(const __bf16* __restrict__ XT, long ld, long n, int nt,
+                                                   long chunk, float* __restrict__ G, int ldg) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * PANEL_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // blockIdx.x -> (upper-triangular tile (ti <= tj), sample split)
+  const int ntiles = nt * (nt + 1) / 2;
+  const int tile = blockIdx.x % ntiles;
+  const long split = blockIdx.x / ntiles;
+  int ti = 0, rem = tile;
+  while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
+  const int tj = ti + rem;
+  const bool diag = ti == tj;
+  const long kbeg = split * chunk;
+  long kend = kbeg + chunk;
+  if (kend > n) kend = n;
+  if (kbeg >= kend) return;
+  const int wr = wave >> 1, wc = wave & 1;  // this wave's 64x64 sub-tile
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
+
+  // buffers: A[c] = smem + c*PANEL, B[c] = smem + (2+c)*PANEL
+  stage_panel(XT, ld, ti * MT, kbeg, smem, wave, lane);
+  if (!diag) stage_panel(XT, ld, tj * MT, kbeg, smem + 2 * PANEL_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (long k0 = kbeg; k0 < kend; k0 += KT) {
+    if (k0 + KT < kend) {
+      stage_panel(XT, ld, ti * MT, k0 + KT, smem + (cur ^ 1) * PANEL_BYTES, wave, lane);
+      if (!diag) stage_panel(XT, ld, tj * MT, k0 + KT, smem + (2 + (cur ^ 1)) * PANEL_BYTES, wave, lane);
+    }
+    const char* A = smem + cur * PANEL_BYTES;
+    const char* B = diag ? A : smem + (2 + cur) * PANEL_BYTES;
+#pragma unroll
+    for (int s = 0; s < KT / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int row = wr * 64 + a * 32 + r;
+        af[a] = *(const bf16x8*)(A + row * (CPR * 16) + swz(row, 2 * s + h) * 16);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int row = wc * 64 + b * 32 + r;
+        bfr[b] = *(const bf16x8*)(B + row * (CPR * 16) + swz(row, 2 * s + h) * 16);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+  // D[i][j]: lane holds col = lane&31, rows (v&3) + 8*(v>>2) + 4h of each 32x32 block
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int i0 = ti * MT + wr * 64 + a * 32;
+      const int j0 = tj * MT + wc * 64 + b * 32;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = (v & 3) + 8 * (v >> 2) + 4 * h;
+        atomicAdd(G + (long)(i0 + row) * ldg + j0 + r, acc[a][b][v]);
+      }
+    }
+}
+
+// row-major X[n][d] (bf16/any) -> feature-major XT[d_pad][ld] bf16 with a ones row at
+// index d (tiled transpose through LDS).
+__global__ void to_feature_major_kernel(const __bf16* __restrict__ X, long n, int d, long ldx,
+                                        __bf16* __restrict__ XT, long ld, int ones_row) {
+  __shared__ __bf16 tile[32][33];
+  const long k0 = (long)blockIdx.x * 32;
+  const int f0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int yy = ty; yy < 32; yy += 8) {
+    const long k = k0 + yy;
+    const int f = f0 + tx;
+    __bf16 v = (__bf16)0.f;
+    if (k < n) {
+      if (f < d) v = X[k * ldx + f];
+      else if (f == ones_row) v = (__bf16)1.f;
+    }
+    tile[yy][tx] = v;
+  }
+  __syncthreads();
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int f = f0 + yy;
+    const long k = k0 + tx;
+    if (k < ld) XT[(long)f * ld + k] = tile[tx][yy];
+  }
+}
+
+}  // namespace
+
+// G[d_pad][ldg] (+)= XT XT^T, upper 128-tiles only; XT [d_pad][ld] bf16, d_pad % 128 == 0,
+// n % 64 == 0 (zero-padded samples), ld >= n, ld % 8 == 0.
+HARP_EXPORT int harp_syrk_t_bf16(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits,
+                                 hipStream_t s) {
+  if (d_pad % MT || n % KT || ld < n || ld % 8 || ldg < d_pad) return HARP_EBADARG;
+  if (n == 0) return HARP_OK;
+  const int nt = d_pad / MT;
+  const int ntiles = nt * (nt + 1) / 2;
+  if (num_splits <= 0) num_splits = (2048 + ntiles - 1) / ntiles;
+  long chunk = (n + num_splits - 1) / num_splits;
+  chunk = (chunk + KT - 1) / KT * KT;
+  const long splits = (n + chunk - 1) / chunk;
+  syrk_kernel<<<dim3((unsigned)(ntiles * splits)), dim3(256), 0, s>>>((const __bf16*)XT, ld, n, nt, chunk, G, ldg);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_to_feature_major_bf16(const void* X, long n, int d, long ldx, void* XT, long ld, int d_pad,
+                                           int ones_row, hipStream_t s) {
+  if (ld < n || d_pad < d) return HARP_EBADARG;
+  dim3 grid((unsigned)((ld + 31) / 32), (unsigned)((d_pad + 31) / 32));
+  to_feature_major_kernel<<<grid, dim3(256), 0, s>>>((const __bf16*)X, n, d, ldx, (__bf16*)XT, ld, ones_row);
+  return harp_launch_status();
+}

@@ -1,0 +1,242 @@
+"""Statistics family: covariance, low-order moments, PCA, normalization, quantiles,
+sorting, outlier detection.
+
+Reference (ml/daal): ``daal_cov/{dense,csr}distri`` (covariance step1 ->
+gather -> step2, COVDaalCollectiveMapper.java:146-175), ``daal_mom/{dense,csr}distri``
+(low_order_moments), ``daal_pca/{cordense,corcsr,svddense}distr`` (correlation /
+SVD PCA, PCADaalCollectiveMapper.java:121-147), batch-only ``daal_normalization``
+(minmax, zscore), ``daal_quantile``, ``daal_sorting``, ``daal_outlier`` (univariate,
+multivariate, BACON).
+
+Each distributed algorithm is: local partial sums on the device (the Gram / cross-product
+partial is a GEMM — ``ops.linalg.gram``) -> one packed allreduce
+(:func:`~harp_amd.models.common.reduce_partials`) -> finalize on every worker in fp64.
+Inputs may be dense tensors or torch sparse (CSR/COO) tensors (the ``csr`` variants).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from ..core.combiner import Operation
+from ..ops import linalg as LA
+from ..parallel.comm import Communicator
+from .common import gather_rows, reduce_partials
+
+
+def _local(comm: Optional[Communicator]) -> Communicator:
+    return comm if comm is not None else Communicator()
+
+
+# ------------------------------------------------------------------ covariance / moments
+def covariance_partial(X: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """Step 1: n, sum x, X^T X (cross-product) of the local block."""
+    n = X.shape[0]
+    s = LA.colsum(X)
+    return {"n": torch.tensor([float(n)], device=s.device), "sum": s, "xtx": LA.gram(X)}
+
+
+def covariance_finalize(p: Dict[str, torch.Tensor], bias: bool = False) -> Dict[str, torch.Tensor]:
+    n = p["n"].double().item()
+    mean = p["sum"].double() / n
+    cov = (p["xtx"].double() - n * torch.outer(mean, mean)) / (n if bias else max(n - 1, 1))
+    return {"mean": mean, "covariance": cov}
+
+
+def covariance(X: torch.Tensor, comm: Optional[Communicator] = None, bias: bool = False) -> Dict[str, torch.Tensor]:
+    return covariance_finalize(reduce_partials(_local(comm), covariance_partial(X)), bias)
+
+
+def correlation(X: torch.Tensor, comm: Optional[Communicator] = None) -> Dict[str, torch.Tensor]:
+    r = covariance(X, comm)
+    sd = r["covariance"].diagonal().clamp_min(0).sqrt()
+    r["correlation"] = r["covariance"] / torch.outer(sd, sd).clamp_min(1e-300)
+    return r
+
+
+def low_order_moments(X: torch.Tensor, comm: Optional[Communicator] = None) -> Dict[str, torch.Tensor]:
+    """DAAL low_order_moments: minimum, maximum, sum, sumSquares, sumSquaresCentered, mean,
+    secondOrderRawMoment, variance, standardDeviation, variation."""
+    comm = _local(comm)
+    Xd = X.to_dense() if X.is_sparse or X.layout == torch.sparse_csr else X
+    Xf = Xd.double() if Xd.device.type == "cpu" else Xd.float()
+    sums = reduce_partials(comm, {"n": torch.tensor([float(Xd.shape[0])], device=Xd.device),
+                                  "sum": Xf.sum(0), "sumsq": (Xf * Xf).sum(0)})
+    mm = reduce_partials(comm, {"min": Xf.min(0).values, "negmax": -Xf.max(0).values}, Operation.MIN)
+    n = sums["n"].item()
+    mean = sums["sum"] / n
+    ssc = sums["sumsq"] - n * mean * mean
+    var = ssc / max(n - 1, 1)
+    sd = var.clamp_min(0).sqrt()
+    return {"minimum": mm["min"], "maximum": -mm["negmax"], "sum": sums["sum"], "sumSquares": sums["sumsq"],
+            "sumSquaresCentered": ssc, "mean": mean, "secondOrderRawMoment": sums["sumsq"] / n, "variance": var,
+            "standardDeviation": sd, "variation": sd / mean}
+
+
+# ------------------------------------------------------------------ PCA
+def pca(X: torch.Tensor, comm: Optional[Communicator] = None, method: str = "correlation",
+        n_components: Optional[int] = None) -> Dict[str, torch.Tensor]:
+    """PCA of the (standardized) data: eigenvalues descending + eigenvectors (rows).
+
+    ``correlation``: eigen-decomposition of the distributed correlation matrix.
+    ``svd``: z-score the data with global moments, distributed TSQR, SVD of R
+    (the DAAL svdDense method); both yield the correlation-PCA spectrum."""
+    comm = _local(comm)
+    if method == "correlation":
+        r = correlation(X, comm)
+        evals, evecs = torch.linalg.eigh(r["correlation"])
+        order = torch.argsort(evals, descending=True)
+        evals, evecs = evals[order], evecs[:, order].t()
+    elif method == "svd":
+        mom = low_order_moments(X, comm)
+        Z = (X.double() - mom["mean"].to(X.device)) / mom["standardDeviation"].to(X.device).clamp_min(1e-300)
+        qr = tsqr(Z, comm, want_q=False)
+        ntot = reduce_partials(comm, {"n": torch.tensor([float(X.shape[0])], device=X.device)})["n"].item()
+        _, s, vt = torch.linalg.svd(qr["R"])
+        evals, evecs = s * s / max(ntot - 1, 1), vt
+    else:
+        raise ValueError(method)
+    # sign convention: largest-magnitude component of each eigenvector positive
+    idx = evecs.abs().argmax(1)
+    sign = torch.sign(evecs.gather(1, idx[:, None]))
+    evecs = evecs * sign
+    if n_components:
+        evals, evecs = evals[:n_components], evecs[:n_components]
+    return {"eigenvalues": evals, "eigenvectors": evecs}
+
+
+# ------------------------------------------------------------------ TSQR / SVD (distributed)
+def tsqr(X: torch.Tensor, comm: Optional[Communicator] = None, want_q: bool = True) -> Dict[str, torch.Tensor]:
+    """Distributed tall-skinny QR (daal_qr 3-step: local QR -> QR of stacked R's -> local
+    Q update). The stacked R's are all-gathered so every worker runs step 2 itself."""
+    comm = _local(comm)
+    Xd = X.double() if X.device.type == "cpu" else X.float()
+    Q1, R1 = torch.linalg.qr(Xd, mode="reduced")
+    d = Xd.shape[1]
+    Rs = gather_rows(comm, R1)  # [P*d, d]
+    Q2, R = torch.linalg.qr(Rs.double(), mode="reduced")
+    # make R's diagonal non-negative (unique QR)
+    sgn = torch.sign(torch.diagonal(R))
+    sgn[sgn == 0] = 1
+    R = R * sgn[:, None]
+    Q2 = Q2 * sgn[None, :]
+    out = {"R": R}
+    if want_q:
+        blk = Q2[comm.rank * d:(comm.rank + 1) * d].to(Xd.device, Xd.dtype)
+        out["Q"] = Q1 @ blk
+    return out
+
+
+def svd(X: torch.Tensor, comm: Optional[Communicator] = None, want_u: bool = True) -> Dict[str, torch.Tensor]:
+    """Distributed SVD via TSQR (daal_svd 3-step): X = Q R, R = U_r S V^T, U = Q U_r."""
+    r = tsqr(X, comm, want_q=want_u)
+    Ur, s, vt = torch.linalg.svd(r["R"])
+    out = {"singularValues": s, "rightSingularMatrix": vt}
+    if want_u:
+        out["leftSingularMatrix"] = r["Q"] @ Ur.to(r["Q"].device, r["Q"].dtype)
+    return out
+
+
+def cholesky(A: torch.Tensor) -> torch.Tensor:
+    """Lower-triangular Cholesky factor (daal_cholesky, batch)."""
+    return torch.linalg.cholesky(A.double())
+
+
+def pivoted_qr(X: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """QR with column pivoting (daal_pivoted_qr, batch): X[:, perm] = Q R."""
+    import scipy.linalg
+
+    Q, R, piv = scipy.linalg.qr(X.double().cpu().numpy(), mode="economic", pivoting=True)
+    return {"Q": torch.from_numpy(Q), "R": torch.from_numpy(R), "permutation": torch.from_numpy(piv)}
+
+
+# ------------------------------------------------------------------ normalization
+def normalize_minmax(X: torch.Tensor, lower: float = 0.0, upper: float = 1.0,
+                     comm: Optional[Communicator] = None) -> torch.Tensor:
+    m = reduce_partials(_local(comm), {"min": X.min(0).values, "negmax": -X.max(0).values}, Operation.MIN)
+    mn, mx = m["min"].to(X.device, X.dtype), (-m["negmax"]).to(X.device, X.dtype)
+    rng = (mx - mn)
+    rng = torch.where(rng == 0, torch.ones_like(rng), rng)
+    return lower + (X - mn) / rng * (upper - lower)
+
+
+def normalize_zscore(X: torch.Tensor, comm: Optional[Communicator] = None) -> torch.Tensor:
+    mom = low_order_moments(X, comm)
+    sd = mom["standardDeviation"].to(X.device, X.dtype)
+    return (X - mom["mean"].to(X.device, X.dtype)) / torch.where(sd == 0, torch.ones_like(sd), sd)
+
+
+# ------------------------------------------------------------------ quantiles / sorting
+def quantiles(X: torch.Tensor, q=(0.1, 0.5, 0.9), comm: Optional[Communicator] = None) -> torch.Tensor:
+    """Per-feature quantiles [len(q), d] (daal_quantile). Distributed: exact, over the
+    all-gathered columns."""
+    Xa = gather_rows(_local(comm), X) if comm is not None else X
+    return torch.quantile(Xa.double(), torch.tensor(q, dtype=torch.float64, device=Xa.device), dim=0)
+
+
+def sort_features(X: torch.Tensor) -> torch.Tensor:
+    """Each feature column sorted ascending (daal_sorting)."""
+    return torch.sort(X, dim=0).values
+
+
+# ------------------------------------------------------------------ outlier detection
+def outliers_univariate(X: torch.Tensor, threshold: float = 3.0, comm: Optional[Communicator] = None) -> torch.Tensor:
+    """Per-feature weights (1 = inlier): |x - mean| / std <= threshold, with global moments
+    (DAAL univariate_outlier_detection default initialization)."""
+    mom = low_order_moments(X, comm)
+    z = (X.double() - mom["mean"].to(X.device)) / mom["standardDeviation"].to(X.device).clamp_min(1e-300)
+    return (z.abs() <= threshold).to(X.dtype)
+
+
+def mahalanobis_sq(X: torch.Tensor, mean: torch.Tensor, cov: torch.Tensor) -> torch.Tensor:
+    L = torch.linalg.cholesky(cov.double() + 1e-12 * torch.eye(cov.shape[0], dtype=torch.float64, device=cov.device))
+    Z = torch.linalg.solve_triangular(L, (X.double() - mean.double()).t(), upper=False)
+    return (Z * Z).sum(0)
+
+
+def outliers_multivariate(X: torch.Tensor, threshold: Optional[float] = None,
+                          comm: Optional[Communicator] = None) -> torch.Tensor:
+    """Row weights (1 = inlier) by Mahalanobis distance to the global mean/covariance;
+    default threshold = chi2_{0.999}(d) on the squared distance."""
+    r = covariance(X, comm)
+    d2 = mahalanobis_sq(X, r["mean"].to(X.device), r["covariance"].to(X.device))
+    if threshold is None:
+        from scipy.stats import chi2
+
+        threshold = float(chi2.ppf(0.999, X.shape[1]))
+    return (d2 <= threshold).to(X.dtype)
+
+
+def outliers_bacon(X: torch.Tensor, alpha: float = 0.05, init: str = "median", max_iter: int = 100) -> torch.Tensor:
+    """BACON outlier detection (Billor, Hadi & Velleman 2000; daal bacon_outlier_detection):
+    grow a clean basic subset by Mahalanobis distance until it stabilises; returns row
+    weights (1 = inlier)."""
+    from scipy.stats import chi2
+
+    Xd = X.double()
+    n, p = Xd.shape
+    if init == "median":
+        d0 = (Xd - Xd.median(0).values).norm(dim=1)
+    else:
+        d0 = mahalanobis_sq(Xd, Xd.mean(0), torch.cov(Xd.t()))
+    m = min(n, max(4 * p, p + 1))
+    basic = torch.zeros(n, dtype=torch.bool, device=X.device)
+    basic[torch.argsort(d0)[:m]] = True
+    cnp = lambda r: max(0.0, 1 + (p + 1) / (n - p) + 2 / (n - 1 - 3 * p) if n - 1 - 3 * p > 0 else 1.0)  # noqa: E731
+    for _ in range(max_iter):
+        sub = Xd[basic]
+        mu = sub.mean(0)
+        cov = torch.cov(sub.t()).reshape(p, p)
+        dist = mahalanobis_sq(Xd, mu, cov).clamp_min(0).sqrt()
+        r = int(basic.sum())
+        h = (n + p + 1) // 2
+        c = max(0.0, (h - r) / (h + r)) + 1 + (p + 1) / max(n - p, 1) + 1 / max(n - h - p, 1)
+        thr = c * math.sqrt(chi2.ppf(1 - alpha / n, p))
+        new = dist < thr
+        if torch.equal(new, basic):
+            break
+        basic = new
+    return basic.to(X.dtype)

@@ -1,0 +1,138 @@
+"""Dense linear-algebra device ops for the partial-result family.
+
+``gram(X)`` = X^T X and ``colsum(X)`` — the step-1 partials of covariance / moments /
+PCA / normal-equation regressions (DAAL ``DistributedStep1Local``). On the GPU, bf16 and
+fp32 inputs go to the hand-written MFMA SYRK kernel in ``csrc/syrk.hip`` (upper-triangle
+tiles only, fp32 accumulation, column sums fused); fp64 and sparse inputs use torch
+(rocBLAS / rocSPARSE) — plain library GEMMs.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _is_sparse(X: torch.Tensor) -> bool:
+    return X.is_sparse or X.layout in (torch.sparse_csr, torch.sparse_csc)
+
+
+def colsum(X: torch.Tensor) -> torch.Tensor:
+    if _is_sparse(X):
+        Xc = X.to_sparse_coo().coalesce()
+        out = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+        return out.index_add_(0, Xc.indices()[1], Xc.values().double())
+    acc = torch.float64 if X.device.type == "cpu" else torch.float32
+    return X.to(acc).sum(0)
+
+
+def gram(X: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """X^T X (fp64 on CPU, fp32 accumulation on the GPU)."""
+    if _is_sparse(X):
+        Xc = X.to_sparse_csr().to(torch.float64 if X.device.type == "cpu" else torch.float32)
+        G = (Xc.t() @ Xc.to_dense()) if X.device.type != "cpu" else (Xc.to_dense().t() @ Xc.to_dense())
+        return G if out is None else out.add_(G)
+    if X.device.type == "cpu":
+        Xd = X.double()
+        G = Xd.t() @ Xd
+        return G if out is None else out.add_(G)
+    if _lib.use_native(X) and X.dtype in (torch.bfloat16, torch.float32) and _has_syrk():
+        return syrk(X, out)  # bf16 operands, fp32 accumulation (MFMA)
+    Xf = X.float()
+    G = Xf.t() @ Xf
+    return G if out is None else out.add_(G)
+
+
+_lib.register({
+    "harp_syrk_t_bf16": [_lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_int,
+                         _lib.c_void_p],
+    "harp_to_feature_major_bf16": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_long,
+                                   _lib.c_int, _lib.c_int, _lib.c_void_p],
+})
+
+MT = 128  # SYRK macro tile (features)
+KT = 64   # samples per SYRK stage
+
+
+class FeatureMajor:
+    """Feature-major bf16 copy of a data block for the MFMA SYRK: ``XT [d_pad, ld]`` with
+    samples contiguous, a row of ones at index ``d`` (so G[:, d] = column sums and
+    G[d, d] = n), zero padding to ``d_pad = round_up(d + 1, 128)`` features and
+    ``ld = round_up(n, 64)`` samples."""
+
+    def __init__(self, XT: torch.Tensor, n: int, d: int):
+        self.XT, self.n, self.d = XT, n, d
+
+    @property
+    def d_pad(self) -> int:
+        return self.XT.shape[0]
+
+    @property
+    def ld(self) -> int:
+        return self.XT.shape[1]
+
+    @staticmethod
+    def dims(n: int, d: int):
+        return (d + 1 + MT - 1) // MT * MT, (n + KT - 1) // KT * KT
+
+    @classmethod
+    def from_rows(cls, X: torch.Tensor) -> "FeatureMajor":
+        n, d = X.shape
+        d_pad, ld = cls.dims(n, d)
+        Xb = X.to(torch.bfloat16).contiguous()
+        XT = torch.empty((d_pad, ld), dtype=torch.bfloat16, device=X.device)
+        st = _lib.kernels().harp_to_feature_major_bf16(Xb.data_ptr(), n, d, Xb.stride(0), XT.data_ptr(), ld, d_pad, d,
+                                                       _lib.stream_ptr(X.device))
+        _lib.check(st, "to_feature_major")
+        return cls(XT, n, d)
+
+    @classmethod
+    def uniform(cls, n: int, d: int, lo: float = 0.0, hi: float = 1.0, seed: int = 0, device="cuda") -> "FeatureMajor":
+        """Synthetic U[lo,hi) data generated directly in feature-major layout on the device."""
+        from .kmeans import _lib as _kl  # same library
+
+        d_pad, ld = cls.dims(n, d)
+        XT = torch.empty((d_pad, ld), dtype=torch.bfloat16, device=device)
+        st = _kl.kernels().harp_uniform_rows_bf16(XT.data_ptr(), d_pad, ld, ld, float(lo), float(hi),
+                                                  seed & 0xFFFFFFFFFFFFFFFF, 0, 0, _lib.stream_ptr(XT.device))
+        _lib.check(st, "uniform_rows")
+        XT[d:].zero_()
+        XT[d, :n] = 1.0
+        if ld > n:
+            XT[:, n:].zero_()
+        return cls(XT, n, d)
+
+
+def syrk_t(fm: FeatureMajor, G: torch.Tensor | None = None, num_splits: int = 0) -> torch.Tensor:
+    """G (+)= XT XT^T over the upper 128-tiles (fp32); call :func:`symmetrize_upper` after."""
+    if G is None:
+        G = torch.zeros((fm.d_pad, fm.d_pad), dtype=torch.float32, device=fm.XT.device)
+    st = _lib.kernels().harp_syrk_t_bf16(fm.XT.data_ptr(), fm.ld, fm.ld, fm.d_pad, G.data_ptr(), G.stride(0),
+                                         num_splits, _lib.stream_ptr(fm.XT.device))
+    _lib.check(st, "syrk_t")
+    return G
+
+
+def symmetrize_upper(G: torch.Tensor) -> torch.Tensor:
+    return torch.triu(G) + torch.triu(G, 1).t()
+
+
+def gram_stats(fm: FeatureMajor, G: torch.Tensor | None = None):
+    """(n, column sums, X^T X) of a FeatureMajor block from ONE SYRK pass."""
+    G = symmetrize_upper(syrk_t(fm, G))
+    d = fm.d
+    return G[d, d], G[:d, d].clone(), G[:d, :d].clone()
+
+
+def _has_syrk() -> bool:
+    try:
+        return hasattr(_lib.kernels(), "harp_syrk_t_bf16")
+    except _lib.NativeUnavailable:
+        return False
+
+
+def syrk(X: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """X^T X of a row-major GPU block via a feature-major bf16 copy + MFMA SYRK."""
+    fm = FeatureMajor.from_rows(X)
+    _, _, G = gram_stats(fm)
+    return G if out is None else out.add_(G)

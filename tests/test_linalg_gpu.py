@@ -1,0 +1,42 @@
+"""MFMA SYRK numerics vs torch fp64 on the same bf16-rounded data."""
+import pytest
+import torch
+
+from harp_amd.ops import linalg as LA
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,d", [(1000, 10), (4096, 100), (20000, 257), (3000, 1000)])
+def test_gram_stats_matches_fp64(cuda, n, d):
+    X = torch.rand(n, d, device=cuda) * 4 - 1
+    fm = LA.FeatureMajor.from_rows(X)
+    cnt, s, G = LA.gram_stats(fm)
+    Xb = X.to(torch.bfloat16).double()
+    assert int(cnt.item()) == n
+    assert torch.allclose(s.double(), Xb.sum(0), rtol=1e-5, atol=1e-2)
+    ref = Xb.t() @ Xb
+    assert torch.allclose(G.double(), ref, rtol=2e-5, atol=1e-3 * ref.abs().max().item() * 1e-3 + 1e-2)
+
+
+def test_feature_major_uniform_and_cov(cuda):
+    fm = LA.FeatureMajor.uniform(50000, 64, 0.0, 1.0, seed=3, device=cuda)
+    assert fm.XT.shape == (128, 50048)
+    cnt, s, G = LA.gram_stats(fm)
+    n = cnt.item()
+    mean = s.double() / n
+    cov = (G.double() - n * torch.outer(mean, mean)) / (n - 1)
+    assert abs(n - 50000) < 0.5
+    assert torch.allclose(mean, torch.full_like(mean, 0.5), atol=0.01)
+    assert torch.allclose(torch.diagonal(cov), torch.full((64,), 1 / 12, dtype=torch.float64, device=cuda), atol=0.003)
+    off = cov - torch.diag(torch.diagonal(cov))
+    assert off.abs().max() < 0.003
+
+
+def test_covariance_gpu_matches_cpu(cuda):
+    from harp_amd.models import stats as ST
+
+    X = torch.randn(5000, 30, dtype=torch.float64) * 3 + 1
+    g = ST.covariance(X.to(cuda).float())
+    c = ST.covariance(X.to(torch.bfloat16).double())
+    assert torch.allclose(g["covariance"].cpu(), c["covariance"], rtol=1e-3, atol=1e-3)

@@ -1,0 +1,148 @@
+"""DAAL-family distributed partial results on 2 gloo workers vs single-process numpy /
+scipy / sklearn on the full data (covariance, moments, PCA x2, TSQR/SVD, normalization,
+outliers, linear/ridge regression (normal eq + QR), quality metrics, Naive Bayes)."""
+import numpy as np
+import pytest
+import torch
+
+from harp_amd.models import naive_bayes as NB
+from harp_amd.models import regression as RG
+from harp_amd.models import stats as ST
+from harp_amd.runtime.launcher import launch
+
+
+def _data(seed=0, n=400, d=6):
+    g = torch.Generator().manual_seed(seed)
+    A = torch.randn(d, d, generator=g, dtype=torch.float64)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64) @ A + torch.arange(d, dtype=torch.float64)
+    beta = torch.randn(d, generator=g, dtype=torch.float64)
+    y = X @ beta + 0.5 + 0.01 * torch.randn(n, generator=g, dtype=torch.float64)
+    cls = (X[:, 0] > X[:, 0].median()).long() + (X[:, 1] > X[:, 1].median()).long()
+    counts = torch.poisson(torch.rand(n, 12, generator=g) * 3 + cls[:, None].double() * torch.linspace(0, 2, 12))
+    return X, y, cls, counts
+
+
+def _job(comm, X, y, cls, counts):
+    P, r = comm.world_size, comm.rank
+    n = X.shape[0]
+    sl = slice(r * n // P, (r + 1) * n // P)
+    Xs, ys, cs, ks = X[sl], y[sl], cls[sl], counts[sl]
+    out = {}
+    out["cov"] = ST.covariance(Xs, comm)
+    out["cov_csr"] = ST.covariance(Xs.to_sparse_csr(), comm)
+    out["mom"] = ST.low_order_moments(Xs, comm)
+    out["pca_cor"] = ST.pca(Xs, comm, "correlation")
+    out["pca_svd"] = ST.pca(Xs, comm, "svd")
+    q = ST.tsqr(Xs, comm)
+    out["qr_R"], out["qr_Q"] = q["R"], q["Q"]
+    out["svd"] = ST.svd(Xs, comm)
+    out["minmax"] = ST.normalize_minmax(Xs, comm=comm)
+    out["zscore"] = ST.normalize_zscore(Xs, comm=comm)
+    out["uni"] = ST.outliers_univariate(Xs, comm=comm)
+    out["multi"] = ST.outliers_multivariate(Xs, comm=comm)
+    out["lin_ne"] = RG.train_linear(Xs, ys, comm)["beta"]
+    out["lin_qr"] = RG.train_linear(Xs, ys, comm, method="qr")["beta"]
+    out["ridge"] = RG.train_linear(Xs, ys, comm, ridge=3.0)["beta"]
+    out["lrq"] = RG.linreg_quality(Xs, ys, out["lin_ne"], comm)
+    out["nb"] = NB.train(ks, cs, 3, comm)
+    out["nb_csr"] = NB.train(ks.to_sparse_csr(), cs, 3, comm)
+    return out
+
+
+@pytest.fixture(scope="module")
+def results():
+    X, y, cls, counts = _data()
+    res = launch(_job, 2, args=(X, y, cls, counts), timeout=300)
+    return (X, y, cls, counts), res
+
+
+def test_covariance_moments(results):
+    (X, y, cls, counts), res = results
+    Xn = X.numpy()
+    for k in ("cov", "cov_csr"):
+        assert np.allclose(res[0][k]["covariance"].numpy(), np.cov(Xn.T), atol=1e-8)
+        assert np.allclose(res[1][k]["mean"].numpy(), Xn.mean(0))
+    m = res[0]["mom"]
+    assert np.allclose(m["minimum"].numpy(), Xn.min(0)) and np.allclose(m["maximum"].numpy(), Xn.max(0))
+    assert np.allclose(m["variance"].numpy(), Xn.var(0, ddof=1)) and np.allclose(m["sumSquares"].numpy(), (Xn ** 2).sum(0))
+    assert np.allclose(m["standardDeviation"].numpy(), Xn.std(0, ddof=1))
+
+
+def test_pca_both_methods(results):
+    (X, *_), res = results
+    C = np.corrcoef(X.numpy().T)
+    w = np.sort(np.linalg.eigvalsh(C))[::-1]
+    for k in ("pca_cor", "pca_svd"):
+        assert np.allclose(res[0][k]["eigenvalues"].numpy(), w, atol=1e-8)
+    a, b = res[0]["pca_cor"]["eigenvectors"].numpy(), res[0]["pca_svd"]["eigenvectors"].numpy()
+    assert np.allclose(np.abs(a), np.abs(b), atol=1e-6)
+
+
+def test_tsqr_svd(results):
+    (X, *_), res = results
+    Xn = X.numpy()
+    R = res[0]["qr_R"].numpy()
+    assert np.allclose(R.T @ R, Xn.T @ Xn, atol=1e-7) and np.allclose(np.tril(R, -1), 0)
+    Q = np.concatenate([res[0]["qr_Q"].numpy(), res[1]["qr_Q"].numpy()])
+    assert np.allclose(Q @ R, Xn, atol=1e-8) and np.allclose(Q.T @ Q, np.eye(Xn.shape[1]), atol=1e-8)
+    s = np.linalg.svd(Xn, compute_uv=False)
+    assert np.allclose(res[0]["svd"]["singularValues"].numpy(), s)
+    U = np.concatenate([res[0]["svd"]["leftSingularMatrix"].numpy(), res[1]["svd"]["leftSingularMatrix"].numpy()])
+    assert np.allclose(U * s @ res[0]["svd"]["rightSingularMatrix"].numpy(), Xn, atol=1e-8)
+
+
+def test_normalization_outliers(results):
+    (X, *_), res = results
+    Xn = X.numpy()
+    mm = np.concatenate([res[0]["minmax"].numpy(), res[1]["minmax"].numpy()])
+    assert np.allclose(mm, (Xn - Xn.min(0)) / (Xn.max(0) - Xn.min(0)))
+    z = np.concatenate([res[0]["zscore"].numpy(), res[1]["zscore"].numpy()])
+    assert np.allclose(z, (Xn - Xn.mean(0)) / Xn.std(0, ddof=1))
+    uni = np.concatenate([res[0]["uni"].numpy(), res[1]["uni"].numpy()])
+    assert uni.shape == Xn.shape and uni.mean() > 0.98
+    multi = np.concatenate([res[0]["multi"].numpy(), res[1]["multi"].numpy()])
+    assert multi.mean() > 0.98
+
+
+def test_regressions(results):
+    (X, y, *_), res = results
+    from sklearn.linear_model import LinearRegression, Ridge
+
+    lr = LinearRegression().fit(X.numpy(), y.numpy())
+    ref = np.concatenate([[lr.intercept_], lr.coef_])
+    for k in ("lin_ne", "lin_qr"):
+        assert np.allclose(res[0][k].numpy()[0], ref, atol=1e-7), k
+    rd = Ridge(alpha=3.0).fit(X.numpy(), y.numpy())
+    assert np.allclose(res[1]["ridge"].numpy()[0], np.concatenate([[rd.intercept_], rd.coef_]), atol=1e-6)
+    q = res[0]["lrq"]
+    assert float(q["determinationCoeff"][0]) > 0.999 and float(q["rms"][0]) < 0.02
+
+
+def test_naive_bayes(results):
+    (X, y, cls, counts), res = results
+    from sklearn.naive_bayes import MultinomialNB
+
+    nb = MultinomialNB(alpha=1.0).fit(counts.numpy(), cls.numpy())
+    for k in ("nb", "nb_csr"):
+        m = res[0][k]
+        assert np.allclose(m["logTheta"].numpy(), nb.feature_log_prob_, atol=1e-10)
+        assert np.allclose(m["logPrior"].numpy(), nb.class_log_prior_)
+        assert (NB.predict(counts, m).numpy() == nb.predict(counts.numpy())).all()
+
+
+def test_quality_metrics_and_batch_ops():
+    yt = torch.tensor([0, 1, 2, 2, 1, 0, 2])
+    yp = torch.tensor([0, 2, 2, 2, 1, 0, 1])
+    q = RG.classification_quality(yt, yp, 3)
+    assert q["confusionMatrix"].sum() == 7 and abs(float(q["errorRate"]) - 2 / 7) < 1e-12
+    X = torch.randn(50, 4, dtype=torch.float64)
+    L = ST.cholesky(X.t() @ X)
+    assert torch.allclose(L @ L.t(), X.t() @ X)
+    pq = ST.pivoted_qr(X)
+    assert torch.allclose(pq["Q"] @ pq["R"], X[:, pq["permutation"]])
+    assert torch.equal(ST.sort_features(X), torch.sort(X, 0).values)
+    qs = ST.quantiles(X, (0.25, 0.75))
+    assert torch.allclose(qs, torch.quantile(X, torch.tensor([0.25, 0.75], dtype=torch.float64), dim=0))
+    Xo = torch.cat([torch.randn(200, 3, dtype=torch.float64), torch.full((5, 3), 25.0, dtype=torch.float64)])
+    w = ST.outliers_bacon(Xo)
+    assert w[-5:].sum() == 0 and w[:200].mean() > 0.9
