@@ -22,18 +22,27 @@
 
 namespace {
 
-constexpr int MT = 128;       // macro tile (features)
 constexpr int KT = 64;        // samples per stage
 constexpr int CPR = KT / 8;   // 16-B chunks per LDS row (8)
-constexpr int PANEL_BYTES = MT * KT * 2;  // 16 KiB
 
 __device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-// one 128 x 64 panel of XT (rows r0.., samples k0..) -> LDS, 16 DMA wave-instructions
+// Workgroup geometry: MT x MT output tile; each wave owns (32*BA) x (32*BB).
+template <int MT_, int BA_, int BB_>
+struct SyrkCfg {
+  static constexpr int MT = MT_, BA = BA_, BB = BB_;
+  static constexpr int WR = MT / (32 * BA), WC = MT / (32 * BB);
+  static constexpr int WAVES = WR * WC;
+  static constexpr int PANEL_BYTES = MT * KT * 2;
+  static constexpr int DMA = PANEL_BYTES / 1024;
+};
+
+// one MT x 64 panel of XT (rows r0.., samples k0..) -> LDS via LDS-DMA
+template <class C>
 __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long ld, int r0, long k0, char* lds,
                                             int wave, int lane) {
 #pragma unroll
-  for (int j = wave; j < PANEL_BYTES / 1024; j += 4) {
+  for (int j = wave; j < C::DMA; j += C::WAVES) {
     const int q = j * 64 + lane;          // chunk position in the LDS image
     const int row = q / CPR, cp = q % CPR;
     const int c = swz(row, cp);           // involution: source chunk for this position
@@ -43,15 +52,22 @@ __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long 
   }
 }
 
-__global__ __launch_bounds__(256) void syrk_kernel(const __bf16* __restrict__ XT, long ld, long n, int nt,
-                                                   long chunk, float* __restrict__ G, int ldg) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * PANEL_BYTES];
+template <int MT_, int BA_, int BB_>
+__global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void syrk_kernel(
+    const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg) {
+  using C = SyrkCfg<MT_, BA_, BB_>;
+  constexpr int MT = C::MT, BA = C::BA, BB = C::BB, PANEL = C::PANEL_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[4 * PANEL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  // blockIdx.x -> (upper-triangular tile (ti <= tj), sample split)
+  // XCD-aware remap (bijective): consecutive logical ids share an XCD (blocks b, b+8, ...
+  // are co-located), so the tiles of one sample split hit the same L2
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  const unsigned q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+  const unsigned L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
   const int ntiles = nt * (nt + 1) / 2;
-  const int tile = blockIdx.x % ntiles;
-  const long split = blockIdx.x / ntiles;
+  const int tile = L % ntiles;
+  const long split = L / ntiles;
   int ti = 0, rem = tile;
   while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
   const int tj = ti + rem;
@@ -60,45 +76,46 @@ __global__ __launch_bounds__(256) void syrk_kernel(const __bf16* __restrict__ XT
   long kend = kbeg + chunk;
   if (kend > n) kend = n;
   if (kbeg >= kend) return;
-  const int wr = wave >> 1, wc = wave & 1;  // this wave's 64x64 sub-tile
-  floatx16 acc[2][2];
+  const int wr = wave / C::WC, wc = wave % C::WC;
+  floatx16 acc[BA][BB];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < BA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int bb = 0; bb < BB; ++bb)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
+      for (int v = 0; v < 16; ++v) acc[a][bb][v] = 0.f;
 
   // buffers: A[c] = smem + c*PANEL, B[c] = smem + (2+c)*PANEL
-  stage_panel(XT, ld, ti * MT, kbeg, smem, wave, lane);
-  if (!diag) stage_panel(XT, ld, tj * MT, kbeg, smem + 2 * PANEL_BYTES, wave, lane);
+  stage_panel<C>(XT, ld, ti * MT, kbeg, smem, wave, lane);
+  if (!diag) stage_panel<C>(XT, ld, tj * MT, kbeg, smem + 2 * PANEL, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int cur = 0;
   for (long k0 = kbeg; k0 < kend; k0 += KT) {
     if (k0 + KT < kend) {
-      stage_panel(XT, ld, ti * MT, k0 + KT, smem + (cur ^ 1) * PANEL_BYTES, wave, lane);
-      if (!diag) stage_panel(XT, ld, tj * MT, k0 + KT, smem + (2 + (cur ^ 1)) * PANEL_BYTES, wave, lane);
+      stage_panel<C>(XT, ld, ti * MT, k0 + KT, smem + (cur ^ 1) * PANEL, wave, lane);
+      if (!diag) stage_panel<C>(XT, ld, tj * MT, k0 + KT, smem + (2 + (cur ^ 1)) * PANEL, wave, lane);
     }
-    const char* A = smem + cur * PANEL_BYTES;
-    const char* B = diag ? A : smem + (2 + cur) * PANEL_BYTES;
+    const char* A = smem + cur * PANEL;
+    const char* B = diag ? A : smem + (2 + cur) * PANEL;
 #pragma unroll
     for (int s = 0; s < KT / 16; ++s) {
-      bf16x8 af[2], bfr[2];
+      bf16x8 af[BA], bfr[BB];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int row = wr * 64 + a * 32 + r;
+      for (int a = 0; a < BA; ++a) {
+        const int row = wr * (32 * BA) + a * 32 + r;
         af[a] = *(const bf16x8*)(A + row * (CPR * 16) + swz(row, 2 * s + h) * 16);
       }
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int row = wc * 64 + b * 32 + r;
-        bfr[b] = *(const bf16x8*)(B + row * (CPR * 16) + swz(row, 2 * s + h) * 16);
+      for (int bb = 0; bb < BB; ++bb) {
+        const int row = wc * (32 * BB) + bb * 32 + r;
+        bfr[bb] = *(const bf16x8*)(B + row * (CPR * 16) + swz(row, 2 * s + h) * 16);
       }
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < BA; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int bb = 0; bb < BB; ++bb)
+          acc[a][bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[bb], acc[a][bb], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -106,15 +123,16 @@ __global__ __launch_bounds__(256) void syrk_kernel(const __bf16* __restrict__ XT
   }
   // D[i][j]: lane holds col = lane&31, rows (v&3) + 8*(v>>2) + 4h of each 32x32 block
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < BA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int i0 = ti * MT + wr * 64 + a * 32;
-      const int j0 = tj * MT + wc * 64 + b * 32;
+    for (int bb = 0; bb < BB; ++bb) {
+      const int i0 = ti * MT + wr * (32 * BA) + a * 32;
+      const int j0 = tj * MT + wc * (32 * BB) + bb * 32;
+      if (diag && i0 > j0 + 31) continue;  // strictly-lower block of a diagonal tile: unused
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int row = (v & 3) + 8 * (v >> 2) + 4 * h;
-        atomicAdd(G + (long)(i0 + row) * ldg + j0 + r, acc[a][b][v]);
+        atomicAdd(G + (long)(i0 + row) * ldg + j0 + r, acc[a][bb][v]);
       }
     }
 }
@@ -147,20 +165,30 @@ __global__ void to_feature_major_kernel(const __bf16* __restrict__ X, long n, in
 
 }  // namespace
 
-// G[d_pad][ldg] (+)= XT XT^T, upper 128-tiles only; XT [d_pad][ld] bf16, d_pad % 128 == 0,
-// n % 64 == 0 (zero-padded samples), ld >= n, ld % 8 == 0.
-HARP_EXPORT int harp_syrk_t_bf16(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits,
-                                 hipStream_t s) {
-  if (d_pad % MT || n % KT || ld < n || ld % 8 || ldg < d_pad) return HARP_EBADARG;
-  if (n == 0) return HARP_OK;
+template <int MT, int BA, int BB>
+static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits, int target_wg,
+                       hipStream_t s) {
+  using C = SyrkCfg<MT, BA, BB>;
   const int nt = d_pad / MT;
   const int ntiles = nt * (nt + 1) / 2;
-  if (num_splits <= 0) num_splits = (2048 + ntiles - 1) / ntiles;
+  if (num_splits <= 0) num_splits = (target_wg + ntiles - 1) / ntiles;
   long chunk = (n + num_splits - 1) / num_splits;
   chunk = (chunk + KT - 1) / KT * KT;
   const long splits = (n + chunk - 1) / chunk;
-  syrk_kernel<<<dim3((unsigned)(ntiles * splits)), dim3(256), 0, s>>>((const __bf16*)XT, ld, n, nt, chunk, G, ldg);
+  syrk_kernel<MT, BA, BB><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
+      (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
   return harp_launch_status();
+}
+
+// G[d_pad][ldg] (+)= XT XT^T over the upper tiles; XT [d_pad][ld] bf16, d_pad % 128 == 0,
+// n % 64 == 0 (zero-padded samples), ld >= n, ld % 8 == 0. 256x256 tiles (8 waves) when
+// d_pad % 256 == 0 and d_pad >= 512 (half the operand re-reads), else 128x128 (4 waves).
+HARP_EXPORT int harp_syrk_t_bf16(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits,
+                                 hipStream_t s) {
+  if (d_pad % 128 || n % KT || ld < n || ld % 8 || ldg < d_pad) return HARP_EBADARG;
+  if (n == 0) return HARP_OK;
+  if (d_pad >= 512 && d_pad % 256 == 0) return launch_syrk<256, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+  return launch_syrk<128, 2, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 2048, s);
 }
 
 HARP_EXPORT int harp_to_feature_major_bf16(const void* X, long n, int d, long ldx, void* XT, long ld, int d_pad,
