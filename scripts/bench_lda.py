@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""LDA-CGS bench (BASELINE config #5: 1M docs x 1M vocab x 1000 topics): sampled
+tokens/sec and seconds per iteration with word-slice model rotation. Strong scaling.
+
+python scripts/bench_lda.py [--docs 1e6] [--vocab 1e6] [--topics 1000] [--len 100] [--iters 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=float, default=1e6)
+    ap.add_argument("--vocab", type=float, default=1e6)
+    ap.add_argument("--topics", type=int, default=1000)
+    ap.add_argument("--len", type=int, default=100)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args()
+    import torch
+
+    from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, synthetic_corpus
+    from harp_amd.runtime.launcher import init_distributed, shutdown
+    from harp_amd.runtime.mapper import KeyValReader
+
+    comm = init_distributed()
+    nd, V = int(a.docs), int(a.vocab)
+    t0 = time.perf_counter()
+    toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
+    gen = time.perf_counter() - t0
+    cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters)
+    m = LDACollectiveMapper(comm, cfg, nd, V, toks)
+    t0 = time.perf_counter()
+    m.init_model(KeyValReader([]))
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    ll0 = m.log_likelihood(-1)
+    for it in range(a.warmup):
+        m.iterate(it)
+    m.rot.wait_all()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    n = 0
+    for it in range(a.warmup, a.warmup + a.iters):
+        n += m.iterate(it)
+    m.rot.wait_all()
+    torch.cuda.synchronize()
+    comm.barrier()
+    dt = time.perf_counter() - t0
+    ll = m.log_likelihood(a.warmup + a.iters)
+    tot = torch.tensor([float(n)], dtype=torch.float64, device=comm.device)
+    if comm.world_size > 1:
+        comm.all_reduce(tot)
+    if comm.rank == 0:
+        print(json.dumps({"metric": "LDA-CGS sampled tokens/sec (model rotation)", "value": float(tot.item()) / dt,
+                          "unit": "tokens/s", "s_per_iter": dt / a.iters, "n_gpus": comm.world_size,
+                          "docs": nd, "vocab": V, "topics": a.topics, "tokens": int(tot.item()) // a.iters,
+                          "loglik_init": ll0, "loglik_end": ll, "init_s": init_s, "gen_s": gen}), flush=True)
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,42 @@
+"""LDA-CGS with rotation on CPU/gloo. The reference gate (ml/java/test_scripts/lda.sh:57,66:
+nytimes-30K, K=1000, 200 iterations, log-likelihood > -6.03e7) needs nytimes-30K.mrlda,
+missing from the reference checkout (.MISSING_LARGE_BLOBS): parity is unpinned; we check
+likelihood improvement on a synthetic corpus and P-invariance of the result."""
+import pytest
+import torch
+
+from harp_amd.models.lda import LDAConfig, run_lda, synthetic_corpus
+from harp_amd.ops import lda as L
+from harp_amd.runtime.launcher import launch
+
+
+def _job(comm, cfg, nd, V, toks):
+    return run_lda(comm, cfg, nd, V, toks)
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    return synthetic_corpus(300, 400, 8, 40, seed=1)
+
+
+def test_chunks():
+    w = torch.tensor([0, 0, 0, 0, 0, 1, 2, 2, 2])
+    assert L.build_chunks(w, 2).tolist() == [0, 2, 4, 5, 6, 8, 9]
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_lda_rotation_improves(corpus, P):
+    cfg = LDAConfig(num_topics=10, alpha=0.1, beta=0.01, iterations=20, print_interval=10, num_slices=2)
+    res = launch(_job, P, args=(cfg, 300, 400, corpus), timeout=300)
+    ll = [v for _, v in res[0]["loglik"]]
+    assert ll[-1] > ll[0] and all(r["loglik"] == res[0]["loglik"] for r in res)
+    test_lda_rotation_improves.ll = getattr(test_lda_rotation_improves, "ll", {})
+    test_lda_rotation_improves.ll[P] = ll[-1]
+
+
+def test_lda_p_invariance(corpus):
+    cfg = LDAConfig(num_topics=10, alpha=0.1, beta=0.01, iterations=30, print_interval=30)
+    one = launch(_job, 1, args=(cfg, 300, 400, corpus))[0]["loglik"][-1][1]
+    two = launch(_job, 2, args=(cfg, 300, 400, corpus), timeout=300)[0]["loglik"][-1][1]
+    n_tok = corpus[0].numel()
+    assert abs(one - two) / n_tok < 0.05, (one, two)  # per-token log-likelihood agrees
