@@ -1,0 +1,290 @@
+"""Graph applications: PageRank and subgraph counting by color coding (FASCIA / SAHAD).
+
+References:
+  * contrib/src/main/java/edu/iu/simplepagerank/PageRankMapper.java:44-190 — adjacency
+    lines ``src dst...`` loaded per worker; PR initialised to 1/N and allgathered; per
+    iteration every worker adds PR(src)/outdeg to its targets (dangling pages spread
+    PR/N to all pages) into a Long2Double KV table, the table is allreduced, and
+    ``PR = 0.85 * sum + 0.15 / N``.
+  * ml/java/.../subgraph/SCCollectiveMapper.java + colorcount_HJ.java (FASCIA color
+    coding: random k-coloring, dynamic programming over a decomposition of the tree
+    template into active / passive children, tables of counts per (vertex, color set);
+    remote neighbour tables exchanged with regroup / allreduce) and
+    ml/java/.../sahad/rotation*/SCCollectiveMapper.java (SAHAD: the passive-child tables
+    rotate around the ring instead).
+
+MI355X design:
+  * PageRank: edges stay source-partitioned; a step is one scatter-add SpMV into a dense
+    length-N vector plus the dangling mass, then ONE reduce-scatter (each worker
+    finalises its slice of pages) and ONE all-gather — half the bytes of the
+    reference's allreduce of a KV table, and no hashing.
+  * Color coding: count tables are dense [n_vertices, C(k, s)] fp64 matrices (color sets
+    in combinatorial-number order); the neighbour sum of a passive table is a sparse x
+    dense product, and the active x passive color-set convolution is a gather-multiply
+    over a precomputed (C, C1, C \\ C1) index list followed by one scatter-add — all
+    vectorised over vertices. Remote passive rows arrive by all-gather ("allgather",
+    FASCIA-like) or by rotating row slabs around the ring with async p2p ("rotation",
+    SAHAD-like) so the partial SpMM overlaps the next slab's transfer.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import random
+import time
+from functools import lru_cache
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..parallel.comm import Communicator
+from .common import gather_rows
+
+
+# ---------------------------------------------------------------- input
+def parse_adjacency(lines: Sequence[str]) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """``src dst dst ...`` lines -> (src, dst) edge arrays and the list of listed sources."""
+    src, dst, nodes = [], [], []
+    for ln in lines:
+        tok = ln.split()
+        if not tok:
+            continue
+        s = int(tok[0])
+        nodes.append(s)
+        for t in tok[1:]:
+            src.append(s)
+            dst.append(int(t))
+    return torch.tensor(src, dtype=torch.long), torch.tensor(dst, dtype=torch.long), torch.tensor(nodes, dtype=torch.long)
+
+
+# ---------------------------------------------------------------- PageRank
+def pagerank(comm: Communicator, src: torch.Tensor, dst: torch.Tensor, nodes: torch.Tensor, num_urls: int,
+             iterations: int = 10, damping: float = 0.85) -> torch.Tensor:
+    """``nodes``: pages whose adjacency lists this worker loaded (every page appears in
+    exactly one worker's list); (src, dst): their out-edges. Returns the full PR vector
+    on every worker."""
+    P, me, dev = comm.world_size, comm.rank, comm.device
+    N = num_urls
+    src, dst, nodes = src.to(dev), dst.to(dev), nodes.to(dev)
+    outdeg = torch.zeros(N, dtype=torch.float64, device=dev)
+    outdeg.index_add_(0, src, torch.ones(src.numel(), dtype=torch.float64, device=dev))
+    dangling = nodes[outdeg[nodes] == 0]
+    pr = torch.full((N,), 1.0 / N, dtype=torch.float64, device=dev)
+    chunk = math.ceil(N / P)
+    Np = chunk * P
+    for _ in range(iterations):
+        contrib = torch.zeros(Np, dtype=torch.float64, device=dev)
+        contrib.index_add_(0, dst, pr[src] / outdeg[src])
+        contrib[:N] += pr[dangling].sum() / N
+        if P > 1:
+            mine = torch.empty(chunk, dtype=torch.float64, device=dev)
+            comm.reduce_scatter(mine, contrib)
+            mine = damping * mine + (1 - damping) / N
+            full = torch.empty(Np, dtype=torch.float64, device=dev)
+            comm.all_gather_into(full, mine)
+            pr = full[:N]
+        else:
+            pr = damping * contrib[:N] + (1 - damping) / N
+    return pr
+
+
+# ---------------------------------------------------------------- color coding
+class Template:
+    """A tree template (k vertices, edge list) rooted at vertex 0, decomposed into
+    (vertex, number of children used) sub-templates."""
+
+    def __init__(self, k: int, edges: Sequence[Tuple[int, int]]):
+        self.k = k
+        adj: Dict[int, List[int]] = {v: [] for v in range(k)}
+        for a, b in edges:
+            adj[a].append(b)
+            adj[b].append(a)
+        if len(edges) != k - 1:
+            raise ValueError("template must be a tree")
+        self.children: Dict[int, List[int]] = {}
+        seen = {0}
+        order = [0]
+        for v in order:
+            self.children[v] = [u for u in sorted(adj[v]) if u not in seen]
+            seen.update(self.children[v])
+            order += self.children[v]
+        if len(seen) != k:
+            raise ValueError("template must be connected")
+        self.adj = adj
+
+    def size(self, v: int, j: Optional[int] = None) -> int:
+        ch = self.children[v] if j is None else self.children[v][:j]
+        return 1 + sum(self.size(c) for c in ch)
+
+    def automorphisms(self) -> int:
+        """|Aut(T)| by brute force over vertex permutations (small templates)."""
+        E = {frozenset(e) for e in self._edges()}
+        cnt = 0
+        for p in itertools.permutations(range(self.k)):
+            if all(frozenset((p[a], p[b])) in E for a, b in self._edges()):
+                cnt += 1
+        return cnt
+
+    def _edges(self):
+        return [(v, c) for v in self.children for c in self.children[v]]
+
+
+@lru_cache(maxsize=None)
+def _colorsets(k: int, s: int):
+    sets = list(itertools.combinations(range(k), s))
+    return sets, {c: i for i, c in enumerate(sets)}
+
+
+@lru_cache(maxsize=None)
+def _split_index(k: int, sa: int, sp: int):
+    """Index triples (C, C1, C2) with |C1| = sa, C2 = C \\ C1, |C| = sa + sp."""
+    s = sa + sp
+    sets, idx = _colorsets(k, s)
+    _, ia = _colorsets(k, sa)
+    _, ip = _colorsets(k, sp)
+    tc, t1, t2 = [], [], []
+    for ci, C in enumerate(sets):
+        for C1 in itertools.combinations(C, sa):
+            C2 = tuple(c for c in C if c not in C1)
+            tc.append(ci)
+            t1.append(ia[C1])
+            t2.append(ip[C2])
+    return torch.tensor(tc), torch.tensor(t1), torch.tensor(t2)
+
+
+def _neighbour_sum(comm: Communicator, adj_src_local: torch.Tensor, adj_dst: torch.Tensor, n_local: int,
+                   M_local: torch.Tensor, owner_rows: torch.Tensor, n_total: int, strategy: str) -> torch.Tensor:
+    """N[v] = sum_{u in N(v)} M[u] for the local vertices v (local row ids in
+    adj_src_local, global neighbour ids in adj_dst)."""
+    P = comm.world_size
+    out = torch.zeros((n_local, M_local.shape[1]), dtype=M_local.dtype, device=M_local.device)
+    if P == 1:
+        out.index_add_(0, adj_src_local, M_local[adj_dst])
+        return out
+    if strategy == "allgather":
+        full = gather_rows(comm, M_local)  # rows in rank order: rank r owns vertices r, r+P, ...
+        counts = [len(range(r, n_total, P)) for r in range(P)]
+        offs = [0]
+        for c in counts:
+            offs.append(offs[-1] + c)
+        owner = adj_dst % P
+        row = torch.tensor(offs[:-1], device=adj_dst.device)[owner] + adj_dst // P
+        out.index_add_(0, adj_src_local, full[row])
+        return out
+    # rotation (SAHAD): slabs of equal size travel the ring; each step adds the edges
+    # whose neighbour lives in the resident slab
+    from ..runtime.dymoro import DeviceRotator
+
+    per = math.ceil(n_total / P)
+    slab = torch.zeros((per, M_local.shape[1]), dtype=M_local.dtype, device=M_local.device)
+    slab[:n_local] = M_local
+    rot = DeviceRotator(comm, [slab], name="sc-rot")
+    owner = adj_dst % P
+    ring = [(r + 1) % P for r in range(P)]
+    for s in range(P):
+        cur = rot.get(0)
+        src_rank = (comm.rank - s) % P
+        m = owner == src_rank
+        out.index_add_(0, adj_src_local[m], cur[adj_dst[m] // P])
+        if s < P - 1:
+            rot.start(0, ring)
+    return out
+
+
+def color_count(comm: Communicator, template: Template, src: torch.Tensor, dst: torch.Tensor, n_vertices: int,
+                colors: torch.Tensor, strategy: str = "allgather") -> float:
+    """Number of colorful embeddings (maps T -> G with all k colors distinct) for the
+    given coloring. Each worker owns vertices v with v % P == rank and passes the edges
+    (both directions) whose source it owns."""
+    P, me, dev = comm.world_size, comm.rank, comm.device
+    k = template.k
+    own = torch.arange(me, n_vertices, P, device=dev)
+    n_local = own.numel()
+    src, dst = src.to(dev), dst.to(dev)
+    keep = (src % P) == me
+    s_loc, d_glob = src[keep] // P, dst[keep]
+    my_col = colors.to(dev)[own]
+    base = torch.zeros((n_local, k), dtype=torch.float64, device=dev)
+    base[torch.arange(n_local, device=dev), my_col] = 1.0  # size-1 sets are {c} -> index c
+    memo: Dict[Tuple[int, int], torch.Tensor] = {}
+
+    def table(v: int, j: int) -> torch.Tensor:
+        key = (v, j)
+        if key in memo:
+            return memo[key]
+        if j == 0:
+            memo[key] = base
+            return base
+        c = template.children[v][j - 1]
+        A = table(v, j - 1)
+        Pm = table(c, len(template.children[c]))
+        sa, sp = template.size(v, j - 1), template.size(c)
+        Np = _neighbour_sum(comm, s_loc, d_glob, n_local, Pm, own, n_vertices, strategy)
+        tc, t1, t2 = (t.to(dev) for t in _split_index(k, sa, sp))
+        out = torch.zeros((n_local, len(_colorsets(k, sa + sp)[0])), dtype=torch.float64, device=dev)
+        step = max(1, (1 << 24) // max(1, tc.numel()))
+        for a in range(0, n_local, step):
+            b = min(n_local, a + step)
+            out[a:b].index_add_(1, tc, A[a:b, t1] * Np[a:b, t2])
+        memo[key] = out
+        return out
+
+    full = table(0, len(template.children[0]))
+    tot = full.sum().reshape(1)
+    if P > 1:
+        from .common import reduce_partials
+
+        tot = reduce_partials(comm, {"t": tot})["t"]
+    return float(tot[0])
+
+
+def count_subgraphs(comm: Communicator, template: Template, src: torch.Tensor, dst: torch.Tensor, n_vertices: int,
+                    iterations: int = 10, seed: int = 0, strategy: str = "allgather") -> Dict[str, float]:
+    """Color-coding estimate of the number of (non-induced) copies of ``template``:
+    mean colorful count * k^k / k! / |Aut(T)| over ``iterations`` random colorings
+    (the same colorings on every worker)."""
+    k = template.k
+    g = torch.Generator().manual_seed(seed)
+    scale = k ** k / math.factorial(k) / template.automorphisms()
+    vals = []
+    t0 = time.perf_counter()
+    for _ in range(iterations):
+        colors = torch.randint(0, k, (n_vertices,), generator=g)
+        vals.append(color_count(comm, template, src, dst, n_vertices, colors, strategy) * scale)
+    return {"estimate": sum(vals) / len(vals), "samples": vals, "time_s": time.perf_counter() - t0}
+
+
+def brute_force_embeddings(template: Template, edges: Sequence[Tuple[int, int]], n: int,
+                           colors: Optional[Sequence[int]] = None) -> int:
+    """Exact count of (colorful, if colors given) injective homomorphisms T -> G."""
+    adj = [set() for _ in range(n)]
+    for a, b in edges:
+        if a != b:
+            adj[a].add(b)
+            adj[b].add(a)
+    order = [0]
+    parent = {0: None}
+    for v in order:
+        for c in template.children[v]:
+            parent[c] = v
+            order.append(c)
+    cnt = 0
+
+    def rec(i, amap, used):
+        nonlocal cnt
+        if i == len(order):
+            if colors is None or len({colors[x] for x in amap.values()}) == template.k:
+                cnt += 1
+            return
+        t = order[i]
+        cand = range(n) if parent[t] is None else adj[amap[parent[t]]]
+        for x in cand:
+            if x not in used:
+                amap[t] = x
+                used.add(x)
+                rec(i + 1, amap, used)
+                used.discard(x)
+                del amap[t]
+
+    rec(0, {}, set())
+    return cnt
