@@ -76,7 +76,8 @@ __device__ __forceinline__ void stage_dma(const __bf16* __restrict__ cm2, int ti
 template <int KS, int G, int WAVES, int RG>
 __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Cm2, long N, int ntiles, int dcount,
-    int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial) {
+    int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial,
+    float* __restrict__ mind) {
   using C = KMCfg<KS, G, WAVES, RG>;
   __shared__ __attribute__((aligned(16))) char smem[2 * C::TILE_BYTES + WAVES * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -173,6 +174,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     if (h == 0 && p < N) {
       labels[p] = idx;
       local_obj += fmaxf(bv + xs, 0.f);
+      if (mind) mind[p] = bv + xs;  // squared distance to the chosen centroid (rotation merge)
     }
   }
   if (obj_partial) {
@@ -277,23 +279,23 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
 
 template <int KS, int G, int WAVES, int RG>
 int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* labels, float* sums, int ld_sums,
-                  float* obj_partial, hipStream_t stream) {
+                  float* obj_partial, float* mind, hipStream_t stream) {
   using C = KMCfg<KS, G, WAVES, RG>;
   if (Kp % C::TILE) return HARP_EBADARG;
   const long nblk = (N + C::PTS - 1) / C::PTS;
   kmeans_assign_kernel<KS, G, WAVES, RG><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
-      (const __bf16*)X, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial);
+      (const __bf16*)X, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial, mind);
   return harp_launch_status();
 }
 
 // variant -> (G, WAVES, RG). Kp must be a multiple of 128 for every variant.
 #define KM_VARIANTS(KS)                                                                       \
   switch (variant) {                                                                        \
-    case 0: return launch_assign<KS, 2, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
-    case 1: return launch_assign<KS, 2, 8, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
-    case 2: return launch_assign<KS, 2, 4, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
-    case 3: return launch_assign<KS, 3, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);  \
-    case 4: return launch_assign<KS, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s); \
+    case 0: return launch_assign<KS, 2, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
+    case 1: return launch_assign<KS, 2, 8, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
+    case 2: return launch_assign<KS, 2, 4, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
+    case 3: return launch_assign<KS, 3, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
+    case 4: return launch_assign<KS, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     default: return HARP_EBADARG;                                                           \
   }
 
@@ -311,7 +313,7 @@ HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
 }
 
 HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, long N, int dp, int Kp, int d, int* labels,
-                                   float* sums, int ld, float* op, int variant, hipStream_t s) {
+                                   float* sums, int ld, float* op, float* md, int variant, hipStream_t s) {
   if (N <= 0 || d + KM_ONES > dp || dp % 16 || Kp <= 0 || Kp % 128) return HARP_EBADARG;
   switch (dp / 16) {
     case 1: KM_VARIANTS(1)
@@ -323,7 +325,7 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, long N, int d
     case 7: KM_VARIANTS(7)
     case 8: KM_VARIANTS(8)
     // wide rows: one 32-point group per wave keeps the X fragments within budget
-#define KM_WIDE(KSV) case KSV: return launch_assign<KSV, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, s);
+#define KM_WIDE(KSV) case KSV: return launch_assign<KSV, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);
     KM_WIDE(9) KM_WIDE(10) KM_WIDE(11) KM_WIDE(12) KM_WIDE(13) KM_WIDE(14) KM_WIDE(15) KM_WIDE(16)
 #undef KM_WIDE
     default: return HARP_EUNSUPPORTED;

@@ -9,7 +9,10 @@ Reference workloads:
     same four strategies (ml/daal/.../daal_kmeans/regroupallgather/
     KMeansDaalCollectiveMapper.java:435-530);
   * kmeans/rotation: centroid partitions rotate through the ring while each worker
-    keeps its points (ml/java/.../kmeans/rotation/KMeansCollectiveMapper.java:106-228).
+    keeps its points (ml/java/.../kmeans/rotation/KMeansCollectiveMapper.java:106-228);
+    here a true model-parallel variant: no worker ever holds all K centroids — the
+    E-step keeps a running argmin over the resident block (kernel min-distance output),
+    the M-step rotates partial-sum slabs back to each block's owner.
 
 MI355X design: points live in HBM as padded bf16 rows (device-generated), one fused
 MFMA kernel does E-step + argmin + accumulation (``ops.kmeans.assign``), the centroid
@@ -144,6 +147,8 @@ class KMeansCollectiveMapper(CollectiveMapper):
     def step(self, it: int) -> None:
         """One Lloyd iteration: fused assign+accumulate, model sync, operand prepare."""
         cfg = self.cfg
+        if cfg.strategy == "rotation":
+            return self._rotation_step(it)
         timer = self.metrics.timer
         t_it = time.perf_counter()
         want_obj = cfg.objective_every > 0 and (it % cfg.objective_every == 0 or it == cfg.iterations - 1)
@@ -164,6 +169,8 @@ class KMeansCollectiveMapper(CollectiveMapper):
 
     def finish(self) -> None:
         k = self.cfg.num_centroids
+        if self.cfg.strategy == "rotation" and hasattr(self, "c_rot"):
+            self.c = self._rotation_gather()
         self.centroids = self.c[:k].clone()
         self.labels = self.lab
         self.result = {"objective": self.objective, "centroids": self.centroids.cpu() if self.is_master() else None}
@@ -234,27 +241,83 @@ class KMeansCollectiveMapper(CollectiveMapper):
             for i in range(k):
                 newc[i] = pulled[i][:d]
             return newc
-        if s == "rotation":
-            # all-to-all of partial sums by owner, normalize, then rotate the centroid
-            # blocks around the ring P-1 times so every worker sees every block
-            t = PackedTable(ids, sums, combiner=sumop)
-            t.static_layout = True
-            if not self.regroup("main", f"regroup-{it}", t, part):
-                raise IOError("regroup failed")
-            mine = t.ids
-            lo = mine[0] if mine else 0
-            cs = c[lo:lo + len(mine)]
-            K.normalize(t.buffer, cs, d)
-            block = PackedTable(mine, cs.clone(), combiner=sumop)
-            newc = c.clone()
-            for step in range(self.get_num_workers()):
-                b_ids = block.ids
-                if b_ids:
-                    newc[b_ids[0]:b_ids[0] + len(b_ids)] = block.buffer
-                if step < self.get_num_workers() - 1 and not self.rotate("main", f"rotate-{it}-{step}", block):
-                    raise IOError("rotate failed")
-            return newc
         raise ValueError(s)
+
+    # -- model rotation (ml/java kmeans/rotation) ------------------------------------------
+    def _rotation_init(self) -> None:
+        """Worker r keeps centroid block r ([Kb, d], Kb a multiple of the kernel's 128-row
+        tile) and never holds the whole model; the block and a partial-sum slab rotate on
+        private channels (DeviceRotator) — the model-parallel K-means of
+        kmeans/rotation/KMeansCollectiveMapper.java:106-228 (ExpTask E-step over the
+        resident block with a running argmin, MaxTask M-step accumulation, rotate)."""
+        from ..runtime.dymoro import DeviceRotator
+
+        cfg = self.cfg
+        P, me = self.get_num_workers(), self.get_self_id()
+        self.Kb = K.padded_k(math.ceil(cfg.num_centroids / P))
+        lo = me * self.Kb
+        real = max(0, min(cfg.num_centroids - lo, self.Kb))
+        blk = torch.zeros((self.Kb, cfg.dim), dtype=torch.float32, device=self.device)
+        blk[:real] = self.c[lo:lo + real]
+        self.c_rot = DeviceRotator(self.comm, [blk], name="km-c")
+        self.s_rot = DeviceRotator(self.comm, [torch.zeros((self.Kb, self.dp), dtype=torch.float32,
+                                                           device=self.device)], name="km-s")
+        self.best_d = torch.empty(self.X.shape[0], dtype=torch.float32, device=self.device)
+        self.md = torch.empty_like(self.best_d)
+        self.best_l = torch.empty(self.X.shape[0], dtype=torch.int64, device=self.device)
+        self.full_sums = torch.zeros((self.Kb * P, self.dp), dtype=torch.float32, device=self.device)
+
+    def _rotation_step(self, it: int) -> None:
+        cfg = self.cfg
+        P, me = self.get_num_workers(), self.get_self_id()
+        if not hasattr(self, "c_rot"):
+            self._rotation_init()
+        ring = [(r + 1) % P for r in range(P)]
+        t_it = time.perf_counter()
+        timer = self.metrics.timer
+        with timer.phase("compute"):
+            self.best_d.fill_(float("inf"))
+            self.best_l.fill_(0)
+            for s in range(P):
+                b = (me - s) % P  # block resident at step s (ring)
+                real = max(0, min(cfg.num_centroids - b * self.Kb, self.Kb))
+                cb = self.c_rot.get(0)
+                if real:
+                    op = K.prepare(cb[:real].contiguous(), self.dp)
+                    K.assign(self.X, op, labels=self.lab, want_objective=False, variant=cfg.variant, min_dist=self.md)
+                    better = self.md < self.best_d
+                    self.best_d = torch.where(better, self.md, self.best_d)
+                    self.best_l = torch.where(better, self.lab.long() + b * self.Kb, self.best_l)
+                self.c_rot.start(0, ring)  # after P steps every block is home again
+            from ..ops import segment
+
+            self.full_sums.zero_()
+            perm, start = segment.bucket_labels(self.best_l.to(torch.int32), self.full_sums.shape[0])
+            segment.bucket_rowsum(self.X, perm, start, self.full_sums)
+        with timer.phase("sync"):
+            for s in range(P):
+                b = (me - s) % P
+                slab = self.s_rot.get(0)
+                if s == 0:
+                    slab.zero_()
+                slab += self.full_sums[b * self.Kb:(b + 1) * self.Kb]
+                self.s_rot.start(0, ring)
+            slab = self.s_rot.get(0)  # block ``me``'s complete sums
+            cb = self.c_rot.get(0)
+            K.normalize(slab, cb, cfg.dim)
+        want_obj = cfg.objective_every > 0 and (it % cfg.objective_every == 0 or it == cfg.iterations - 1)
+        if want_obj:
+            ot = self.best_d.double().clamp_min(0).sum().reshape(1)
+            if P > 1:
+                self.comm.all_reduce(ot)
+            self.objective.append(float(ot.item()))
+        self.history.append({"iter": it, "s": time.perf_counter() - t_it})
+
+    def _rotation_gather(self) -> torch.Tensor:
+        from .common import gather_rows
+
+        cb = self.c_rot.get(0)
+        return gather_rows(self.comm, cb)[: self.cfg.num_centroids]
 
 
 def run_kmeans(comm, cfg: KMeansConfig, points=None, init_centroids=None) -> dict:

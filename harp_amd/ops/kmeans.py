@@ -97,12 +97,15 @@ def prepare(c: torch.Tensor, dp: int, out: Optional[CentroidOperand] = None) -> 
 
 def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = None,
            labels: Optional[torch.Tensor] = None, want_objective: bool = True, variant: int = DEFAULT_VARIANT,
-           obj_partial: Optional[torch.Tensor] = None, accumulate: str = "bucket"):
+           obj_partial: Optional[torch.Tensor] = None, accumulate: str = "bucket",
+           min_dist: Optional[torch.Tensor] = None):
     """Assign every point to its nearest centroid; optionally accumulate (x, 1) into
     ``sums`` [Kp, dp] and return the sum of squared distances (0-dim fp64 tensor).
 
     ``accumulate``: "bucket" (labels -> counting sort -> per-centroid row gather-sum,
     deterministic) or "atomic" (fused fp32 atomics in the assign kernel).
+    ``min_dist`` (fp32 [n], optional) receives each point's squared distance to its
+    centroid (used to merge partial argmins across centroid blocks under rotation).
     Returns (labels, objective)."""
     n, dp = X.shape
     dev = X.device
@@ -128,7 +131,8 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
         fused = sums if accumulate == "atomic" else None
         st = lib.harp_kmeans_assign(X.data_ptr(), op.Cm2.data_ptr(), n, dp, op.Cm2.shape[0], op.d,
                                     labels.data_ptr(), _lib.ptr(fused), fused.stride(0) if fused is not None else 0,
-                                    _lib.ptr(obj_partial) if want_objective else None, variant, _lib.stream_ptr(dev))
+                                    _lib.ptr(obj_partial) if want_objective else None, _lib.ptr(min_dist), variant,
+                                    _lib.stream_ptr(dev))
         _lib.check(st, "kmeans_assign")
         if sums is not None and fused is None:
             from . import segment
@@ -145,6 +149,8 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
     dist = op.cn[: op.K].unsqueeze(0) - 2.0 * (x @ C.t())
     lab = dist.argmin(1)
     labels.copy_(lab.to(labels.dtype))
+    if min_dist is not None:
+        min_dist.copy_((dist.gather(1, lab[:, None])[:, 0] + (x * x).sum(1)).to(min_dist.dtype))
     if sums is not None:
         sums[:, : d + 1].index_add_(0, lab, Xf[:, : d + 1])
     obj = None

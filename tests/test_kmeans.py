@@ -70,3 +70,14 @@ def test_kmeans_single_worker_matches_multi():
     one = launch(_job, 1, args=(cfg, x, c0))[0]
     three = launch(_job, 3, args=(cfg, x, c0), timeout=300)[0]
     assert torch.allclose(one["centroids"], three["centroids"], atol=1e-4)
+
+
+def test_kmeans_model_rotation_multi_block():
+    """True model-parallel rotation: K=300 over 3 workers -> blocks of 128 rows, every
+    worker's points meet all three blocks; result equals plain Lloyd."""
+    x, c0 = _data(900, 6, 300, 10.0, seed=11)
+    cfg = KMeansConfig(num_points=300, num_centroids=300, dim=6, iterations=5, strategy="rotation")
+    res = launch(_job, 3, args=(cfg, x, c0), timeout=300)
+    ref = _lloyd(x, c0, 5)
+    for r in res:
+        assert torch.allclose(r["centroids"].double(), ref, atol=1e-3), (r["centroids"].double() - ref).abs().max()
