@@ -21,6 +21,7 @@ import datetime
 import importlib
 import json
 import os
+import pickle
 import socket
 import sys
 import traceback
@@ -71,6 +72,17 @@ def shutdown() -> None:
         dist.destroy_process_group()
 
 
+def _to_cpu(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        t = [_to_cpu(v) for v in obj]
+        return type(obj)(t) if not hasattr(obj, "_fields") else type(obj)(*t)
+    return obj
+
+
 def _worker(rank: int, world: int, port: int, backend: str, target: Callable, args: tuple,
             result_q) -> None:
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
@@ -79,7 +91,9 @@ def _worker(rank: int, world: int, port: int, backend: str, target: Callable, ar
         torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(world, 1)))
         comm = init_distributed(backend)
         res = target(comm, *args)
-        result_q.put((rank, "ok", res))
+        # by-value pickle (not the shared-memory fd reducers of torch.multiprocessing):
+        # the worker may exit before the parent reads, which would strand an fd handle
+        result_q.put((rank, "ok", pickle.dumps(_to_cpu(res))))
     except BaseException as e:  # report to parent, then fail
         result_q.put((rank, "error", f"{e!r}\n{traceback.format_exc()}"))
         raise
@@ -113,7 +127,7 @@ def launch(target: Callable, num_workers: int, args: tuple = (), backend: str = 
             break
         if not q.empty():
             rank, status, val = q.get()
-            (results.__setitem__(rank, val) if status == "ok" else errors.append((rank, val)))
+            (results.__setitem__(rank, pickle.loads(val)) if status == "ok" else errors.append((rank, val)))
         elif all(not p.is_alive() for p in procs) and q.empty():
             break
         else:
