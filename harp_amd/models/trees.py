@@ -167,7 +167,7 @@ class DecisionTree(Writable):
             if not bool(inner.any()):
                 break
             xv = Xd.gather(1, f[node].clamp_min(0)[:, None])[:, 0]
-            node = torch.where(inner, lf + (xv > t[node]).long(), node)
+            node = torch.where(inner, lf + (xv >= t[node]).long(), node)  # training: left <=> x < thr
         return node
 
     def predict_proba(self, X: torch.Tensor) -> torch.Tensor:
@@ -294,12 +294,18 @@ class AdaBoost:
 
 class BrownBoost:
     """Binary BrownBoost (Freund 2001; daal_brownboost): boosting in continuous time with
-    a total time budget ``c``; each round solves for (alpha, t) by Newton's method so the
-    remaining time shrinks while the weighted correlation stays zero."""
+    a total time budget ``c``. Each round picks the weak learner on weights
+    exp(-(r_i + s)^2 / c), then solves for the step (alpha, t): t(alpha) keeps the total
+    potential sum_i (1 - erf((r_i + s) / sqrt(c))) constant, alpha zeroes the weighted
+    correlation of the learner after the step (both by bisection: robust also when the
+    weak learner is nearly perfect). Stops when the remaining time s reaches 0."""
 
-    def __init__(self, c: float = 2.0, max_rounds: int = 100, nu: float = 1e-3, newton_iters: int = 30):
-        self.c, self.max_rounds, self.nu, self.newton_iters = c, max_rounds, nu, newton_iters
+    def __init__(self, c: float = 2.0, max_rounds: int = 100, nu: float = 1e-3, newton_iters: int = 60):
+        self.c, self.max_rounds, self.nu, self.iters = c, max_rounds, nu, newton_iters
         self.learners, self.alphas = [], []
+
+    def _pot(self, z):
+        return (1 - torch.erf(z / math.sqrt(self.c))).sum()
 
     def fit(self, X, y):
         yl = y.long().to(X.device)
@@ -307,41 +313,53 @@ class BrownBoost:
         r = torch.zeros(X.shape[0], dtype=torch.float64, device=X.device)
         s = self.c
         for _ in range(self.max_rounds):
-            if s <= 0:
+            if s <= 1e-9:
                 break
             w = torch.exp(-(r + s) ** 2 / self.c)
             h = DecisionTree("classification", 1, n_bins=256).fit(X, yl, w / w.sum() * X.shape[0], 2)
-            hx = (2 * h.predict(X) - 1).double()
-            u = hx * ys
-            gamma = float((w * u).sum() / w.sum())
-            if gamma <= 0:
+            u = (2 * h.predict(X) - 1).double() * ys
+            if float((w * u).sum()) <= 0:
                 break
-            a, t = min(0.5, gamma), 0.0
-            for _ in range(self.newton_iters):
+            target = self._pot(r + s)
+
+            def t_of(a):
+                lo, hi = 0.0, s
+                if float(self._pot(r + s - hi + a * u)) <= float(target):
+                    return hi
+                for _ in range(self.iters):
+                    mid = 0.5 * (lo + hi)
+                    if float(self._pot(r + s - mid + a * u)) < float(target):
+                        lo = mid
+                    else:
+                        hi = mid
+                return 0.5 * (lo + hi)
+
+            def corr(a):
+                t = t_of(a)
                 z = r + s - t + a * u
-                e = torch.exp(-z * z / self.c)
-                f1 = (e * u).sum()  # weighted correlation after the step -> 0
-                f2 = (e + 0 * u).sum() - torch.exp(-(r + s) ** 2 / self.c).sum()  # potential conserved
-                # Jacobian
-                d1a = (-2 * z / self.c * e * u * u).sum()
-                d1t = (2 * z / self.c * e * u).sum()
-                d2a = (-2 * z / self.c * e * u).sum()
-                d2t = (2 * z / self.c * e).sum()
-                J = torch.tensor([[d1a, d1t], [d2a, d2t]], dtype=torch.float64)
-                F = torch.tensor([f1, f2], dtype=torch.float64)
-                try:
-                    step = torch.linalg.solve(J, F)
-                except RuntimeError:
-                    break
-                a -= float(step[0])
-                t -= float(step[1])
-                t = max(0.0, min(t, s))
-                if float(F.abs().max()) < self.nu:
-                    break
-            if not math.isfinite(a) or a <= 0:
-                break
+                return float((torch.exp(-z * z / self.c) * u).sum()), t
+
+            a_lo, a_hi = 0.0, 1.0
+            g_hi, t_hi = corr(a_hi)
+            while g_hi > 0 and t_hi < s and a_hi < 1e3:
+                a_lo, a_hi = a_hi, a_hi * 2
+                g_hi, t_hi = corr(a_hi)
+            if g_hi > 0:  # time runs out before the correlation vanishes
+                a, t = a_hi, t_hi
+            else:
+                for _ in range(self.iters):
+                    mid = 0.5 * (a_lo + a_hi)
+                    g, _t = corr(mid)
+                    if g > 0:
+                        a_lo = mid
+                    else:
+                        a_hi = mid
+                    if a_hi - a_lo < self.nu * 1e-3:
+                        break
+                a = 0.5 * (a_lo + a_hi)
+                t = t_of(a)
             r = r + a * u
-            s -= max(t, 1e-3)
+            s -= max(t, self.nu)
             self.learners.append(h)
             self.alphas.append(a)
         return self

@@ -1,0 +1,158 @@
+"""Algorithms on the reference's own fixture files (datasets/daal_*; read as text only).
+
+Where the reference ships expected outputs (daal_reg groundTruth, daal_nn groundTruth,
+daal_naive testTruth) we compare to them; elsewhere we compare to sklearn on the same
+file ("parity unpinned" for DAAL's exact numbers: the DAAL native library is not
+available). Skipped when the reference tree is absent (e.g. on the GPU box)."""
+import os
+
+import pytest
+import torch
+
+from harp_amd.models import apriori as AP
+from harp_amd.models import kernels as KF
+from harp_amd.models import regression as RG
+from harp_amd.models import svm as S
+from harp_amd.models import trees as T
+from harp_amd.models import naive_bayes as NB
+from harp_amd.models import kmeans_csr as KC
+from harp_amd.utils import datasets as DS
+
+ROOT = "/root/reference/datasets"
+pytestmark = pytest.mark.skipif(not os.path.isdir(ROOT), reason="reference datasets not present")
+
+
+def P(*a):
+    return os.path.join(ROOT, *a)
+
+
+def test_linear_regression_vs_ground_truth():
+    X, Y = DS.load_features_labels(P("daal_reg", "train"), n_labels=2)
+    Xt, Yt = DS.load_features_labels(P("daal_reg", "test"), n_labels=2)
+    gt = DS.load_dense_csv(P("daal_reg", "groundTruth"))
+    assert X.shape[1] == 10 and gt.shape == Yt.shape
+    beta = RG.train_linear(X, Y)["beta"]  # two responses at once, intercept first
+    assert beta.shape == (2, 11)
+    pred = RG.predict_linear(Xt, beta)
+    # ground truth = the test responses; least squares must explain them closely
+    r2 = 1 - ((pred - gt) ** 2).sum(0) / ((gt - gt.mean(0)) ** 2).sum(0)
+    assert bool((r2 > 0.99).all()), r2
+
+
+def test_decision_tree_and_forest_vs_sklearn():
+    from sklearn.tree import DecisionTreeClassifier
+
+    X, y = DS.load_features_labels(P("daal_dtree", "train"))
+    Xt, yt = DS.load_features_labels(P("daal_dtree", "test"))
+    y, yt = y.long(), yt.long()
+    ours = (T.DecisionTree(max_depth=10, n_bins=256).fit(X, y).predict(Xt) == yt).double().mean().item()
+    ref = DecisionTreeClassifier(max_depth=10, random_state=0).fit(X.numpy(), y.numpy()).score(Xt.numpy(), yt.numpy())
+    assert ours > ref - 0.05
+    Xf, yf = DS.load_features_labels(P("daal_dforest", "clsdensebatch", "train"))
+    Xft, yft = DS.load_features_labels(P("daal_dforest", "clsdensebatch", "test"))
+    f = T.DecisionForest(n_trees=30, max_depth=12).fit(Xf, yf.long())
+    assert (f.predict(Xft) == yft.long()).double().mean() > 0.75  # sklearn RF(30, depth 12): 0.867
+
+
+def test_boosting_datasets():
+    X, y = DS.load_features_labels(P("daal_adaboost", "train"))
+    Xt, yt = DS.load_features_labels(P("daal_adaboost", "test"))
+    yb, ybt = (y > 0).long(), (yt > 0).long()  # labels are {-1, +1}
+    ada = T.AdaBoost(30).fit(X, yb)
+    assert (ada.predict(Xt) == ybt).double().mean() > 0.8
+    X, y = DS.load_features_labels(P("daal_logitboost", "train"))
+    Xt, yt = DS.load_features_labels(P("daal_logitboost", "test"))
+    lb = T.LogitBoost(20).fit(X, y.long())
+    st = T.stump(X, y.long())
+    assert (lb.predict(Xt) == yt.long()).double().mean() > (st.predict(Xt) == yt.long()).double().mean()
+    X, y = DS.load_features_labels(P("daal_brownboost", "train"))
+    Xt, yt = DS.load_features_labels(P("daal_brownboost", "test"))
+    bb = T.BrownBoost(c=2.0, max_rounds=40).fit(X, (y > 0).long())
+    assert (bb.predict(Xt) == (yt > 0).long()).double().mean() > 0.8
+
+
+def test_svm_multiclass_vs_sklearn():
+    from sklearn.svm import SVC
+
+    X, y = DS.load_features_labels(P("daal_svm", "multidense", "train"))
+    Xt, yt = DS.load_features_labels(P("daal_svm", "multidense", "test"))
+    K = int(y.max()) + 1
+    m = S.MultiClassSVM(K, C=1.0, kernel="linear").fit(X[:600], y[:600].long())
+    ours = (m.predict(Xt[:400]) == yt[:400].long()).double().mean().item()
+    ref = SVC(C=1.0, kernel="linear").fit(X[:600].numpy(), y[:600].numpy()).score(Xt[:400].numpy(), yt[:400].numpy())
+    assert ours > ref - 0.03
+
+
+def test_knn_vs_sklearn():
+    from sklearn.neighbors import KNeighborsClassifier
+
+    X, y = DS.load_features_labels(P("daal_knn", "batchdense", "train"))
+    Xt, yt = DS.load_features_labels(P("daal_knn", "batchdense", "test"))
+    ours = KF.KNNClassifier(5).fit(X, y.long()).predict(Xt)
+    ref = KNeighborsClassifier(5).fit(X.numpy(), y.numpy()).predict(Xt.numpy())
+    assert (ours.numpy() == ref).mean() > 0.97
+
+
+def test_naive_bayes_csr_vs_truth():
+    files = DS.list_files(P("daal_naive", "csrdistri", "train"))
+    # train CSR files: 3 CSR lines followed by one label per row
+    Xs, ys = [], []
+    for fn in files:
+        with open(fn) as f:
+            lines = [ln for ln in f if ln.strip()]
+        Xs.append(_csr_from_lines(lines[:3]))
+        ys.append(torch.tensor([int(float(x)) for x in lines[3:]]))
+    ncol = max(x.shape[1] for x in Xs)
+    X = torch.cat([_pad_cols(x, ncol).to_dense() for x in Xs])
+    y = torch.cat(ys)
+    assert X.shape[0] == y.numel()
+    Xt = DS.load_daal_csr(P("daal_naive", "csrdistri", "test", "naivebayes_test_csr.csv"), ncol).to_dense()
+    yt = DS.load_dense_csv(P("daal_naive", "csrdistri", "testTruth")).reshape(-1).long()
+    C = int(y.max()) + 1
+    model = NB.train(X.to_sparse_csr(), y, C)
+    acc = (NB.predict(Xt, model) == yt).double().mean().item()
+    from sklearn.naive_bayes import MultinomialNB
+
+    ref = MultinomialNB().fit(X.numpy(), y.numpy()).score(Xt.numpy(), yt.numpy())
+    assert abs(acc - ref) < 0.02
+
+
+def _csr_from_lines(lines):
+    import numpy as np
+
+    ro = np.array([int(x) for x in lines[0].strip().rstrip(",").split(",")]) - 1
+    ci = np.array([int(x) for x in lines[1].strip().rstrip(",").split(",")]) - 1
+    va = np.array([float(x) for x in lines[2].strip().rstrip(",").split(",")])
+    return torch.sparse_csr_tensor(torch.from_numpy(ro), torch.from_numpy(ci), torch.from_numpy(va),
+                                   size=(len(ro) - 1, int(ci.max()) + 1))
+
+
+def _pad_cols(x, n):
+    return torch.sparse_csr_tensor(x.crow_indices(), x.col_indices(), x.values(), size=(x.shape[0], n))
+
+
+def test_kmeans_csr_file():
+    X = DS.load_daal_csr(P("daal_kmeans", "csrdistri", "kmeans_csr_1.csv"))
+    C0 = KC.kmeans_init(X, 20, method="first")
+    out = KC.kmeans_sparse(X, C0, 5)
+    dense = KC.kmeans_sparse(X.to_dense(), C0, 5)
+    assert torch.allclose(out["centroids"], dense["centroids"], atol=1e-8)
+    assert out["objective"][-1] <= out["objective"][0]
+
+
+def test_apriori_file():
+    A = DS.load_dense_csv(P("daal_ar", "batchdense", "train")).long()
+    T_ = AP.incidence(A[:, 0], A[:, 1], int(A[:, 1].max()) + 1)
+    out = AP.apriori(T_, min_support=0.001, min_confidence=0.7, max_len=3)
+    assert len(out["large_itemsets"]) > 0
+    for a, c, conf, s in out["rules"]:
+        assert conf >= 0.7 and s >= 0.001
+
+
+def test_em_gmm_file():
+    from sklearn.mixture import GaussianMixture
+
+    X = DS.load_dense_csv(P("daal_em", "batchdense", "train"))
+    m = KF.em_gmm(X, 2, n_iterations=200, accuracy_threshold=1e-10)
+    sk = GaussianMixture(2, reg_covar=1e-6, tol=1e-10, max_iter=200, n_init=5, random_state=0).fit(X.numpy())
+    assert float(m["loglik"]) >= sk.score(X.numpy()) - 0.05
