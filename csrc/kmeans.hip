@@ -73,7 +73,7 @@ __device__ __forceinline__ void stage_dma(const __bf16* __restrict__ cm2, int ti
   }
 }
 
-template <int KS, int G, int WAVES, int RG>
+template <int KS, int G, int WAVES, int RG, int PIPE>
 __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Cm2, long N, int ntiles, int dcount,
     int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial,
@@ -122,6 +122,46 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     bf16x8 af[2][KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) af[0][s] = *(const bf16x8*)(buf + aoff[s]);
+    if constexpr (PIPE > 0) {
+      // software pipeline over the stage's RG*G (row group, point group) items: the MFMA
+      // chain of item i+1 is issued before the argmin epilogue of item i, so the epilogue's
+      // VALU work fills the MFMA gaps instead of waiting on the chain's tail latency
+      constexpr int NI = RG * G;
+      floatx16 acc[2];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[0][q] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][s], xf[0][s], acc[0], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int rg = i / G, g = i % G;
+        if (g == 0 && rg + 1 < RG) {
+          const char* nb = buf + (rg + 1) * 32 * C::CPR * 16;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) af[(rg + 1) & 1][s] = *(const bf16x8*)(nb + aoff[s]);
+        }
+        if (i + 1 < NI) {
+          const int rg1 = (i + 1) / G, g1 = (i + 1) % G;
+          floatx16& an = acc[(i + 1) & 1];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) an[q] = 0.f;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) an = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg1 & 1][s], xf[g1][s], an, 0, 0, 0);
+        }
+        const floatx16& ac = acc[i & 1];
+        float m = keyed(ac[0], 0u);
+#pragma unroll
+        for (int q = 1; q < 16; ++q) m = fminf(m, keyed(ac[q], (unsigned)q));
+        if (m < best[g]) { best[g] = m; bestt[g] = t * RG + rg; }
+        if constexpr (PIPE == 2) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to 4 VALU
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg) {
       if (rg + 1 < RG) {
@@ -277,13 +317,13 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
   }
 }
 
-template <int KS, int G, int WAVES, int RG>
+template <int KS, int G, int WAVES, int RG, int PIPE = 0>
 int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* labels, float* sums, int ld_sums,
                   float* obj_partial, float* mind, hipStream_t stream) {
   using C = KMCfg<KS, G, WAVES, RG>;
   if (Kp % C::TILE) return HARP_EBADARG;
   const long nblk = (N + C::PTS - 1) / C::PTS;
-  kmeans_assign_kernel<KS, G, WAVES, RG><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
+  kmeans_assign_kernel<KS, G, WAVES, RG, PIPE><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
       (const __bf16*)X, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial, mind);
   return harp_launch_status();
 }
@@ -296,6 +336,20 @@ int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* la
     case 2: return launch_assign<KS, 2, 4, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
     case 3: return launch_assign<KS, 3, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
     case 4: return launch_assign<KS, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 5: return launch_assign<KS, 2, 8, 4, 1>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 6: return launch_assign<KS, 2, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 7: return launch_assign<KS, 2, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 8: return launch_assign<KS, 2, 4, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 9: return launch_assign<KS, 2, 4, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 10: return launch_assign<KS, 2, 8, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 11: return launch_assign<KS, 3, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 12: return launch_assign<KS, 3, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 13: return launch_assign<KS, 4, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 14: return launch_assign<KS, 4, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 15: return launch_assign<KS, 3, 4, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 16: return launch_assign<KS, 4, 4, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 17: return launch_assign<KS, 4, 8, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 18: return launch_assign<KS, 4, 8, 6, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     default: return HARP_EBADARG;                                                           \
   }
 
@@ -308,6 +362,13 @@ HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
     case 2: return 4 * 2 * 32;
     case 3: return 8 * 3 * 32;
     case 4: return 16 * 1 * 32;
+    case 5: case 6: case 7: return 8 * 2 * 32;
+    case 8: case 9: return 4 * 2 * 32;
+    case 10: return 8 * 2 * 32;
+    case 11: case 12: return 8 * 3 * 32;
+    case 13: case 14: case 17: case 18: return 8 * 4 * 32;
+    case 15: return 4 * 3 * 32;
+    case 16: return 4 * 4 * 32;
     default: return -1;
   }
 }

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--d", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--acc", default="none,atomic,bucket")
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
     n = int(a.n)
     dev = torch.device("cuda", 0)
@@ -33,7 +35,7 @@ def main():
     res = {}
     for _ in range(a.rounds):
         for v in variants:
-            for acc in ("none", "atomic", "bucket"):
+            for acc in a.acc.split(","):
                 kw = dict(sums=None if acc == "none" else sums, labels=lab, want_objective=False, variant=v,
                           accumulate=acc if acc != "none" else "bucket")
                 K.assign(X, op, **kw)
@@ -47,6 +49,9 @@ def main():
     out = {k: {"ms_min": min(v), "ms_med": sorted(v)[len(v) // 2], "tflops": flops / (min(v) / 1e3) / 1e12}
            for k, v in res.items()}
     print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
