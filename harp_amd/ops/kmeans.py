@@ -27,7 +27,7 @@ from . import _lib
 
 KP_ALIGN = 128
 ONES = 4  # X columns d..d+3 hold 1.0
-DEFAULT_VARIANT = 1
+DEFAULT_VARIANT = 14  # (G4, W8, RG4, pipelined): 1024 points per workgroup
 
 
 def padded_dim(d: int) -> int:
