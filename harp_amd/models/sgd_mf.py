@@ -73,6 +73,13 @@ def synthetic_ratings(n_users: int, n_items: int, n_ratings: int, seed: int = 0,
     return u, it, val.clamp_(1.0, 5.0)
 
 
+def row_owner(users: torch.Tensor, P: int, seed: int = 0) -> torch.Tensor:
+    """Random-but-shared row owner (the reference's RandomPartitioner, seeded from an
+    allreduced seed): a multiplicative hash of the row id, mod P."""
+    h = (users * 2654435761 + seed) % 4294967296
+    return h % P
+
+
 class _Buckets:
     """Ratings of this worker bucketed by global H slice, user-sorted inside a bucket."""
 
@@ -104,10 +111,7 @@ class SGDCollectiveMapper(CollectiveMapper):
 
     # -- partitioning -------------------------------------------------------------------
     def _owner(self, users: torch.Tensor) -> torch.Tensor:
-        # random-but-shared row owner (RandomPartitioner seeded from an allreduced seed)
-        P = self.get_num_workers()
-        h = (users * 2654435761 + self.cfg.seed) % 4294967296
-        return h % P
+        return row_owner(users, self.get_num_workers(), self.cfg.seed)
 
     def init_model(self, reader: KeyValReader) -> None:
         cfg = self.cfg
