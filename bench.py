@@ -35,6 +35,7 @@ def main() -> int:
     ap.add_argument("--dim", type=int, default=100)
     ap.add_argument("--strategy", default="allreduce")
     ap.add_argument("--variant", type=int, default=None)
+    ap.add_argument("--backend", default=None, help="override (e.g. gloo to rehearse >1 rank on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -49,7 +50,12 @@ def main() -> int:
     from harp_amd.runtime.mapper import KeyValReader
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    comm = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
+    backend = args.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    comm = init_distributed(backend)
+    if backend == "gloo" and torch.cuda.is_available():
+        from harp_amd.parallel.comm import Communicator
+
+        comm = Communicator(None, torch.device("cuda", torch.cuda.current_device()))
     if world > 1:
         comm.barrier()  # rank 0's (rare) build finishes before any rank loads the library
     P, rank = comm.world_size, comm.rank
