@@ -37,6 +37,7 @@ class LDAConfig:
     print_interval: int = 5
     seed: int = 0
     max_chunk: int = 2048
+    block_words: int = 4096   # push/pull strategy: words per model partition
 
 
 def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, seed: int = 0, device="cpu"):
@@ -179,5 +180,124 @@ class LDACollectiveMapper(CollectiveMapper):
 
 def run_lda(comm, cfg: LDAConfig, n_docs: int, vocab: int, tokens) -> dict:
     m = LDACollectiveMapper(comm, cfg, n_docs, vocab, tokens)
+    m.run(KeyValReader([]))
+    return m.result
+
+
+class LDAPushPullMapper(LDACollectiveMapper):
+    """LDA-CGS with the word-topic model as a parameter-server table (BASELINE config #5:
+    "push-pull parameter server collective"; the pattern of contrib LDAMapperDyn.java:
+    push :380 / pull :429, applied to the collapsed Gibbs sampler).
+
+    The model is a distributed global :class:`Table` of word blocks (``block_words`` rows
+    x K_pad int32 counts; owner = block id % P, the default Partitioner). Per iteration a
+    worker pulls the blocks its tokens touch into one contiguous device slab, runs the
+    ``lda_cgs`` kernel over all of its tokens against that snapshot (bulk-synchronous
+    staleness, like the reference's stale topic sums), and pushes the count deltas back
+    to the owners, where the SUM combiner merges them; topic-sum deltas are allreduced."""
+
+    def init_model(self, reader: KeyValReader) -> None:
+        from ..core.combiner import ArrCombiner, Operation
+        from ..core.table import Table
+
+        cfg = self.cfg
+        P, me, dev = self.get_num_workers(), self.get_self_id(), self.device
+        K = cfg.num_topics
+        self.Kp = L.padded_topics(K)
+        B = self.B = int(getattr(cfg, "block_words", 0) or 4096)
+        doc, word = self._tokens
+        mine = (doc % P) == me
+        doc, word = doc[mine].to(dev), word[mine].to(dev)
+        self.ndoc_local = (self.n_docs - me + P - 1) // P
+        ldoc = (doc // P).to(torch.int32)
+        blocks = torch.unique(word // B)
+        self.need = blocks.cpu().tolist()
+        lrow = torch.searchsorted(blocks, word // B) * B + word % B
+        order = torch.argsort(lrow)
+        self.tdoc = ldoc[order].contiguous()
+        self.tword = lrow[order].to(torch.int32).contiguous()
+        self.chunk_idx = L.build_chunks(self.tword, cfg.max_chunk)
+        gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
+        self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
+        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=torch.int32, device=dev)
+        slab = torch.zeros((len(self.need) * B, self.Kp), dtype=torch.int32, device=dev)
+        nk = torch.zeros(self.Kp, dtype=torch.int32, device=dev)
+        L.count(self.tdoc, self.tword, self.tz, self.ndk, slab, nk)
+        if P > 1:
+            nk = reduce_partials(self.comm, {"nk": nk}, dtype=torch.float64)["nk"].round().to(torch.int32)
+        self.nk = nk
+        self.sum = ArrCombiner(Operation.SUM)
+        nblocks = math.ceil(self.vocab / B)
+        self.glob = Table(1, self.sum)
+        for b in range(me, nblocks, P):
+            self.glob.add(b, torch.zeros((B, self.Kp), dtype=torch.int32, device=dev))
+        self._push(slab)
+        self.vbeta = self.vocab * cfg.beta
+
+    def _push(self, slab: torch.Tensor) -> None:
+        from ..core.table import Table
+
+        local = Table(2, self.sum)
+        for k, b in enumerate(self.need):
+            local.add(b, slab[k * self.B:(k + 1) * self.B])
+        if not self.push("lda", "push-model", local, self.glob, None):
+            raise IOError("push failed")
+
+    def _pull(self) -> torch.Tensor:
+        from ..core.table import Table
+
+        want = Table(3, self.sum)
+        for b in self.need:
+            want.add(b, torch.zeros((self.B, self.Kp), dtype=torch.int32, device=self.device))
+        if not self.pull("lda", "pull-model", want, self.glob, True):
+            raise IOError("pull failed")
+        if not self.need:
+            return torch.zeros((0, self.Kp), dtype=torch.int32, device=self.device)
+        return torch.cat([want[b] for b in self.need]).contiguous()
+
+    def iterate(self, it: int) -> int:
+        cfg = self.cfg
+        slab = self._pull()
+        before = slab.clone()
+        n = self.tz.numel()
+        if n:
+            d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, slab, self.nk,
+                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, (cfg.seed << 40) ^ (it << 20) ^ 0x5A)
+        else:
+            d = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
+        slab -= before
+        self._push(slab)
+        if self.get_num_workers() > 1:
+            d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
+        self.nk += d
+        return n
+
+    def log_likelihood(self, it: int) -> float:
+        cfg = self.cfg
+        K = cfg.num_topics
+        wp = torch.zeros(2, dtype=torch.float64, device=self.device)
+        for p in self.glob.get_partitions():  # each block counted once, at its owner
+            wp += L.loglik_terms(p.get(), cfg.beta, K)
+        dp = L.loglik_terms(self.ndk, cfg.alpha, K)
+        tot = reduce_partials(self.comm, {"w": wp[:1], "d": dp})
+        nk = self.nk[:K].double()
+        topic = (torch.lgamma(torch.tensor(self.vbeta, dtype=torch.float64)) - torch.lgamma(nk + self.vbeta)).sum()
+        return float(tot["w"][0] + topic.cpu() + tot["d"].sum())
+
+    def map_collective(self, reader: KeyValReader, context: Context) -> None:
+        self.init_model(reader)
+        for it in range(self.cfg.iterations):
+            t0 = time.perf_counter()
+            self.iterate(it)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            self.iter_times.append(time.perf_counter() - t0)
+            if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
+                self.loglik.append((it + 1, self.log_likelihood(it)))
+        self.result = {"loglik": self.loglik, "iter_s": self.iter_times}
+
+
+def run_lda_push_pull(comm, cfg: LDAConfig, n_docs: int, vocab: int, tokens) -> dict:
+    m = LDAPushPullMapper(comm, cfg, n_docs, vocab, tokens)
     m.run(KeyValReader([]))
     return m.result

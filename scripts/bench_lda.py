@@ -21,10 +21,11 @@ def main():
     ap.add_argument("--len", type=int, default=100)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--strategy", default="rotation", choices=["rotation", "push_pull"])
     a = ap.parse_args()
     import torch
 
-    from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, synthetic_corpus
+    from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, LDAPushPullMapper, synthetic_corpus
     from harp_amd.runtime.launcher import init_distributed, shutdown
     from harp_amd.runtime.mapper import KeyValReader
 
@@ -34,7 +35,8 @@ def main():
     toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
     gen = time.perf_counter() - t0
     cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters)
-    m = LDACollectiveMapper(comm, cfg, nd, V, toks)
+    cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper
+    m = cls(comm, cfg, nd, V, toks)
     t0 = time.perf_counter()
     m.init_model(KeyValReader([]))
     torch.cuda.synchronize()
@@ -42,14 +44,16 @@ def main():
     ll0 = m.log_likelihood(-1)
     for it in range(a.warmup):
         m.iterate(it)
-    m.rot.wait_all()
+    if hasattr(m, "rot"):
+        m.rot.wait_all()
     torch.cuda.synchronize()
     comm.barrier()
     t0 = time.perf_counter()
     n = 0
     for it in range(a.warmup, a.warmup + a.iters):
         n += m.iterate(it)
-    m.rot.wait_all()
+    if hasattr(m, "rot"):
+        m.rot.wait_all()
     torch.cuda.synchronize()
     comm.barrier()
     dt = time.perf_counter() - t0
@@ -58,7 +62,7 @@ def main():
     if comm.world_size > 1:
         comm.all_reduce(tot)
     if comm.rank == 0:
-        print(json.dumps({"metric": "LDA-CGS sampled tokens/sec (model rotation)", "value": float(tot.item()) / dt,
+        print(json.dumps({"metric": f"LDA-CGS sampled tokens/sec ({a.strategy})", "value": float(tot.item()) / dt,
                           "unit": "tokens/s", "s_per_iter": dt / a.iters, "n_gpus": comm.world_size,
                           "docs": nd, "vocab": V, "topics": a.topics, "tokens": int(tot.item()) // a.iters,
                           "loglik_init": ll0, "loglik_end": ll, "init_s": init_s, "gen_s": gen}), flush=True)

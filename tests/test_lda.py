@@ -40,3 +40,32 @@ def test_lda_p_invariance(corpus):
     two = launch(_job, 2, args=(cfg, 300, 400, corpus), timeout=300)[0]["loglik"][-1][1]
     n_tok = corpus[0].numel()
     assert abs(one - two) / n_tok < 0.05, (one, two)  # per-token log-likelihood agrees
+
+
+def _pp_job(comm, cfg, nd, V, toks):
+    from harp_amd.models.lda import LDAPushPullMapper
+    from harp_amd.runtime.mapper import KeyValReader
+
+    m = LDAPushPullMapper(comm, cfg, nd, V, toks)
+    m.run(KeyValReader([]))
+    # model consistency: the distributed table holds exactly the token counts per topic
+    owned = sum(p.get().sum(0).double() for p in m.glob.get_partitions())
+    from harp_amd.models.common import reduce_partials
+
+    tot = reduce_partials(comm, {"t": owned if torch.is_tensor(owned) else torch.zeros(m.Kp, dtype=torch.float64)})
+    return m.result, tot["t"][:cfg.num_topics], m.nk[:cfg.num_topics].double()
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_lda_push_pull(corpus, P):
+    cfg = LDAConfig(num_topics=10, alpha=0.1, beta=0.01, iterations=20, print_interval=10, block_words=64)
+    res = launch(_pp_job, P, args=(cfg, 300, 400, corpus), timeout=300)
+    ll = [v for _, v in res[0][0]["loglik"]]
+    assert ll[-1] > ll[0]
+    for r in res:
+        assert torch.equal(r[1], r[2])  # sum of pushed model == allreduced topic sums
+        assert int(r[2].sum()) == corpus[0].numel()
+    rot = launch(_job, 1, args=(LDAConfig(num_topics=10, alpha=0.1, beta=0.01, iterations=20, print_interval=20),
+                                300, 400, corpus))[0]["loglik"][-1][1]
+    # bulk-synchronous snapshot staleness costs a little at this tiny scale (12k tokens)
+    assert abs(ll[-1] - rot) / abs(rot) < 0.08

@@ -17,3 +17,19 @@ def test_lda_gpu_matches_cpu_quality(cuda, K):
     n = toks[0].numel()
     lg, lc = g["loglik"][-1][1], c["loglik"][-1][1]
     assert abs(lg - lc) / n < 0.1, (lg, lc)
+
+
+def test_lda_push_pull_gpu(cuda):
+    from harp_amd.models.lda import LDAConfig, LDAPushPullMapper, synthetic_corpus
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    toks = synthetic_corpus(2000, 3000, 20, 50, seed=2)
+    cfg = LDAConfig(num_topics=64, alpha=0.1, beta=0.01, iterations=6, print_interval=3, block_words=512)
+    m = LDAPushPullMapper(Communicator(device=cuda), cfg, 2000, 3000, toks)
+    m.run(KeyValReader([]))
+    ll = [v for _, v in m.result["loglik"]]
+    assert ll[-1] > ll[0]
+    owned = sum(p.get().sum(0) for p in m.glob.get_partitions())
+    assert torch.equal(owned[:64].cpu(), m.nk[:64].cpu())
+    assert int(m.nk.sum()) == toks[0].numel()
