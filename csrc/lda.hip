@@ -28,83 +28,216 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   return z ^ (z >> 31);
 }
 
-__device__ __forceinline__ float wave_incl_scan(float v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
+// wave64 inclusive prefix sum on the DPP network (no LDS round trips): Hillis-Steele
+// within each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 and 3
+// and row_bcast:31 into rows 2 and 3. Lanes without a source add 0 (old = 0).
+__device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
+  int t;
+  switch (ctrl_sel) {
+    case 0: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false); break;
+    case 1: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, false); break;
+    case 2: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, false); break;
+    case 3: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, false); break;
+    case 4: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false); break;
+    default: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false); break;
   }
+  return v + __int_as_float(t);
+}
+
+__device__ __forceinline__ float wave_incl_scan(float v, int) {
+  v = dpp_add(v, 0);
+  v = dpp_add(v, 1);
+  v = dpp_add(v, 2);
+  v = dpp_add(v, 3);
+  v = dpp_add(v, 4);
+  v = dpp_add(v, 5);
   return v;
 }
 
-template <int TPL>  // topics per lane; K_pad = 64 * TPL
-__global__ __launch_bounds__(256) void lda_cgs_kernel(
+// doc-topic row element: int (32-bit counts) or unsigned short (16-bit counts, half the
+// bytes of the per-token row read that bounds this kernel; updated with 32-bit atomics
+// on the containing dword: counts stay in [0, 65535], so a +-1 on one half never
+// carries or borrows into the other)
+template <class DT>
+struct DocRow;
+template <>
+struct DocRow<int> {
+  static constexpr int RAW_PER_T = 1;  // raw dwords per topic slot: TPL dwords per lane
+  template <int TPL>
+  __device__ static __forceinline__ void load_raw(const int* drow, int k0, unsigned (&r)[TPL]) {
+#pragma unroll
+    for (int t = 0; t < TPL; t += 4) {
+      const uint4 v = *(const uint4*)(drow + k0 + t);
+      r[t] = v.x; r[t + 1] = v.y; r[t + 2] = v.z; r[t + 3] = v.w;
+    }
+  }
+  template <int TPL>
+  __device__ static __forceinline__ void unpack(const unsigned (&r)[TPL], int (&nd)[TPL]) {
+#pragma unroll
+    for (int t = 0; t < TPL; ++t) nd[t] = (int)r[t];
+  }
+  template <int TPL>
+  __device__ static __forceinline__ void load(const int* drow, int k0, int (&nd)[TPL]) {
+#pragma unroll
+    for (int t = 0; t < TPL; t += 4) {
+      const int4 v = *(const int4*)(drow + k0 + t);
+      nd[t] = v.x; nd[t + 1] = v.y; nd[t + 2] = v.z; nd[t + 3] = v.w;
+    }
+  }
+  __device__ static __forceinline__ void add(int* drow, int k, int v) { atomicAdd(drow + k, v); }
+  template <int TPL>
+  __device__ static __forceinline__ void patch(unsigned (&r)[TPL], int lane, int z, int nz) {
+#pragma unroll
+    for (int t = 0; t < TPL; ++t)
+      r[t] += (lane * TPL + t == nz ? 1u : 0u) - (lane * TPL + t == z ? 1u : 0u);
+  }
+};
+template <>
+struct DocRow<unsigned short> {
+  template <int TPL>
+  __device__ static __forceinline__ void load_raw(const unsigned short* drow, int k0, unsigned (&r)[TPL]) {
+    // only the first TPL/2 dwords are used: two 16-bit counts per dword
+    if constexpr (TPL % 8 != 0) {
+      const uint2 v = *(const uint2*)(drow + k0);
+      r[0] = v.x; r[1] = v.y;
+    } else {
+#pragma unroll
+      for (int t = 0; t < TPL / 2; t += 4) {
+        const uint4 v = *(const uint4*)(drow + k0 + 2 * t);
+        r[t] = v.x; r[t + 1] = v.y; r[t + 2] = v.z; r[t + 3] = v.w;
+      }
+    }
+  }
+  template <int TPL>
+  __device__ static __forceinline__ void unpack(const unsigned (&r)[TPL], int (&nd)[TPL]) {
+#pragma unroll
+    for (int q = 0; q < TPL / 2; ++q) {
+      nd[2 * q] = (int)(r[q] & 0xFFFFu);
+      nd[2 * q + 1] = (int)(r[q] >> 16);
+    }
+  }
+  template <int TPL>
+  __device__ static __forceinline__ void load(const unsigned short* drow, int k0, int (&nd)[TPL]) {
+    static_assert(TPL % 4 == 0, "TPL must be a multiple of 4");
+    if constexpr (TPL % 8 != 0) {
+#pragma unroll
+      for (int t = 0; t < TPL; t += 4) {
+        const uint2 v = *(const uint2*)(drow + k0 + t);
+        nd[t] = (int)(v.x & 0xFFFFu);
+        nd[t + 1] = (int)(v.x >> 16);
+        nd[t + 2] = (int)(v.y & 0xFFFFu);
+        nd[t + 3] = (int)(v.y >> 16);
+      }
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < (TPL % 8 == 0 ? TPL : 0); t += 8) {
+      const uint4 v = *(const uint4*)(drow + k0 + t);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        nd[t + 2 * q] = (int)(w[q] & 0xFFFFu);
+        nd[t + 2 * q + 1] = (int)(w[q] >> 16);
+      }
+    }
+  }
+  template <int TPL>
+  __device__ static __forceinline__ void patch(unsigned (&r)[TPL], int lane, int z, int nz) {
+#pragma unroll
+    for (int q = 0; q < TPL / 2; ++q) {
+      const int k = lane * TPL + 2 * q;
+      r[q] += (k == nz ? 1u : 0u) + (k + 1 == nz ? 0x10000u : 0u);
+      r[q] -= (k == z ? 1u : 0u) + (k + 1 == z ? 0x10000u : 0u);
+    }
+  }
+  __device__ static __forceinline__ void add(unsigned short* drow, int k, int v) {
+    unsigned* word = (unsigned*)(drow + (k & ~1));
+    const unsigned sh = (k & 1) ? 16u : 0u;
+    if (v > 0) atomicAdd(word, (unsigned)v << sh);
+    else atomicSub(word, (unsigned)(-v) << sh);
+  }
+};
+
+template <int TPL, class DT>  // topics per lane; K_pad = 64 * TPL
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ? 4 : 5, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
-    const long* __restrict__ chunk_start, long nchunks, int* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
+    const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
     unsigned long long seed) {
   constexpr int KP = 64 * TPL;
+  constexpr int WAVES = 4;
   __shared__ float s_inv[KP];
   __shared__ int s_delta[KP];
+  __shared__ int s_nw0[WAVES][KP];  // chunk-start word row (flush delta), kept out of VGPRs
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
     s_inv[k] = k < K ? inv_nk[k] : 0.f;
     s_delta[k] = 0;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
   const long wave_g = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
   const int k0 = lane * TPL;
+  int* nw0s = &s_nw0[wv][k0];
   for (long c = wave_g; c < nchunks; c += nwaves) {
     const long a = chunk_start[c], b = chunk_start[c + 1];
     const int w = tword[a];
     int* wrow = nwk + (long)w * ldw + k0;
-    int nw0[TPL], nw[TPL];
+    int nw[TPL];
 #pragma unroll
     for (int t = 0; t < TPL; t += 4) {
       const int4 v = *(const int4*)(wrow + t);
-      nw0[t] = v.x; nw0[t + 1] = v.y; nw0[t + 2] = v.z; nw0[t + 3] = v.w;
+      nw[t] = v.x; nw[t + 1] = v.y; nw[t + 2] = v.z; nw[t + 3] = v.w;
+      *(int4*)(nw0s + t) = v;
     }
-#pragma unroll
-    for (int t = 0; t < TPL; ++t) nw[t] = nw0[t];
     for (long i = a; i < b; ++i) {
       const int d = tdoc[i];
       const int z = tz[i];
-      int* drow = ndk + (long)d * ldd;
+      DT* drow = ndk + (long)d * ldd;
       int nd[TPL];
-#pragma unroll
-      for (int t = 0; t < TPL; t += 4) {
-        const int4 v = *(const int4*)(drow + k0 + t);
-        nd[t] = v.x; nd[t + 1] = v.y; nd[t + 2] = v.z; nd[t + 3] = v.w;
-      }
-      // remove the token (registers; the global doc count is decremented below)
+      DocRow<DT>::template load<TPL>(drow, k0, nd);
+      // remove the token from the word row (registers) and, virtually, from the doc row
       const int zl = z / TPL, zt = z % TPL;
-      float p[TPL];
-      float s = 0.f;
 #pragma unroll
       for (int t = 0; t < TPL; ++t) {
         const int own = (lane == zl && t == zt) ? 1 : 0;
         nw[t] -= own;
-        const float pt = ((float)(nd[t] - own) + alpha) * ((float)nw[t] + beta) * s_inv[k0 + t];
-        p[t] = (k0 + t < K) ? pt : 0.f;
-        s += p[t];
+        nd[t] -= own;
+      }
+      // unnormalised p_t = (n_dt + alpha)(n_wt + beta) / (n_t + V beta); not stored:
+      // recomputed in the walk below (16 fewer live registers -> more waves per SIMD)
+      float s = 0.f;
+      const float* sinv0 = s_inv;
+      asm volatile("" : "+v"(sinv0));  // re-read 1/(n_t + V beta) from LDS (not 16 live VGPRs)
+#pragma unroll
+      for (int t = 0; t < TPL; ++t) {
+        const float pt = ((float)nd[t] + alpha) * ((float)nw[t] + beta) * sinv0[k0 + t];
+        s += (k0 + t < K) ? pt : 0.f;
       }
       const float incl = wave_incl_scan(s, lane);
-      const float total = __shfl(incl, 63, 64);
+      const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
       const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
       const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * total;
       const unsigned long long hit = __ballot(incl > u);
-      int src = hit ? (int)__builtin_ctzll(hit) : 63;
-      // walk the chosen lane's topics: first t with excl + prefix(t) > u
+      const int src = hit ? (int)__builtin_ctzll(hit) : 63;
+      // walk the chosen lane's topics: first t with excl + prefix(t) > u. The counts are
+      // made opaque first so the compiler recomputes p_t instead of keeping 16 products
+      // (or their factors) live across the scan
+#pragma unroll
+      for (int t = 0; t < TPL; ++t) asm volatile("" : "+v"(nd[t]), "+v"(nw[t]));
+      const float* sinv = s_inv;
+      asm volatile("" : "+v"(sinv));
       float acc = incl - s;
       int found = -1;
 #pragma unroll
       for (int t = 0; t < TPL; ++t) {
-        acc += p[t];
+        const float pt = ((float)nd[t] + alpha) * ((float)nw[t] + beta) * sinv[k0 + t];
+        acc += (k0 + t < K) ? pt : 0.f;
         if (found < 0 && acc > u) found = t;
       }
       const int sel = found < 0 ? TPL - 1 : found;
-      int nz = __shfl(k0 + sel, src, 64);
+      int nz = __builtin_amdgcn_readlane(k0 + sel, src);
       if (nz >= K) nz = K - 1;
       // add the token back with its new topic
       const int nzl = nz / TPL, nzt = nz % TPL;
@@ -113,8 +246,8 @@ __global__ __launch_bounds__(256) void lda_cgs_kernel(
       if (lane == 0) {
         tz[i] = nz;
         if (nz != z) {
-          atomicSub(drow + z, 1);
-          atomicAdd(drow + nz, 1);
+          DocRow<DT>::add(drow, z, -1);
+          DocRow<DT>::add(drow, nz, 1);
           atomicSub(&s_delta[z], 1);
           atomicAdd(&s_delta[nz], 1);
         }
@@ -123,7 +256,7 @@ __global__ __launch_bounds__(256) void lda_cgs_kernel(
     // flush this chunk's word-row delta
 #pragma unroll
     for (int t = 0; t < TPL; ++t) {
-      const int dlt = nw[t] - nw0[t];
+      const int dlt = nw[t] - nw0s[t];
       if (dlt) atomicAdd(wrow + t, dlt);
     }
   }
@@ -133,12 +266,13 @@ __global__ __launch_bounds__(256) void lda_cgs_kernel(
 }
 
 // count tables from assignments: ndk[d][z]++, nwk[w][z]++, nk[z]++
+template <class DT>
 __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __restrict__ tword, const int* __restrict__ tz,
-                                 long n, int* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
+                                 long n, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
                                  int* __restrict__ nk) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int z = tz[i];
-    if (ndk) atomicAdd(ndk + (long)tdoc[i] * ldd + z, 1);
+    if (ndk) DocRow<DT>::add(ndk + (long)tdoc[i] * ldd, z, 1);
     if (nwk) atomicAdd(nwk + (long)tword[i] * ldw + z, 1);
     if (nk) atomicAdd(nk + z, 1);
   }
@@ -146,35 +280,63 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 
 }  // namespace
 
-HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, int* ndk,
-                             int ldd, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
-                             float beta, unsigned long long seed, hipStream_t s) {
-  if (nchunks <= 0) return HARP_OK;
-  if (K <= 0 || K > 1024 || ldd % 4 || ldw % 4) return HARP_EBADARG;
+namespace {
+template <class DT>
+int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
+               int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
+               unsigned long long seed, hipStream_t s) {
   long blocks = (nchunks + 3) / 4;  // 4 waves per block
   if (blocks > 8192) blocks = 8192;
   const dim3 g((unsigned)blocks), bl(256);
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
-    lda_cgs_kernel<4><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K,
-                                       alpha, beta, seed);
+    lda_cgs_kernel<4, DT><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+                                           nk_delta, K, alpha, beta, seed);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
-    lda_cgs_kernel<8><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K,
-                                       alpha, beta, seed);
+    lda_cgs_kernel<8, DT><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+                                           nk_delta, K, alpha, beta, seed);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
-    lda_cgs_kernel<16><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K,
-                                        alpha, beta, seed);
+    lda_cgs_kernel<16, DT><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+                                            nk_delta, K, alpha, beta, seed);
   }
   return harp_launch_status();
 }
+}  // namespace
 
-HARP_EXPORT int harp_lda_count(const int* tdoc, const int* tword, const int* tz, long n, int* ndk, int ldd, int* nwk,
-                               int ldw, int* nk, hipStream_t s) {
+// ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8)
+HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
+                             void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
+                             int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
+  if (nchunks <= 0) return HARP_OK;
+  if (K <= 0 || K > 1024 || ldw % 4) return HARP_EBADARG;
+  if (ndk_bits == 32) {
+    if (ldd % 4) return HARP_EBADARG;
+    return launch_cgs<int>(tdoc, tword, tz, chunk_start, nchunks, (int*)ndk, ldd, nwk, ldw, inv_nk, nk_delta, K,
+                           alpha, beta, seed, s);
+  }
+  if (ndk_bits == 16) {
+    if (ldd % 8) return HARP_EBADARG;
+    return launch_cgs<unsigned short>(tdoc, tword, tz, chunk_start, nchunks, (unsigned short*)ndk, ldd, nwk, ldw,
+                                      inv_nk, nk_delta, K, alpha, beta, seed, s);
+  }
+  return HARP_EBADARG;
+}
+
+HARP_EXPORT int harp_lda_count(const int* tdoc, const int* tword, const int* tz, long n, void* ndk, int ldd,
+                               int ndk_bits, int* nwk, int ldw, int* nk, hipStream_t s) {
   if (n <= 0) return HARP_OK;
   long blocks = (n + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  lda_count_kernel<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(tdoc, tword, tz, n, ndk, ldd, nwk, ldw, nk);
+  if (ndk_bits == 16) {
+    if (ldd % 2) return HARP_EBADARG;
+    lda_count_kernel<unsigned short><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(tdoc, tword, tz, n,
+                                                                                  (unsigned short*)ndk, ldd, nwk, ldw,
+                                                                                  nk);
+  } else {
+    lda_count_kernel<int><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(tdoc, tword, tz, n, (int*)ndk, ldd, nwk, ldw,
+                                                                       nk);
+  }
   return harp_launch_status();
 }

@@ -102,7 +102,8 @@ class LDACollectiveMapper(CollectiveMapper):
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
         # counts: doc-topic local; word-topic global (allreduced once), then each worker keeps
         # the slices of its initial placement
-        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=torch.int32, device=dev)
+        maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
+        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(dev, maxlen), device=dev)
         nwk_full = torch.zeros((ns * self.vps, self.Kp), dtype=torch.int32, device=dev)
         nk = torch.zeros(self.Kp, dtype=torch.int32, device=dev)
         for s in range(ns):
@@ -219,7 +220,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self.chunk_idx = L.build_chunks(self.tword, cfg.max_chunk)
         gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
-        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=torch.int32, device=dev)
+        maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
+        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(dev, maxlen), device=dev)
         slab = torch.zeros((len(self.need) * B, self.Kp), dtype=torch.int32, device=dev)
         nk = torch.zeros(self.Kp, dtype=torch.int32, device=dev)
         L.count(self.tdoc, self.tword, self.tz, self.ndk, slab, nk)

@@ -9,9 +9,9 @@ from . import _lib
 
 _lib.register({
     "harp_lda_cgs": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int,
-                     _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float,
-                     _lib.c_ulonglong, _lib.c_void_p],
-    "harp_lda_count": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int,
+                     _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
+                     _lib.c_float, _lib.c_ulonglong, _lib.c_void_p],
+    "harp_lda_count": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_int,
                        _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
 })
 
@@ -42,19 +42,29 @@ def build_chunks(words: torch.Tensor, max_chunk: int = 2048) -> torch.Tensor:
     return torch.cat([b, torch.tensor([n], device=words.device)]).to(torch.int64)
 
 
+def doc_topic_dtype(device, max_doc_len: int) -> torch.dtype:
+    """Doc-topic count storage: packed 16-bit on the GPU when every doc has < 32768
+    tokens (halves the per-token row read that bounds the sampler), else int32."""
+    return torch.int16 if device.type == "cuda" and max_doc_len < 32768 else torch.int32
+
+
+def _bits(ndk) -> int:
+    return 16 if ndk is not None and ndk.dtype == torch.int16 else 32
+
+
 def count(tdoc, tword, tz, ndk=None, nwk=None, nk=None) -> None:
     n = tz.numel()
     dev = tz.device
     if _lib.use_native(tz):
         st = _lib.kernels().harp_lda_count(_lib.ptr(tdoc), _lib.ptr(tword), tz.data_ptr(), n, _lib.ptr(ndk),
-                                           ndk.stride(0) if ndk is not None else 0, _lib.ptr(nwk),
+                                           ndk.stride(0) if ndk is not None else 0, _bits(ndk), _lib.ptr(nwk),
                                            nwk.stride(0) if nwk is not None else 0, _lib.ptr(nk), _lib.stream_ptr(dev))
         _lib.check(st, "lda_count")
         return
     one = torch.ones(n, dtype=torch.int32)
     z = tz.long()
     if ndk is not None:
-        ndk.index_put_((tdoc.long(), z), one, accumulate=True)
+        ndk.index_put_((tdoc.long(), z), one.to(ndk.dtype), accumulate=True)
     if nwk is not None:
         nwk.index_put_((tword.long(), z), one, accumulate=True)
     if nk is not None:
@@ -73,7 +83,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
         inv[:K] = 1.0 / (nk[:K].float() + vbeta)
         delta = torch.zeros(Kp, dtype=torch.int32, device=dev)
         st = _lib.kernels().harp_lda_cgs(tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(),
-                                         chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), nwk.data_ptr(),
+                                         chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
                                          seed & 0xFFFFFFFFFFFFFFFF, _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
@@ -96,6 +106,8 @@ def loglik_terms(counts: torch.Tensor, prior: float, K: int) -> torch.Tensor:
     """sum_k lgamma(c + prior) - lgamma(prior) over the first K columns, and
     sum_rows lgamma(row_total + K prior) terms: returns (entry_sum, row_sum) fp64."""
     c = counts[:, :K].double()
+    if counts.dtype == torch.int16:  # packed unsigned 16-bit counts
+        c = torch.where(c < 0, c + 65536.0, c)
     ent = (torch.lgamma(c + prior) - torch.lgamma(torch.tensor(prior, dtype=torch.float64))).sum()
     tot = c.sum(1)
     rows = (torch.lgamma(torch.tensor(K * prior, dtype=torch.float64)) - torch.lgamma(tot + K * prior)).sum()
