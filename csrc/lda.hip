@@ -184,65 +184,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ?
     const long a = chunk_start[c], b = chunk_start[c + 1];
     const int w = tword[a];
     int* wrow = nwk + (long)w * ldw + k0;
-    int nw[TPL];
+    // word row held as floats (exact for counts < 2^24) plus the per-word factor
+    // qw_t = (n_wt + beta) / (n_t + V beta); a token then costs ONE multiply-add per
+    // topic, p_t = (n_dt + alpha) * qw_t, and only the two topics a token moves have
+    // their qw refreshed
+    float nwf[TPL], qw[TPL];
 #pragma unroll
     for (int t = 0; t < TPL; t += 4) {
       const int4 v = *(const int4*)(wrow + t);
-      nw[t] = v.x; nw[t + 1] = v.y; nw[t + 2] = v.z; nw[t + 3] = v.w;
       *(int4*)(nw0s + t) = v;
+      nwf[t] = (float)v.x; nwf[t + 1] = (float)v.y; nwf[t + 2] = (float)v.z; nwf[t + 3] = (float)v.w;
     }
+#pragma unroll
+    for (int t = 0; t < TPL; ++t) qw[t] = (nwf[t] + beta) * s_inv[k0 + t];
+    int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
+                                           // waits on ONE memory round trip, not two
     for (long i = a; i < b; ++i) {
-      const int d = tdoc[i];
-      const int z = tz[i];
+      const int d = d_next;
+      const int z = z_next;
+      if (i + 1 < b) {
+        d_next = tdoc[i + 1];
+        z_next = tz[i + 1];
+      }
       DT* drow = ndk + (long)d * ldd;
-      int nd[TPL];
-      DocRow<DT>::template load<TPL>(drow, k0, nd);
-      // remove the token from the word row (registers) and, virtually, from the doc row
+      float nd[TPL];
+      {
+        int ndi[TPL];
+        DocRow<DT>::template load<TPL>(drow, k0, ndi);
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
+      }      // remove the token: only lane z / TPL changes, at the uniform slot z % TPL (a
+      // scalar branch picks the slot; one lane updates three registers)
       const int zl = z / TPL, zt = z % TPL;
+      const float inv_z = s_inv[z];
 #pragma unroll
       for (int t = 0; t < TPL; ++t) {
-        const int own = (lane == zl && t == zt) ? 1 : 0;
-        nw[t] -= own;
-        nd[t] -= own;
+        if (t == zt) {
+          if (lane == zl) {
+            nd[t] -= 1.f;
+            nwf[t] -= 1.f;
+            qw[t] = (nwf[t] + beta) * inv_z;
+          }
+        }
       }
-      // unnormalised p_t = (n_dt + alpha)(n_wt + beta) / (n_t + V beta); not stored:
-      // recomputed in the walk below (16 fewer live registers -> more waves per SIMD)
       float s = 0.f;
-      const float* sinv0 = s_inv;
-      asm volatile("" : "+v"(sinv0));  // re-read 1/(n_t + V beta) from LDS (not 16 live VGPRs)
 #pragma unroll
-      for (int t = 0; t < TPL; ++t) {
-        const float pt = ((float)nd[t] + alpha) * ((float)nw[t] + beta) * sinv0[k0 + t];
-        s += (k0 + t < K) ? pt : 0.f;
-      }
+      for (int t = 0; t < TPL; ++t) s = fmaf(nd[t] + alpha, qw[t], s);
       const float incl = wave_incl_scan(s, lane);
       const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
       const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
       const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * total;
       const unsigned long long hit = __ballot(incl > u);
       const int src = hit ? (int)__builtin_ctzll(hit) : 63;
-      // walk the chosen lane's topics: first t with excl + prefix(t) > u. The counts are
-      // made opaque first so the compiler recomputes p_t instead of keeping 16 products
-      // (or their factors) live across the scan
+      // walk the chosen lane's topics: first t with excl + prefix(t) > u
+      int found;
+      {
+        float pre = incl - s;
+        int f = -1;
 #pragma unroll
-      for (int t = 0; t < TPL; ++t) asm volatile("" : "+v"(nd[t]), "+v"(nw[t]));
-      const float* sinv = s_inv;
-      asm volatile("" : "+v"(sinv));
-      float acc = incl - s;
-      int found = -1;
-#pragma unroll
-      for (int t = 0; t < TPL; ++t) {
-        const float pt = ((float)nd[t] + alpha) * ((float)nw[t] + beta) * sinv[k0 + t];
-        acc += (k0 + t < K) ? pt : 0.f;
-        if (found < 0 && acc > u) found = t;
+        for (int t = 0; t < TPL; ++t) {
+          pre = fmaf(nd[t] + alpha, qw[t], pre);
+          f = (f < 0 && pre > u) ? t : f;
+        }
+        found = f < 0 ? TPL - 1 : f;
       }
-      const int sel = found < 0 ? TPL - 1 : found;
-      int nz = __builtin_amdgcn_readlane(k0 + sel, src);
+      int nz = __builtin_amdgcn_readlane(k0 + found, src);
       if (nz >= K) nz = K - 1;
       // add the token back with its new topic
       const int nzl = nz / TPL, nzt = nz % TPL;
+      const float inv_nz = s_inv[nz];
 #pragma unroll
-      for (int t = 0; t < TPL; ++t) nw[t] += (lane == nzl && t == nzt) ? 1 : 0;
+      for (int t = 0; t < TPL; ++t) {
+        if (t == nzt) {
+          if (lane == nzl) {
+            nwf[t] += 1.f;
+            qw[t] = (nwf[t] + beta) * inv_nz;
+          }
+        }
+      }
       if (lane == 0) {
         tz[i] = nz;
         if (nz != z) {
@@ -256,7 +275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ?
     // flush this chunk's word-row delta
 #pragma unroll
     for (int t = 0; t < TPL; ++t) {
-      const int dlt = nw[t] - nw0s[t];
+      const int dlt = (int)nwf[t] - nw0s[t];
       if (dlt) atomicAdd(wrow + t, dlt);
     }
   }
