@@ -38,3 +38,34 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// wave64 inclusive prefix sum on the DPP network (no LDS round trips): Hillis-Steele within
+// each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3; lanes without a source add 0.
+__device__ __forceinline__ float dpp_shift_add(float v, int sel) {
+  int t;
+  switch (sel) {
+    case 0: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false); break;
+    case 1: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, false); break;
+    case 2: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, false); break;
+    case 3: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, false); break;
+    case 4: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false); break;
+    default: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false); break;
+  }
+  return v + __int_as_float(t);
+}
+
+__device__ __forceinline__ float wave_scan_incl(float v) {
+  v = dpp_shift_add(v, 0);
+  v = dpp_shift_add(v, 1);
+  v = dpp_shift_add(v, 2);
+  v = dpp_shift_add(v, 3);
+  v = dpp_shift_add(v, 4);
+  v = dpp_shift_add(v, 5);
+  return v;
+}
+
+// wave-uniform total (scalar register), no LDS traffic
+__device__ __forceinline__ float wave_total(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_scan_incl(v)), 63));
+}

@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from ..parallel.comm import Communicator
+from ..ops import ccd as C
 from .mf_common import gather_factors, rmse, shuffle_coo
 
 
@@ -38,24 +39,6 @@ class CCDConfig:
     init_scale: float = -1.0  # <= 0: uniform [0, 1/sqrt(rank)) like CCDMPCollectiveMapper.java:200-213
 
 
-def _phase(rows: torch.Tensor, cols: torch.Tensor, res: torch.Tensor, n_rows: int, F_own: torch.Tensor,
-           F_other: torch.Tensor, lam: float, cnt: torch.Tensor) -> None:
-    """Coordinate updates of F_own (rows local) against fixed F_other; res updated in place."""
-    k = F_own.shape[1]
-    down0 = lam * cnt
-    for t in range(k):
-        h = F_other[cols, t]
-        w = F_own[rows, t]
-        up = torch.zeros(n_rows, dtype=res.dtype, device=res.device)
-        down = down0.clone()
-        up.index_add_(0, rows, (res + w * h) * h)
-        down.index_add_(0, rows, h * h)
-        z = torch.where(down > 0, up / down.clamp_min(1e-300), F_own[:, t])
-        delta = z - F_own[:, t]
-        res -= delta[rows] * h
-        F_own[:, t] = z
-
-
 def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Tensor, n_users: int, n_items: int,
               cfg: CCDConfig, test: Optional[Tuple[torch.Tensor, ...]] = None) -> Dict[str, object]:
     P, me, dev = comm.world_size, comm.rank, comm.device
@@ -64,35 +47,43 @@ def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
     iu, ii, iv = shuffle_coo(comm, i % P, u, i, v)
     my_users = torch.arange(me, n_users, P, device=dev)
     my_items = torch.arange(me, n_items, P, device=dev)
-    ur, uc, uval = uu.to(dev) // P, ui.to(dev), uv.to(dev, dt)
-    ir, ic, ival = ii.to(dev) // P, iu.to(dev), iv.to(dev, dt)
-    cnt_u = torch.bincount(ur, minlength=my_users.numel()).to(dt)
-    cnt_i = torch.bincount(ir, minlength=my_items.numel()).to(dt)
+
+    def csr(rows_local, cols_global, vals, n_rows):
+        o = torch.argsort(rows_local, stable=True)
+        r = rows_local[o].to(torch.int32).contiguous()
+        return r, C.row_ptr_of(r, n_rows), cols_global[o].to(torch.int32).contiguous(), vals[o].to(dt).contiguous()
+
+    ur, uptr, uc, uval = csr(uu.to(dev) // P, ui.to(dev), uv.to(dev), my_users.numel())
+    ir, iptr, ic, ival = csr(ii.to(dev) // P, iu.to(dev), iv.to(dev), my_items.numel())
     g = torch.Generator().manual_seed(cfg.seed)
     sc = cfg.init_scale if cfg.init_scale > 0 else cfg.rank ** -0.5
     W0 = (torch.rand((n_users, cfg.rank), generator=g, dtype=torch.float64) * sc).to(dev, dt)
     H0 = (torch.rand((n_items, cfg.rank), generator=g, dtype=torch.float64) * sc).to(dev, dt)
-    W = W0[my_users].clone()
-    H = H0[my_items].clone()
+    W = W0[my_users].contiguous()
+    H = H0[my_items].contiguous()
     del W0, H0
+    ulong, ilong = C.long_rows_of(uptr), C.long_rows_of(iptr)
+    res_u = torch.empty_like(uval)
+    res_i = torch.empty_like(ival)
     hist: List[Dict[str, float]] = []
     for it in range(cfg.iterations):
         t0 = time.perf_counter()
-        Hf = gather_factors(comm, my_items, H, n_items)
-        res = uval - (W[ur] * Hf[uc]).sum(1)  # ResTask
-        _phase(ur, uc, res, my_users.numel(), W, Hf, cfg.lam, cnt_u)
-        Wf = gather_factors(comm, my_users, W, n_users)
-        res = ival - (H[ir] * Wf[ic]).sum(1)
-        _phase(ir, ic, res, my_items.numel(), H, Wf, cfg.lam, cnt_i)
+        Hf = gather_factors(comm, my_items, H, n_items).contiguous()
+        C.residual(ur, uc, uval, W, Hf, res_u)  # ResTask
+        C.phase(ur, uptr, uc, res_u, W, Hf, cfg.lam, ulong)
+        Wf = gather_factors(comm, my_users, W, n_users).contiguous()
+        C.residual(ir, ic, ival, H, Wf, res_i)
+        C.phase(ir, iptr, ic, res_i, H, Wf, cfg.lam, ilong)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         rec = {"iter": it + 1, "time_s": time.perf_counter() - t0,
-               "train_rmse": rmse(comm, (res * res).sum(), res.numel())}
+               "train_rmse": rmse(comm, (res_i.double() ** 2).sum(), res_i.numel())}
         if test is not None:
             Hf = gather_factors(comm, my_items, H, n_items)
             tu, ti, tv = test
             mine = (tu % P) == me
             pred = (Wf[tu[mine].to(dev)] * Hf[ti[mine].to(dev)]).sum(1)
-            rec["test_rmse"] = rmse(comm, ((pred - tv[mine].to(dev, dt)) ** 2).sum(), int(mine.sum()))
+            rec["test_rmse"] = rmse(comm, ((pred.double() - tv[mine].to(dev, torch.float64)) ** 2).sum(),
+                                    int(mine.sum()))
         hist.append(rec)
     return {"W": W, "H": H, "user_ids": my_users, "item_ids": my_items, "history": hist}
