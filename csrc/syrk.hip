@@ -163,31 +163,186 @@ __global__ void to_feature_major_kernel(const __bf16* __restrict__ X, long n, in
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Multi-stage variant: KT2 = 32 samples per stage and NS-deep LDS-DMA pipeline (the stage
+// about to be consumed was issued NS-1 stages earlier), so L2-miss latency (the operand
+// panels are re-read by every tile of a split and mostly miss L2) hides behind NS-1
+// stages of MFMA work instead of one. Swizzle for 4 chunks per 64-B row:
+// c ^ ((row >> 2) & 3) keeps every ds_read_b128 lane group on 16 distinct 16-B units.
+constexpr int KT2 = 32;
+constexpr int CPR2 = KT2 / 8;  // 4
+__device__ __forceinline__ int swz2(int row, int c) { return c ^ ((row >> 2) & 3); }
+
+template <class C>
+__device__ __forceinline__ void stage_panel2(const __bf16* __restrict__ XT, long ld, int r0, long k0, char* lds,
+                                             int wave, int lane) {
+  constexpr int DMA = C::MT * KT2 * 2 / 1024;
+#pragma unroll
+  for (int j = wave; j < DMA; j += C::WAVES) {
+    const int q = j * 64 + lane;
+    const int row = q / CPR2, cp = q % CPR2;
+    const __bf16* src = XT + (long)(r0 + row) * ld + k0 + swz2(row, cp) * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
+  }
+}
+
+// wait until at most `left` of this wave's DMA instructions are outstanding
+__device__ __forceinline__ void wait_vm(int left) {
+  switch (left) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
+template <int MT_, int BA_, int BB_, int NS>
+__global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void syrk_ms_kernel(
+    const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg) {
+  using C = SyrkCfg<MT_, BA_, BB_>;
+  constexpr int MT = C::MT, BA = C::BA, BB = C::BB;
+  constexpr int PANEL = MT * KT2 * 2;
+  constexpr int DPW = (PANEL / 1024 + C::WAVES - 1) / C::WAVES;  // DMA instructions per wave per panel
+  static_assert((PANEL / 1024) % C::WAVES == 0, "panel DMA must split evenly over the waves");
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * PANEL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  const unsigned q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+  const unsigned L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+  const int ntiles = nt * (nt + 1) / 2;
+  const int tile = L % ntiles;
+  const long split = L / ntiles;
+  int ti = 0, rem = tile;
+  while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
+  const int tj = ti + rem;
+  const bool diag = ti == tj;
+  const long kbeg = split * chunk;
+  long kend = kbeg + chunk;
+  if (kend > n) kend = n;
+  if (kbeg >= kend) return;
+  const int nsteps = (int)((kend - kbeg) / KT2);
+  const int per_step = diag ? DPW : 2 * DPW;
+  const int wr = wave / C::WC, wc = wave % C::WC;
+  floatx16 acc[BA][BB];
+#pragma unroll
+  for (int a = 0; a < BA; ++a)
+#pragma unroll
+    for (int bb = 0; bb < BB; ++bb)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[a][bb][v] = 0.f;
+  auto issue = [&](int step) {
+    char* buf = smem + (step % NS) * 2 * PANEL;
+    const long k0 = kbeg + (long)step * KT2;
+    stage_panel2<C>(XT, ld, ti * MT, k0, buf, wave, lane);
+    if (!diag) stage_panel2<C>(XT, ld, tj * MT, k0, buf + PANEL, wave, lane);
+  };
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nsteps) issue(st);
+  for (int i = 0; i < nsteps; ++i) {
+    // stages issued after step i so far: min(NS-2, nsteps-1-i)
+    int later = nsteps - 1 - i;
+    if (later > NS - 2) later = NS - 2;
+    wait_vm(later * per_step);
+    __syncthreads();  // step i landed for every wave; step i-1's buffer is free
+    if (i + NS - 1 < nsteps) issue(i + NS - 1);
+    const char* A = smem + (i % NS) * 2 * PANEL;
+    const char* B = diag ? A : A + PANEL;
+#pragma unroll
+    for (int s = 0; s < KT2 / 16; ++s) {
+      bf16x8 af[BA], bfr[BB];
+#pragma unroll
+      for (int a = 0; a < BA; ++a) {
+        const int row = wr * (32 * BA) + a * 32 + r;
+        af[a] = *(const bf16x8*)(A + row * (CPR2 * 16) + swz2(row, 2 * s + h) * 16);
+      }
+#pragma unroll
+      for (int bb = 0; bb < BB; ++bb) {
+        const int row = wc * (32 * BB) + bb * 32 + r;
+        bfr[bb] = *(const bf16x8*)(B + row * (CPR2 * 16) + swz2(row, 2 * s + h) * 16);
+      }
+#pragma unroll
+      for (int a = 0; a < BA; ++a)
+#pragma unroll
+        for (int bb = 0; bb < BB; ++bb)
+          acc[a][bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[bb], acc[a][bb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < BA; ++a)
+#pragma unroll
+    for (int bb = 0; bb < BB; ++bb) {
+      const int i0 = ti * MT + wr * (32 * BA) + a * 32;
+      const int j0 = tj * MT + wc * (32 * BB) + bb * 32;
+      if (diag && i0 > j0 + 31) continue;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = (v & 3) + 8 * (v >> 2) + 4 * h;
+        atomicAdd(G + (long)(i0 + row) * ldg + j0 + r, acc[a][bb][v]);
+      }
+    }
+}
+
 }  // namespace
 
-template <int MT, int BA, int BB>
+template <int MT, int BA, int BB, int NS = 0>
 static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits, int target_wg,
                        hipStream_t s) {
   using C = SyrkCfg<MT, BA, BB>;
   const int nt = d_pad / MT;
   const int ntiles = nt * (nt + 1) / 2;
-  if (num_splits <= 0) num_splits = (target_wg + ntiles - 1) / ntiles;
+  if (num_splits <= 0) {
+    // about target_wg workgroups, rounded so the grid fills whole rounds of the 256 CUs
+    // (one workgroup per CU at these LDS sizes): 1030 blocks = 4 rounds + a 6-block tail
+    const int s0 = (target_wg + ntiles - 1) / ntiles;
+    num_splits = s0;
+    double best = 0.0;
+    for (int sp = s0; sp <= 2 * s0; ++sp) {
+      const long B = (long)ntiles * sp;
+      const double eff = (double)B / (double)(((B + 255) / 256) * 256);
+      if (eff > best + 1e-9) { best = eff; num_splits = sp; }
+      if (eff > 0.999) break;
+    }
+  }
   long chunk = (n + num_splits - 1) / num_splits;
   chunk = (chunk + KT - 1) / KT * KT;
   const long splits = (n + chunk - 1) / chunk;
-  syrk_kernel<MT, BA, BB><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
-      (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
+  if constexpr (NS > 0) {
+    syrk_ms_kernel<MT, BA, BB, NS><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
+        (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
+  } else {
+    syrk_kernel<MT, BA, BB><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
+        (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
+  }
   return harp_launch_status();
 }
 
 // G[d_pad][ldg] (+)= XT XT^T over the upper tiles; XT [d_pad][ld] bf16, d_pad % 128 == 0,
 // n % 64 == 0 (zero-padded samples), ld >= n, ld % 8 == 0. 256x256 tiles (8 waves) when
 // d_pad % 256 == 0 and d_pad >= 512 (half the operand re-reads), else 128x128 (4 waves).
+// variant 0: 64-sample stages, double buffer; 1: 32-sample stages, 4-deep pipeline
 HARP_EXPORT int harp_syrk_t_bf16(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits,
-                                 hipStream_t s) {
+                                 int variant, hipStream_t s) {
   if (d_pad % 128 || n % KT || ld < n || ld % 8 || ldg < d_pad) return HARP_EBADARG;
   if (n == 0) return HARP_OK;
-  if (d_pad >= 512 && d_pad % 256 == 0) return launch_syrk<256, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+  const bool big = d_pad >= 512 && d_pad % 256 == 0;
+  if (variant == 1) {
+    if (big) return launch_syrk<256, 2, 4, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    return launch_syrk<128, 2, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 2048, s);
+  }
+  if (variant != 0) return HARP_EBADARG;
+  if (big) return launch_syrk<256, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
   return launch_syrk<128, 2, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 2048, s);
 }
 

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--d", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--variant", type=int, default=None)
+    ap.add_argument("--splits", type=int, default=0)
     a = ap.parse_args()
     import torch
 
@@ -35,7 +37,7 @@ def main():
     torch.cuda.synchronize()
 
     def one_pass():
-        G = LA.syrk_t(fm)
+        G = LA.syrk_t(fm, num_splits=a.splits, variant=a.variant)
         part = reduce_partials(comm, {"g": G}, dtype=torch.float32)
         Gs = LA.symmetrize_upper(part["g"]).double()
         d = a.d
@@ -60,7 +62,7 @@ def main():
     if r == 0:
         s, e = torch.cuda.Event(True), torch.cuda.Event(True)
         s.record()
-        LA.syrk_t(fm)
+        LA.syrk_t(fm, num_splits=a.splits, variant=a.variant)
         e.record()
         e.synchronize()
         t_syrk = s.elapsed_time(e) / 1e3

@@ -40,3 +40,15 @@ def test_covariance_gpu_matches_cpu(cuda):
     g = ST.covariance(X.to(cuda).float())
     c = ST.covariance(X.to(torch.bfloat16).double())
     assert torch.allclose(g["covariance"].cpu(), c["covariance"], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("n,d", [(4096, 100), (20032, 700), (30016, 1000)])
+def test_syrk_variants_agree(cuda, variant, n, d):
+    X = torch.rand(n, d, device=cuda) * 2 - 1
+    fm = LA.FeatureMajor.from_rows(X)
+    G = LA.symmetrize_upper(LA.syrk_t(fm, variant=variant))
+    Xb = torch.cat([X.to(torch.bfloat16).double(), torch.ones(n, 1, device=cuda, dtype=torch.float64)], 1)
+    ref = Xb.t() @ Xb
+    got = G[: d + 1, : d + 1].double()
+    assert torch.allclose(got, ref, rtol=2e-5, atol=1e-2), (got - ref).abs().max()
