@@ -1,0 +1,344 @@
+// Multithreaded text loaders of the data sources: dense CSV, COO triples, libsvm.
+//
+// Reference: core/harp-daal-interface/.../datasource/HarpDAALDataSource.java:198-333 with
+// MTReader / ReadDenseCSVTask / ReadCOOTask (one Java thread per FILE; per line
+// String.split + Double.parseDouble into boxed double[] rows), and the sharded variant
+// ReadDenseCSVShardingTask.java:90-139.
+//
+// Here one file is mmap'ed and cut into byte ranges that start at line boundaries; each range
+// is scanned by its own std::thread in two passes: (1) count records (and fields / nnz) so a
+// prefix sum gives every range its output offset, (2) parse with std::from_chars straight
+// into the caller's preallocated (numpy) buffers — no per-line allocation, no locale, no
+// GIL. Tokens are maximal runs of characters other than the separator and blanks, so
+// "1, 2,3," and "1 2 3" both give three fields; blank lines are skipped, and for COO /
+// libsvm so are lines starting with '%' or '#'.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <charconv>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "harp_runtime.h"
+
+namespace {
+
+struct Range {
+  const char* b;
+  const char* e;
+  int64_t rows = 0;   // records in the range (pass 1)
+  int64_t nnz = 0;    // libsvm entries in the range (pass 1)
+  int64_t width = 0;  // max fields per record (pass 1)
+  int64_t max_index = 0;
+  int err = 0;
+};
+
+struct TextFile {
+  int fd = -1;
+  const char* data = nullptr;
+  size_t size = 0;
+  std::vector<Range> ranges;
+};
+
+inline bool is_blank(char c) { return c == ' ' || c == '\t' || c == '\r'; }
+
+inline bool is_delim(char c, char sep) { return c == sep || is_blank(c); }
+
+// next token in [p, e) (stops at '\n'); returns false at end of line
+inline bool next_token(const char*& p, const char* e, char sep, const char*& tb, const char*& te) {
+  while (p < e && *p != '\n' && is_delim(*p, sep)) ++p;
+  if (p >= e || *p == '\n') return false;
+  tb = p;
+  while (p < e && *p != '\n' && !is_delim(*p, sep)) ++p;
+  te = p;
+  return true;
+}
+
+inline const char* line_end(const char* p, const char* e) {
+  const void* q = memchr(p, '\n', (size_t)(e - p));
+  return q ? (const char*)q : e;
+}
+
+inline bool skip_line(const char* p, const char* le, bool comments) {
+  while (p < le && is_blank(*p)) ++p;
+  if (p == le) return true;
+  return comments && (*p == '%' || *p == '#');
+}
+
+inline int parse_double(const char* b, const char* e, double* out) {
+  if (b < e && *b == '+') ++b;
+  auto r = std::from_chars(b, e, *out);
+  return (r.ec == std::errc() && r.ptr == e) ? 0 : 1;
+}
+
+inline int parse_long(const char* b, const char* e, int64_t* out) {
+  if (b < e && *b == '+') ++b;
+  auto r = std::from_chars(b, e, *out);
+  if (r.ec == std::errc() && r.ptr == e) return 0;
+  double d;  // tolerate "12.0" style integer fields
+  if (parse_double(b, e, &d) == 0 && d == (double)(int64_t)d) {
+    *out = (int64_t)d;
+    return 0;
+  }
+  return 1;
+}
+
+template <class F>
+void run_ranges(TextFile* f, F fn) {
+  std::vector<std::thread> ts;
+  for (size_t i = 1; i < f->ranges.size(); ++i) ts.emplace_back(fn, std::ref(f->ranges[i]));
+  if (!f->ranges.empty()) fn(f->ranges[0]);
+  for (auto& t : ts) t.join();
+}
+
+int first_error(TextFile* f) {
+  for (auto& r : f->ranges)
+    if (r.err) return r.err;
+  return 0;
+}
+
+}  // namespace
+
+// Map `path` and split it into up to `nthreads` line-aligned ranges. NULL on failure.
+HARP_HOST_EXPORT void* harp_text_open(const char* path, int nthreads) {
+  auto* f = new TextFile();
+  f->fd = open(path, O_RDONLY);
+  if (f->fd < 0) {
+    delete f;
+    return nullptr;
+  }
+  struct stat st;
+  if (fstat(f->fd, &st) != 0) {
+    close(f->fd);
+    delete f;
+    return nullptr;
+  }
+  f->size = (size_t)st.st_size;
+  if (f->size > 0) {
+    void* m = mmap(nullptr, f->size, PROT_READ, MAP_PRIVATE, f->fd, 0);
+    if (m == MAP_FAILED) {
+      close(f->fd);
+      delete f;
+      return nullptr;
+    }
+    madvise(m, f->size, MADV_SEQUENTIAL);
+    f->data = (const char*)m;
+  }
+  const char* b = f->data;
+  const char* e = f->data + f->size;
+  int T = std::max(1, std::min(nthreads, 256));
+  if (f->size < ((size_t)1 << 16)) T = 1;  // small files: one range
+  std::vector<const char*> starts{b};
+  for (int t = 1; t < T; ++t) {
+    const char* s = b + f->size * (size_t)t / (size_t)T;
+    if (s <= starts.back()) continue;
+    const char* le = line_end(s - 1, e);  // a line starting exactly at s begins after s-1's '\n'
+    const char* next = le < e ? le + 1 : e;
+    if (next > starts.back() && next < e) starts.push_back(next);
+  }
+  for (size_t i = 0; i < starts.size(); ++i) {
+    Range r;
+    r.b = starts[i];
+    r.e = i + 1 < starts.size() ? starts[i + 1] : e;
+    f->ranges.push_back(r);
+  }
+  return f;
+}
+
+HARP_HOST_EXPORT void harp_text_close(void* h) {
+  auto* f = (TextFile*)h;
+  if (!f) return;
+  if (f->data) munmap((void*)f->data, f->size);
+  if (f->fd >= 0) close(f->fd);
+  delete f;
+}
+
+// ---- dense rows -------------------------------------------------------------------------
+// pass 1: non-blank lines and the widest line's field count
+HARP_HOST_EXPORT int harp_dense_shape(void* h, char sep, int64_t* rows, int64_t* cols) {
+  auto* f = (TextFile*)h;
+  run_ranges(f, [sep](Range& r) {
+    const char* p = r.b;
+    while (p < r.e) {
+      const char* le = line_end(p, r.e);
+      if (!skip_line(p, le, false)) {
+        int64_t k = 0;
+        const char *q = p, *tb, *te;
+        while (next_token(q, le, sep, tb, te)) ++k;
+        r.width = std::max(r.width, k);
+        ++r.rows;
+      }
+      p = le + 1;
+    }
+  });
+  int64_t n = 0, w = 0;
+  for (auto& r : f->ranges) {
+    n += r.rows;
+    w = std::max(w, r.width);
+  }
+  *rows = n;
+  *cols = w;
+  return 0;
+}
+
+// pass 2: out[rows][ld] (row-major, zero-filled by the caller; short rows stay 0-padded)
+HARP_HOST_EXPORT int harp_dense_fill(void* h, char sep, double* out, int64_t ld) {
+  auto* f = (TextFile*)h;
+  std::vector<int64_t> base(f->ranges.size(), 0);
+  for (size_t i = 1; i < f->ranges.size(); ++i) base[i] = base[i - 1] + f->ranges[i - 1].rows;
+  std::vector<std::thread> ts;
+  auto work = [&](size_t i) {
+    Range& r = f->ranges[i];
+    int64_t row = base[i];
+    const char* p = r.b;
+    while (p < r.e) {
+      const char* le = line_end(p, r.e);
+      if (!skip_line(p, le, false)) {
+        double* o = out + row * ld;
+        int64_t k = 0;
+        const char *q = p, *tb, *te;
+        while (next_token(q, le, sep, tb, te) && k < ld)
+          if (parse_double(tb, te, o + k++)) r.err = 2;
+        ++row;
+      }
+      p = le + 1;
+    }
+  };
+  for (size_t i = 1; i < f->ranges.size(); ++i) ts.emplace_back(work, i);
+  if (!f->ranges.empty()) work(0);
+  for (auto& t : ts) t.join();
+  return first_error(f);
+}
+
+// ---- COO triples `row col value` ---------------------------------------------------------
+HARP_HOST_EXPORT int harp_coo_count(void* h, int64_t* n) {
+  auto* f = (TextFile*)h;
+  run_ranges(f, [](Range& r) {
+    const char* p = r.b;
+    while (p < r.e) {
+      const char* le = line_end(p, r.e);
+      if (!skip_line(p, le, true)) ++r.rows;
+      p = le + 1;
+    }
+  });
+  int64_t t = 0;
+  for (auto& r : f->ranges) t += r.rows;
+  *n = t;
+  return 0;
+}
+
+HARP_HOST_EXPORT int harp_coo_fill(void* h, char sep, int64_t* rows, int64_t* cols, double* vals) {
+  auto* f = (TextFile*)h;
+  std::vector<int64_t> base(f->ranges.size(), 0);
+  for (size_t i = 1; i < f->ranges.size(); ++i) base[i] = base[i - 1] + f->ranges[i - 1].rows;
+  std::vector<std::thread> ts;
+  auto work = [&](size_t i) {
+    Range& r = f->ranges[i];
+    int64_t k = base[i];
+    const char* p = r.b;
+    while (p < r.e) {
+      const char* le = line_end(p, r.e);
+      if (!skip_line(p, le, true)) {
+        const char *q = p, *tb, *te;
+        int got = 0;
+        if (next_token(q, le, sep, tb, te) && !parse_long(tb, te, rows + k)) ++got;
+        if (next_token(q, le, sep, tb, te) && !parse_long(tb, te, cols + k)) ++got;
+        if (next_token(q, le, sep, tb, te) && !parse_double(tb, te, vals + k)) ++got;
+        if (got != 3) r.err = 2;
+        ++k;
+      }
+      p = le + 1;
+    }
+  };
+  for (size_t i = 1; i < f->ranges.size(); ++i) ts.emplace_back(work, i);
+  if (!f->ranges.empty()) work(0);
+  for (auto& t : ts) t.join();
+  return first_error(f);
+}
+
+// ---- libsvm `label idx:val ...` (1-based idx) -> CSR ---------------------------------------
+HARP_HOST_EXPORT int harp_libsvm_count(void* h, int64_t* rows, int64_t* nnz, int64_t* max_index) {
+  auto* f = (TextFile*)h;
+  run_ranges(f, [](Range& r) {
+    const char* p = r.b;
+    while (p < r.e) {
+      const char* le = line_end(p, r.e);
+      if (!skip_line(p, le, true)) {
+        const char *q = p, *tb, *te;
+        next_token(q, le, ' ', tb, te);  // label
+        while (next_token(q, le, ' ', tb, te)) {
+          const char* c = (const char*)memchr(tb, ':', (size_t)(te - tb));
+          int64_t idx;
+          if (!c || parse_long(tb, c, &idx)) {
+            r.err = 2;
+            continue;
+          }
+          r.max_index = std::max(r.max_index, idx);
+          ++r.nnz;
+        }
+        ++r.rows;
+      }
+      p = le + 1;
+    }
+  });
+  int64_t n = 0, z = 0, m = 0;
+  for (auto& r : f->ranges) {
+    n += r.rows;
+    z += r.nnz;
+    m = std::max(m, r.max_index);
+  }
+  *rows = n;
+  *nnz = z;
+  *max_index = m;
+  return first_error(f);
+}
+
+// y[rows], indptr[rows + 1], indices[nnz] (0-based), values[nnz]
+HARP_HOST_EXPORT int harp_libsvm_fill(void* h, double* y, int64_t* indptr, int64_t* indices, double* values) {
+  auto* f = (TextFile*)h;
+  const size_t R = f->ranges.size();
+  std::vector<int64_t> rbase(R, 0), zbase(R, 0);
+  for (size_t i = 1; i < R; ++i) {
+    rbase[i] = rbase[i - 1] + f->ranges[i - 1].rows;
+    zbase[i] = zbase[i - 1] + f->ranges[i - 1].nnz;
+  }
+  std::vector<std::thread> ts;
+  auto work = [&](size_t i) {
+    Range& r = f->ranges[i];
+    int64_t row = rbase[i], z = zbase[i];
+    const char* p = r.b;
+    while (p < r.e) {
+      const char* le = line_end(p, r.e);
+      if (!skip_line(p, le, true)) {
+        const char *q = p, *tb, *te;
+        indptr[row] = z;
+        if (!next_token(q, le, ' ', tb, te) || parse_double(tb, te, y + row)) r.err = 2;
+        while (next_token(q, le, ' ', tb, te)) {
+          const char* c = (const char*)memchr(tb, ':', (size_t)(te - tb));
+          int64_t idx;
+          if (!c || parse_long(tb, c, &idx) || parse_double(c + 1, te, values + z)) {
+            r.err = 2;
+            continue;
+          }
+          indices[z++] = idx - 1;
+        }
+        ++row;
+      }
+      p = le + 1;
+    }
+  };
+  for (size_t i = 1; i < R; ++i) ts.emplace_back(work, i);
+  if (R) work(0);
+  for (auto& t : ts) t.join();
+  int64_t rows = 0, nnz = 0;
+  for (auto& r : f->ranges) {
+    rows += r.rows;
+    nnz += r.nnz;
+  }
+  indptr[rows] = nnz;
+  return first_error(f);
+}

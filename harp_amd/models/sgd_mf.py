@@ -36,6 +36,8 @@ class SGDConfig:
     epochs: int = 10
     num_slices: int = 2        # model slices per worker (numModelSlices)
     chunk: int = 64            # ratings per GPU update stream
+    xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
+    blocks_per_xcd: int = 256  # workgroups per XCD of the blocked kernel
     random_order: bool = False  # random rotation orders (RotationUtil) vs ring
     test_every: int = 5        # rmseIteInterval
     seed: int = 0
@@ -81,22 +83,45 @@ def row_owner(users: torch.Tensor, P: int, seed: int = 0) -> torch.Tensor:
 
 
 class _Buckets:
-    """Ratings of this worker bucketed by global H slice, user-sorted inside a bucket."""
+    """Ratings of this worker bucketed by global H slice, user-sorted inside a bucket.
 
-    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device):
+    ``cells=(n_rows, items_per_slice)``: inside a slice the ratings are further grouped
+    into the 8 x 8 (user block, item block) cells of the XCD-blocked kernel
+    (``ops.mf.sgd_update_blocked``), user-sorted inside a cell; ``cell_off[s]`` holds the
+    65 cell offsets of slice s (relative to the slice start)."""
+
+    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device, cells=None):
         g = slice_of_item[cols]
-        key = g * (int(rows.max().item()) + 1 if rows.numel() else 1) + rows
+        lc = local_of_item[cols]
+        span = int(rows.max().item()) + 1 if rows.numel() else 1
+        nc = MF.XCDS * MF.XCDS
+        if cells is not None:
+            cid = g * nc + MF.cell_layout(rows, lc, cells[0], cells[1])
+            key = cid * span + rows
+        else:
+            key = g * span + rows
         order = torch.argsort(key)
         self.rows = rows[order].to(torch.int32).contiguous().to(device)
-        self.cols = local_of_item[cols[order]].to(torch.int32).contiguous().to(device)
+        self.cols = lc[order].to(torch.int32).contiguous().to(device)
         self.vals = vals[order].to(torch.float32).contiguous().to(device)
         counts = torch.bincount(g, minlength=n_slices).cpu()
         self.offsets = [0] + torch.cumsum(counts, 0).tolist()
         self.n = rows.numel()
+        self.cell_off = None
+        if cells is not None:
+            cc = torch.bincount(cid, minlength=n_slices * nc).cpu().view(n_slices, nc)
+            off = torch.zeros((n_slices, nc + 1), dtype=torch.int64)
+            off[:, 1:] = torch.cumsum(cc, 1)
+            self.cell_off_host = off.tolist()
+            self.cell_off = off.to(device)
 
     def get(self, s: int):
         a, b = self.offsets[s], self.offsets[s + 1]
         return self.rows[a:b], self.cols[a:b], self.vals[a:b]
+
+    def get_cells(self, s: int):
+        """(rows, cols, vals, device cell offsets, host cell offsets) of slice s."""
+        return (*self.get(s), self.cell_off[s], self.cell_off_host[s])
 
 
 class SGDCollectiveMapper(CollectiveMapper):
@@ -135,7 +160,8 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.slice_of_item = (pos // self.ips).to(u.device)
         self.local_of_item = (pos % self.ips).to(u.device)
         self.item_perm = perm  # slice s holds items perm[s*ips:(s+1)*ips]
-        self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev)
+        cells = (self.users.numel(), self.ips) if cfg.xcd_blocks else None
+        self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells)
         if self._test is not None:
             tu, ti, tv = self._test
             m = self._owner(tu) == me
@@ -182,7 +208,12 @@ class SGDCollectiveMapper(CollectiveMapper):
                 slab = self.rot.get(k)
                 gs = block * S + k
                 with timer.phase("compute"):
-                    n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
+                    if cfg.xcd_blocks:
+                        r_, c_, v_, off, hoff = self.train.get_cells(gs)
+                        n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
+                                                   cfg.blocks_per_xcd, host_off=hoff)
+                    else:
+                        n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
                 with timer.phase("rotate"):
                     self.rot.start(k, self.schedule.rotation_map(epoch, s))
         self.trained += n

@@ -18,6 +18,10 @@ SUPPORTED_RANKS = (16, 32, 48, 64, 128, 256)
 _lib.register({
     "harp_mf_sgd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
                     _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_void_p],
+    "harp_mf_xcds": [],
+    "harp_mf_sgd_xcd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
+                        _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float,
+                        _lib.c_void_p],
     "harp_mf_rmse_blocks": [],
     "harp_mf_rmse": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int,
                      _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
@@ -65,6 +69,54 @@ def sgd_update(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: to
         return n
     _rt().harp_mf_sgd_cpu(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, W.data_ptr(), W.stride(0),
                           H.data_ptr(), H.stride(0), float(lr), float(lam))
+    return n
+
+
+XCDS = 8  # cells per side of the XCD-blocked layout (csrc/mf_sgd.hip)
+
+
+def cell_layout(rows: torch.Tensor, cols: torch.Tensor, n_rows: int, n_cols: int, nb: int = XCDS) -> torch.Tensor:
+    """Cell id (user block * nb + item block) of every rating: contiguous user / item
+    ranges, so a cell's H rows are one contiguous 1/nb of the slice."""
+    rb = (rows.long() * nb) // max(n_rows, 1)
+    cb = (cols.long() * nb) // max(n_cols, 1)
+    return rb * nb + cb
+
+
+def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, cell_off: torch.Tensor,
+                       W: torch.Tensor, H: torch.Tensor, lr: float, lam: float, chunk: int = 64,
+                       blocks_per_xcd: int = 256, host_off: list | None = None) -> int:
+    """One SGD pass over ratings laid out in nb x nb cells (cell-major, user-sorted inside a
+    cell; ``cell_off`` = nb*nb+1 int64 offsets on W's device). Sub-step s trains the nb
+    row- and column-disjoint cells (x, (x+s) mod nb): on the GPU one XCD per cell
+    (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
+    ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path)."""
+    _check(rows, cols, vals, W, H)
+    n = rows.numel()
+    if n == 0:
+        return 0
+    r = W.shape[1]
+    nb = XCDS
+    assert cell_off.numel() == nb * nb + 1 and cell_off.dtype == torch.int64
+    if _lib.use_native(W):
+        if r not in SUPPORTED_RANKS:
+            raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS}, got {r}")
+        assert cell_off.device == W.device and cell_off.is_contiguous()
+        lib = _lib.kernels()
+        st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(), r, nb, chunk,
+                                 blocks_per_xcd, W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr),
+                                 float(lam), _lib.stream_ptr(W.device))
+        _lib.check(st, "mf_sgd_xcd")
+        return n
+    off = host_off if host_off is not None else cell_off.tolist()
+    rt = _rt()
+    for s in range(nb):
+        for x in range(nb):
+            c = x * nb + (x + s) % nb
+            a, b = off[c], off[c + 1]
+            if b > a:
+                rt.harp_mf_sgd_cpu(rows[a:].data_ptr(), cols[a:].data_ptr(), vals[a:].data_ptr(), b - a, r,
+                                   W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam))
     return n
 
 

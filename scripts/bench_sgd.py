@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--lr", type=float, default=0.002)
     ap.add_argument("--lam", type=float, default=0.05)
+    ap.add_argument("--layout", choices=("xcd", "flat"), default="xcd")
+    ap.add_argument("--blocks-per-xcd", type=int, default=256)
     a = ap.parse_args()
     import torch
 
@@ -37,7 +39,8 @@ def main():
     t0 = time.perf_counter()
     u, i, v = synthetic_ratings(a.users, a.items, a.ratings, seed=7, device=dev)
     gen_s = time.perf_counter() - t0
-    cfg = SGDConfig(rank=a.rank, lam=a.lam, lr=a.lr, epochs=a.warmup + a.epochs, chunk=a.chunk, test_every=0)
+    cfg = SGDConfig(rank=a.rank, lam=a.lam, lr=a.lr, epochs=a.warmup + a.epochs, chunk=a.chunk, test_every=0,
+                    xcd_blocks=a.layout == "xcd", blocks_per_xcd=a.blocks_per_xcd)
     m = SGDCollectiveMapper(comm, cfg, a.users, a.items, (u, i, v), None)
     m.init_model(KeyValReader([]))
     del u, i, v
@@ -70,7 +73,8 @@ def main():
         print(json.dumps({"metric": "MF-SGD updates/sec (Netflix-shape synthetic, rank 128, model rotation)",
                           "value": n / dt, "unit": "updates/s", "n_gpus": comm.world_size, "epochs": a.epochs,
                           "s_per_epoch": dt / a.epochs, "train_rmse": tr, "data_gen_s": gen_s,
-                          "ratings": a.ratings, "rank": a.rank, "dtype": "fp32 factors"}), flush=True)
+                          "ratings": a.ratings, "rank": a.rank, "dtype": "fp32 factors",
+                          "layout": a.layout, "chunk": a.chunk, "blocks_per_xcd": a.blocks_per_xcd}), flush=True)
     shutdown()
 
 

@@ -79,3 +79,52 @@ def test_sgd_movielens_fixture_two_workers():
     res = launch(_job, 2, args=(cfg, nu, ni, train, test), timeout=600)
     hist = res[0]["rmse"]
     assert hist[-1][2] < 1.0 and hist[-1][1] < hist[0][1], hist
+
+
+def test_xcd_cell_layout_and_blocked_schedule():
+    """The 8 x 8 cell layout is a permutation of the slice, cells of one sub-step are
+    user- and item-disjoint, and the blocked CPU pass equals a sequential pass over the
+    cells in schedule order."""
+    from harp_amd.ops import mf as MF
+
+    g = torch.Generator().manual_seed(3)
+    nu, ni, n, r = 200, 96, 6000, 16
+    rows = torch.randint(0, nu, (n,), generator=g)
+    cols = torch.randint(0, ni, (n,), generator=g)
+    vals = torch.rand(n, generator=g) * 4 + 1
+    cid = MF.cell_layout(rows, cols, nu, ni)
+    order = torch.argsort(cid * nu + rows)
+    R, C, V, cid = rows[order].int(), cols[order].int(), vals[order].float(), cid[order]
+    off = torch.zeros(65, dtype=torch.int64)
+    off[1:] = torch.cumsum(torch.bincount(cid, minlength=64), 0)
+    for s in range(8):
+        us, its = set(), set()
+        for x in range(8):
+            c = x * 8 + (x + s) % 8
+            u = set(R[off[c]:off[c + 1]].tolist())
+            i = set(C[off[c]:off[c + 1]].tolist())
+            assert not (u & us) and not (i & its)
+            us |= u
+            its |= i
+    W0 = torch.rand(nu, r, generator=g) * 0.3
+    H0 = torch.rand(ni, r, generator=g) * 0.3
+    Wb, Hb = W0.clone(), H0.clone()
+    assert MF.sgd_update_blocked(R, C, V, off, Wb, Hb, 0.01, 0.05) == n
+    Ws, Hs = W0.clone(), H0.clone()
+    for s in range(8):
+        for x in range(8):
+            c = x * 8 + (x + s) % 8
+            a, b = int(off[c]), int(off[c + 1])
+            MF.sgd_update(R[a:b].contiguous(), C[a:b].contiguous(), V[a:b].contiguous(), Ws, Hs, 0.01, 0.05)
+    assert torch.equal(Wb, Ws) and torch.equal(Hb, Hs)
+
+
+def test_sgd_flat_and_blocked_layouts_both_converge(small):
+    nu, ni, train, test = small
+    out = {}
+    for blocked in (False, True):
+        cfg = SGDConfig(rank=16, lam=0.05, lr=0.01, epochs=12, test_every=12, xcd_blocks=blocked)
+        out[blocked] = launch(_job, 2, args=(cfg, nu, ni, train, test), timeout=300)[0]
+    for blocked in (False, True):
+        assert out[blocked]["rmse"][-1][2] < 0.6, out[blocked]["rmse"]
+    assert abs(out[True]["rmse"][-1][2] - out[False]["rmse"][-1][2]) < 0.05

@@ -52,3 +52,51 @@ def test_sgd_gpu_converges_like_cpu(cuda):
     # ~1.7k concurrent Hogwild streams on only 800 items: staleness costs a little accuracy
     assert abs(g["rmse"][-1][2] - c["rmse"][-1][2]) < 0.04, (g["rmse"], c["rmse"])
     assert g["trained"] == c["trained"] == 10 * k
+
+
+def _cells(nu, ni, n, r, seed):
+    g = torch.Generator().manual_seed(seed)
+    rows = torch.randint(0, nu, (n,), generator=g)
+    cols = torch.randint(0, ni, (n,), generator=g)
+    vals = torch.rand(n, generator=g) * 4 + 1
+    cid = MF.cell_layout(rows, cols, nu, ni)
+    order = torch.argsort(cid * nu + rows)
+    off = torch.zeros(65, dtype=torch.int64)
+    off[1:] = torch.cumsum(torch.bincount(cid, minlength=64), 0)
+    W0 = torch.rand(nu, r, generator=g) * 0.3
+    H0 = torch.rand(ni, r, generator=g) * 0.3
+    return rows[order].int(), cols[order].int(), vals[order].float(), off, W0, H0
+
+
+@pytest.mark.parametrize("r", [16, 128])
+def test_sgd_xcd_one_stream_per_cell_matches_cpu(cuda, r):
+    """chunk >= cell size: one stream per cell, and the 8 cells of a sub-step share no user
+    and no item, so the XCD-blocked kernel is deterministic and equals the CPU schedule."""
+    R, C, V, off, W0, H0 = _cells(64, 48, 4000, r, 1)
+    Wc, Hc = W0.clone(), H0.clone()
+    MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.01, 0.05)
+    Wg, Hg = W0.to(cuda), H0.to(cuda)
+    MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=1 << 20,
+                          blocks_per_xcd=4)
+    torch.cuda.synchronize()
+    assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
+
+
+def test_sgd_xcd_many_streams_close_to_cpu(cuda):
+    """Hogwild inside each cell (~780 streams on ~100 items per XCD): after a few passes the
+    error lands close to the sequential schedule's (H rows are read from L2, so concurrent
+    streams see each other's updates)."""
+    R, C, V, off, W0, H0 = _cells(3000, 800, 200000, 32, 2)
+    Wc, Hc = W0.clone(), H0.clone()
+    Wg, Hg = W0.to(cuda), H0.to(cuda)
+    Rg, Cg, Vg, og = R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda)
+    for _ in range(5):
+        MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.005, 0.05)
+        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wg, Hg, 0.005, 0.05, chunk=32)
+    torch.cuda.synchronize()
+    e0 = MF.sse(R, C, V, W0, H0).item()
+    e_cpu = MF.sse(R, C, V, Wc, Hc).item()
+    e_gpu = MF.sse(Rg, Cg, Vg, Wg, Hg).item()
+    print(f"sse initial {e0:.4g} cpu {e_cpu:.4g} gpu-xcd {e_gpu:.4g}")
+    assert e_gpu < 0.5 * e0
+    assert abs(e_gpu - e_cpu) < 0.1 * e_cpu, (e_gpu, e_cpu)
