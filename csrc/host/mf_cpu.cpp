@@ -12,11 +12,13 @@ HARP_HOST_EXPORT void harp_mf_sgd_cpu(const int32_t* rows, const int32_t* cols, 
     float* h = H + (int64_t)cols[i] * ldh;
     float dot = 0.f;
     for (int k = 0; k < r; ++k) dot = fmaf(w[k], h[k], dot);
-    const float err = dot - vals[i];
+    const float ge = -lr * (dot - vals[i]);
+    const float decay = 1.0f - lr * lam;
+    // w' = w - lr*(err*h + lam*w) = (1 - lr*lam) w - lr*err*h  (and h' alike)
     for (int k = 0; k < r; ++k) {
       const float wk = w[k], hk = h[k];
-      w[k] = wk - lr * fmaf(err, hk, lam * wk);
-      h[k] = hk - lr * fmaf(err, wk, lam * hk);
+      w[k] = fmaf(ge, hk, decay * wk);
+      h[k] = fmaf(ge, wk, decay * hk);
     }
   }
 }

@@ -62,6 +62,18 @@ __device__ __forceinline__ void load_row_l2(const float* __restrict__ p, float (
 }
 
 template <int EPL>
+__device__ __forceinline__ void store_row_nt(float* __restrict__ p, const float (&x)[EPL]) {
+  if constexpr (EPL % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4)
+      __builtin_nontemporal_store(floatx4{x[k], x[k + 1], x[k + 2], x[k + 3]}, (floatx4*)(p + k));
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) __builtin_nontemporal_store(x[k], p + k);
+  }
+}
+
+template <int EPL>
 __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&x)[EPL]) {
   if constexpr (EPL % 4 == 0) {
 #pragma unroll
@@ -72,66 +84,141 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&x
   }
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+// Sum over the 16 lanes of a DPP row (= one update stream), result in every lane: row
+// rotations by 8 and 4, then the two quad permutations. Four dependent VALU ops with DPP
+// operands instead of four ds_bpermute round trips through the LDS crossbar.
 __device__ __forceinline__ float sub16_sum(float v) {
-  v += __shfl_xor(v, 8, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 1, 64);
+  v += dpp<0x128>(v);  // row_ror:8
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
   return v;
 }
 
-// One update stream: ratings [i0, i1) in order, run by the 16-lane subgroup holding lane `sl`.
+__device__ __forceinline__ int shfl16(int v, int src) { return __shfl(v, src, 16); }
+__device__ __forceinline__ float shfl16(float v, int src) { return __shfl(v, src, 16); }
+
+// 16 consecutive ratings, one per lane of the subgroup (coalesced; masked past u1)
+__device__ __forceinline__ void load16(const int* __restrict__ rows, const int* __restrict__ cols,
+                                       const float* __restrict__ vals, unsigned base, unsigned u1, int sl, int& r,
+                                       int& c, float& v) {
+  const unsigned k = base + (unsigned)sl;
+  if (k < u1) {
+    r = rows[k];
+    c = cols[k];
+    v = vals[k];
+  }
+}
+
+// One update stream: ratings [u0, u1) of rows/cols/vals in order, run by the 16-lane
+// subgroup holding lane `sl`.
+//  * indices: the (row, col, value) triples arrive 16 at a time (one per lane, the next batch
+//    in flight) and are broadcast inside the subgroup, so an H-row prefetch never waits on
+//    an index load;
+//  * H rows are prefetched TWO ratings ahead into ping-pong buffers, and each prefetch is
+//    issued after the previous rating's H store. CDNA's vmcnt retires loads and stores in
+//    issue order, so with a distance of one every wait for the next row also waited for the
+//    store just issued (measured: dropping the stores alone ran 1.7x faster); at distance two
+//    the wait only covers the load issued a full update earlier. A row is forwarded in
+//    registers when the next rating hits the same item; a row loaded after the store of the
+//    same item (same wave, program order) already sees it;
+//  * update w' = (1 - lr*lam) w - lr*err*h (and h' alike): 2 packed fp32 ops per factor pair.
+// All offsets are 32-bit (uniform 64-bit bases stay in SGPRs).
 template <int R>
 __device__ __forceinline__ void sgd_stream(const int* __restrict__ rows, const int* __restrict__ cols,
-                                           const float* __restrict__ vals, long i0, long i1, int sl,
-                                           float* __restrict__ W, int ldw, float* __restrict__ H, int ldh, float lr,
-                                           float lam) {
+                                           const float* __restrict__ vals, unsigned u0, unsigned u1, int sl,
+                                           float* __restrict__ W, unsigned ldw, float* __restrict__ H, unsigned ldh,
+                                           float lr, float lam) {
   constexpr int EPL = R / 16;
-  float w[EPL], h[EPL], hn[EPL];
-  int cur = rows[i0];
-  load_row<EPL>(W + (long)cur * ldw + sl * EPL, w);
-  int col = cols[i0];
-  float v = vals[i0];
-  load_row_l2<EPL>(H + (long)col * ldh + sl * EPL, h);
-  for (long i = i0; i < i1; ++i) {
-    // prefetch the next rating and its H row
-    int nrow = cur, ncol = col;
-    float nv = 0.f;
-    const bool more = i + 1 < i1;
-    if (more) {
-      nrow = rows[i + 1];
-      ncol = cols[i + 1];
-      nv = vals[i + 1];
-      load_row_l2<EPL>(H + (long)ncol * ldh + sl * EPL, hn);
-    }
-    float dot = 0.f;
+  constexpr int PAIRS = EPL / 2;
+  const float decay = 1.0f - lr * lam;
+  const unsigned lo = (unsigned)sl * EPL;
+  float w[EPL], h[EPL], hA[EPL], hB[EPL];
+  unsigned base = u0;
+  int bR = 0, bC = 0, nR = 0, nC = 0;
+  float bV = 0.f, nV = 0.f;
+  load16(rows, cols, vals, base, u1, sl, bR, bC, bV);
+  load16(rows, cols, vals, base + 16, u1, sl, nR, nC, nV);
+  // rating i = u0 (current) and i + 1 (in flight)
+  unsigned cur = (unsigned)shfl16(bR, 0), col0 = (unsigned)shfl16(bC, 0);
+  float v0 = shfl16(bV, 0);
+  unsigned row1 = (unsigned)shfl16(bR, 1), col1 = (unsigned)shfl16(bC, 1);
+  float v1 = shfl16(bV, 1);
+  load_row<EPL>(W + (cur * ldw + lo), w);
+  load_row_l2<EPL>(H + (col0 * ldh + lo), h);
+  if (u0 + 1 < u1) load_row_l2<EPL>(H + (col1 * ldh + lo), hB);
+  unsigned i = u0;
+
+  // one rating; `hl` receives the prefetch of rating i + 2, `hx` holds rating i + 1's row
+  auto step = [&](float(&hl)[EPL], float(&hx)[EPL]) -> bool {
+    floatx2 d2 = {0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) dot = fmaf(w[k], h[k], dot);
-    const float err = sub16_sum(dot) - v;
+    for (int p = 0; p < PAIRS; ++p)
+      d2 = __builtin_elementwise_fma(floatx2{w[2 * p], w[2 * p + 1]}, floatx2{h[2 * p], h[2 * p + 1]}, d2);
+    float dot = d2[0] + d2[1];
+    if constexpr (EPL % 2) dot = fmaf(w[EPL - 1], h[EPL - 1], dot);
+    const float ge = -lr * (sub16_sum(dot) - v0);
+    const floatx2 g = {ge, ge}, dc = {decay, decay};
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const float wk = w[k], hk = h[k];
-      w[k] = wk - lr * fmaf(err, hk, lam * wk);
-      h[k] = hk - lr * fmaf(err, wk, lam * hk);
+    for (int p = 0; p < PAIRS; ++p) {
+      const floatx2 wk = {w[2 * p], w[2 * p + 1]}, hk = {h[2 * p], h[2 * p + 1]};
+      const floatx2 wn = __builtin_elementwise_fma(g, hk, dc * wk);
+      const floatx2 hn = __builtin_elementwise_fma(g, wk, dc * hk);
+      w[2 * p] = wn[0];
+      w[2 * p + 1] = wn[1];
+      h[2 * p] = hn[0];
+      h[2 * p + 1] = hn[1];
     }
-    store_row<EPL>(H + (long)col * ldh + sl * EPL, h);
-    if (!more) break;
-    if (ncol == col) {
-      // same item again: use the row just written, not the stale prefetch
+    if constexpr (EPL % 2) {
+      const float wk = w[EPL - 1], hk = h[EPL - 1];
+      w[EPL - 1] = fmaf(ge, hk, decay * wk);
+      h[EPL - 1] = fmaf(ge, wk, decay * hk);
+    }
+    store_row<EPL>(H + (col0 * ldh + lo), h);
+    // indices + prefetch of rating i + 2 (issued after the store above)
+    const unsigned t2 = i + 2 - base;
+    if (t2 == 16) {
+      base += 16;
+      bR = nR;
+      bC = nC;
+      bV = nV;
+      load16(rows, cols, vals, base + 16, u1, sl, nR, nC, nV);
+    }
+    unsigned row2 = row1, col2 = col1;
+    float v2 = 0.f;
+    if (i + 2 < u1) {
+      const int tt = (int)(t2 & 15u);
+      row2 = (unsigned)shfl16(bR, tt);
+      col2 = (unsigned)shfl16(bC, tt);
+      v2 = shfl16(bV, tt);
+      load_row_l2<EPL>(H + (col2 * ldh + lo), hl);
+    }
+    if (i + 1 >= u1) return false;
+    if (row1 != cur) {
+      store_row<EPL>(W + (cur * ldw + lo), w);
+      cur = row1;
+      load_row<EPL>(W + (cur * ldw + lo), w);
+    }
+    if (col1 != col0) {  // else: same item again, keep the row just updated
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) hn[k] = h[k];
+      for (int k = 0; k < EPL; ++k) h[k] = hx[k];
     }
-    if (nrow != cur) {
-      store_row<EPL>(W + (long)cur * ldw + sl * EPL, w);
-      cur = nrow;
-      load_row<EPL>(W + (long)cur * ldw + sl * EPL, w);
-    }
-    col = ncol;
-    v = nv;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) h[k] = hn[k];
+    col0 = col1;
+    v0 = v1;
+    row1 = row2;
+    col1 = col2;
+    v1 = v2;
+    ++i;
+    return true;
+  };
+  while (step(hA, hB) && step(hB, hA)) {
   }
-  store_row<EPL>(W + (long)cur * ldw + sl * EPL, w);
+  store_row<EPL>(W + (cur * ldw + lo), w);
 }
 
 template <int R>
@@ -145,31 +232,142 @@ __global__ __launch_bounds__(256) void mf_sgd_kernel(const int* __restrict__ row
   long i1 = i0 + chunk;
   if (i1 > n) i1 = n;
   if (i0 >= i1) return;
-  sgd_stream<R>(rows, cols, vals, i0, i1, sl, W, ldw, H, ldh, lr, lam);
+  sgd_stream<R>(rows + i0, cols + i0, vals + i0, 0u, (unsigned)(i1 - i0), sl, W, (unsigned)ldw, H, (unsigned)ldh,
+                lr, lam);
 }
 
 constexpr int XCDS = 8;
 
+// One update stream whose (row, col, value) triples sit in LDS (sR/sC/sV[0..n)), staged by
+// the workgroup. CDNA retires vmcnt in issue order and counts stores too, so the loop is
+// ordered never to wait on anything younger than what it consumes (no vmcnt(0) in the loop):
+//  * index reads are LDS traffic (lgkmcnt), not vector memory;
+//  * per rating: update -> W switch (rare; store old row, load new) -> prefetch the H row of
+//    rating i+2 into a ping-pong buffer -> store this rating's H row;
+//  * a prefetch is issued before the stores of the two ratings preceding its use, so a row
+//    is forwarded in registers when rating i+1 repeats the item of rating i or i-1 (the
+//    updated rows of the last two ratings are kept: h, hp).
+// Loads are unconditional (clamped indices), so the wait counts stay exact. Measured on
+// MI355X (profiles/r1_sgd_xcd): per-stream latency is NOT the limit — removing the index /
+// store waits changed nothing, while ablating the H stores (+66 %) or the H loads (+32 %)
+// and uniform instead of skewed item popularity (+30 %) did: the kernel is bound by L2
+// traffic on hot H rows.
+template <int R, bool NTS = false>
+__device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, const float* sV, int n, int sl,
+                                               float* __restrict__ W, unsigned ldw, float* __restrict__ H,
+                                               unsigned ldh, float lr, float lam) {
+  constexpr int EPL = R / 16;
+  constexpr int PAIRS = EPL / 2;
+  const float decay = 1.0f - lr * lam;
+  const unsigned lo = (unsigned)sl * EPL;
+  float w[EPL], h[EPL], hp[EPL], hA[EPL], hB[EPL];
+  unsigned cur = (unsigned)sR[0], col0 = (unsigned)sC[0], colp = 0xffffffffu;
+  float v0 = sV[0];
+  const int i1c = n > 1 ? 1 : 0;
+  unsigned row1 = (unsigned)sR[i1c], col1 = (unsigned)sC[i1c];
+  float v1 = sV[i1c];
+  load_row<EPL>(W + (cur * ldw + lo), w);
+  load_row_l2<EPL>(H + (col0 * ldh + lo), h);
+  load_row_l2<EPL>(H + (col1 * ldh + lo), hB);
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) hp[k] = 0.f;
+  int i = 0;
+  auto step = [&](float(&hl)[EPL], float(&hx)[EPL]) -> bool {
+    floatx2 d2 = {0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p)
+      d2 = __builtin_elementwise_fma(floatx2{w[2 * p], w[2 * p + 1]}, floatx2{h[2 * p], h[2 * p + 1]}, d2);
+    float dot = d2[0] + d2[1];
+    if constexpr (EPL % 2) dot = fmaf(w[EPL - 1], h[EPL - 1], dot);
+    const float ge = -lr * (sub16_sum(dot) - v0);
+    const floatx2 g = {ge, ge}, dc = {decay, decay};
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p) {
+      const floatx2 wk = {w[2 * p], w[2 * p + 1]}, hk = {h[2 * p], h[2 * p + 1]};
+      const floatx2 wn = __builtin_elementwise_fma(g, hk, dc * wk);
+      const floatx2 hn = __builtin_elementwise_fma(g, wk, dc * hk);
+      w[2 * p] = wn[0];
+      w[2 * p + 1] = wn[1];
+      h[2 * p] = hn[0];
+      h[2 * p + 1] = hn[1];
+    }
+    if constexpr (EPL % 2) {
+      const float wk = w[EPL - 1], hk = h[EPL - 1];
+      w[EPL - 1] = fmaf(ge, hk, decay * wk);
+      h[EPL - 1] = fmaf(ge, wk, decay * hk);
+    }
+    const bool last = i + 1 >= n;
+    if (!last && row1 != cur) {
+      store_row<EPL>(W + (cur * ldw + lo), w);
+      cur = row1;
+      load_row<EPL>(W + (cur * ldw + lo), w);
+    }
+    const int i2 = i + 2 < n ? i + 2 : n - 1;  // clamped: the last prefetch is a harmless re-read
+    const unsigned row2 = (unsigned)sR[i2], col2 = (unsigned)sC[i2];
+    const float v2 = sV[i2];
+    load_row_l2<EPL>(H + (col2 * ldh + lo), hl);
+    if constexpr (NTS) store_row_nt<EPL>(H + (col0 * ldh + lo), h);
+    else store_row<EPL>(H + (col0 * ldh + lo), h);
+    if (last) return false;
+    // row of rating i+1: just updated (same item as i), updated one rating ago (same item as
+    // i-1, its store was issued after the prefetch), or the prefetched copy
+    const bool s0 = col1 == col0, s1 = col1 == colp;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const float nx = s0 ? h[k] : (s1 ? hp[k] : hx[k]);
+      hp[k] = h[k];
+      h[k] = nx;
+    }
+    colp = col0;
+    col0 = col1;
+    v0 = v1;
+    row1 = row2;
+    col1 = col2;
+    v1 = v2;
+    ++i;
+    return true;
+  };
+  while (step(hA, hB) && step(hB, hA)) {
+  }
+  store_row<EPL>(W + (cur * ldw + lo), w);
+}
+
 // Sub-step `step` of the XCD-blocked schedule. off[c] .. off[c + 1] are the ratings of cell
 // c = user_block * 8 + item_block (cell-major, user-sorted inside a cell). The blocks that
-// share an XCD (same blockIdx.x % 8) stride over the streams of their cell.
-template <int R>
+// share an XCD (same blockIdx.x % 8) take rounds of 16 consecutive streams of CH ratings:
+// the round's 16*CH index triples are one contiguous, coalesced copy into LDS, then each
+// 16-lane subgroup runs one stream.
+template <int R, int CH, bool NTS = false>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
-                                                         int step, int chunk, float* __restrict__ W, int ldw,
+                                                         int step, float* __restrict__ W, int ldw,
                                                          float* __restrict__ H, int ldh, float lr, float lam) {
+  __shared__ int sR[16 * CH], sC[16 * CH];
+  __shared__ float sV[16 * CH];
   const int x = blockIdx.x % XCDS;
   const long j = blockIdx.x / XCDS;
   const long per_xcd = gridDim.x / XCDS;
   const int cell = x * XCDS + (x + step) % XCDS;
-  const long a = off[cell], e = off[cell + 1];
-  const long nst = (e - a + chunk - 1) / chunk;
+  const long a = off[cell];
+  const long n = off[cell + 1] - a;
+  const long nst = (n + CH - 1) / CH;
   const int sl = threadIdx.x & 15;
-  const long sub = threadIdx.x >> 4;  // 16 streams per 256-thread block
-  for (long st = j * 16 + sub; st < nst; st += per_xcd * 16) {
-    const long i0 = a + st * chunk;
-    const long i1 = i0 + chunk < e ? i0 + chunk : e;
-    sgd_stream<R>(rows, cols, vals, i0, i1, sl, W, ldw, H, ldh, lr, lam);
+  const int sub = threadIdx.x >> 4;  // 16 streams per 256-thread block
+  for (long st0 = j * 16; st0 < nst; st0 += per_xcd * 16) {
+    const long r0 = st0 * CH;
+    __syncthreads();  // the previous round is done with the LDS triples
+    for (int k = threadIdx.x; k < 16 * CH; k += 256) {
+      if (r0 + k < n) {
+        sR[k] = rows[a + r0 + k];
+        sC[k] = cols[a + r0 + k];
+        sV[k] = vals[a + r0 + k];
+      }
+    }
+    __syncthreads();
+    const long mine = n - (r0 + (long)sub * CH);
+    if (mine > 0)
+      sgd_stream_lds<R, NTS>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
+                        (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
 }
 
@@ -211,12 +409,12 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
-template <int R>
-int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, int steps, int chunk,
-                   int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
+template <int R, int CH, bool NTS = false>
+int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, int steps, int blocks_per_xcd,
+                   float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
-    mf_sgd_xcd_kernel<R><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-        rows, cols, vals, off, step, chunk, W, ldw, H, ldh, lr, lam);
+    mf_sgd_xcd_kernel<R, CH, NTS><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+        rows, cols, vals, off, step, W, ldw, H, ldh, lr, lam);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -255,15 +453,24 @@ HARP_EXPORT int harp_mf_sgd(const int* rows, const int* cols, const float* vals,
 HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 
 // All `steps` (= 8) sub-steps of the XCD-blocked schedule over one resident slice: `off`
-// is a DEVICE array of 65 int64 cell offsets into rows/cols/vals.
+// is a DEVICE array of 65 int64 cell offsets into rows/cols/vals (every cell < 2^31 ratings).
+// `chunk` (ratings per stream and round) is 32, 64 or 128; `variant` 1 = non-temporal H
+// stores (chunk 64 only; measured 23 % slower, kept for the record).
 HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, int r,
-                                int steps, int chunk, int blocks_per_xcd, float* W, int ldw, float* H, int ldh,
-                                float lr, float lam, hipStream_t s) {
-  if (chunk <= 0 || blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r) return HARP_EBADARG;
-#define SGDX_CALL(RR) \
-  launch_sgd_xcd<RR>(rows, cols, vals, off, steps, chunk, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s)
+                                int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw, float* H,
+                                int ldh, float lr, float lam, hipStream_t s) {
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant < 0 || variant > 1)
+    return HARP_EBADARG;
+#define SGDX_ARGS rows, cols, vals, off, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
+#define SGDX_CALL(RR)                                                                          \
+  (variant == 1 ? (chunk == 64 ? launch_sgd_xcd<RR, 64, true>(SGDX_ARGS) : HARP_EBADARG)            \
+                : chunk == 32 ? launch_sgd_xcd<RR, 32>(SGDX_ARGS)                                   \
+                              : chunk == 64 ? launch_sgd_xcd<RR, 64>(SGDX_ARGS)                     \
+                                            : chunk == 128 ? launch_sgd_xcd<RR, 128>(SGDX_ARGS)     \
+                                                           : HARP_EBADARG)
   MF_DISPATCH(r, SGDX_CALL)
 #undef SGDX_CALL
+#undef SGDX_ARGS
 }
 
 HARP_EXPORT int harp_mf_rmse_blocks() { return 1024; }

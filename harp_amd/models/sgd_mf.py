@@ -37,7 +37,8 @@ class SGDConfig:
     num_slices: int = 2        # model slices per worker (numModelSlices)
     chunk: int = 64            # ratings per GPU update stream
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
-    blocks_per_xcd: int = 256  # workgroups per XCD of the blocked kernel
+    blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
+    kernel_variant: int = 0    # blocked kernel variant (reserved)
     random_order: bool = False  # random rotation orders (RotationUtil) vs ring
     test_every: int = 5        # rmseIteInterval
     seed: int = 0
@@ -57,12 +58,14 @@ def load_mm(path: str) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
             torch.from_numpy(arr[:, 2].astype("float32")))
 
 
-def synthetic_ratings(n_users: int, n_items: int, n_ratings: int, seed: int = 0, device="cpu", true_rank: int = 8):
-    """Netflix-shaped synthetic ratings: uniform users, Zipf-like item popularity, values
-    from a hidden rank-``true_rank`` model + noise clipped to [1, 5]."""
+def synthetic_ratings(n_users: int, n_items: int, n_ratings: int, seed: int = 0, device="cpu", true_rank: int = 8,
+                      skew: float = 2.0):
+    """Netflix-shaped synthetic ratings: uniform users, Zipf-like item popularity (item of
+    rank q drawn with density ~ q^(1/skew - 1); skew=1 is uniform), values from a hidden
+    rank-``true_rank`` model + noise clipped to [1, 5]."""
     g = torch.Generator(device=device).manual_seed(seed)
     u = torch.randint(0, n_users, (n_ratings,), generator=g, device=device)
-    pop = torch.rand(n_ratings, generator=g, device=device) ** 2.0
+    pop = torch.rand(n_ratings, generator=g, device=device) ** skew
     perm = torch.randperm(n_items, generator=g, device=device)
     it = perm[(pop * n_items).long().clamp_max(n_items - 1)]
     Ut = torch.randn((n_users, true_rank), generator=g, device=device) / math.sqrt(true_rank)
@@ -96,7 +99,11 @@ class _Buckets:
         span = int(rows.max().item()) + 1 if rows.numel() else 1
         nc = MF.XCDS * MF.XCDS
         if cells is not None:
-            cid = g * nc + MF.cell_layout(rows, lc, cells[0], cells[1])
+            # equal-work cells: contiguous user / item ranges holding ~1/8 of the slice's
+            # ratings each (skewed item popularity would otherwise leave XCDs idle)
+            rb = MF.balanced_blocks(g, rows, n_slices, cells[0])
+            cb = MF.balanced_blocks(g, lc, n_slices, cells[1])
+            cid = g * nc + rb * MF.XCDS + cb
             key = cid * span + rows
         else:
             key = g * span + rows
@@ -211,7 +218,7 @@ class SGDCollectiveMapper(CollectiveMapper):
                     if cfg.xcd_blocks:
                         r_, c_, v_, off, hoff = self.train.get_cells(gs)
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
-                                                   cfg.blocks_per_xcd, host_off=hoff)
+                                                   cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant)
                     else:
                         n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
                 with timer.phase("rotate"):

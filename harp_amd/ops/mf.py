@@ -20,7 +20,7 @@ _lib.register({
                     _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_void_p],
     "harp_mf_xcds": [],
     "harp_mf_sgd_xcd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
-                        _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float,
+                        _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float,
                         _lib.c_void_p],
     "harp_mf_rmse_blocks": [],
     "harp_mf_rmse": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int,
@@ -83,14 +83,28 @@ def cell_layout(rows: torch.Tensor, cols: torch.Tensor, n_rows: int, n_cols: int
     return rb * nb + cb
 
 
+def balanced_blocks(group: torch.Tensor, idx: torch.Tensor, n_groups: int, n_idx: int, nb: int = XCDS) -> torch.Tensor:
+    """Block (0..nb-1) of every (group, idx) record: within each group, contiguous idx
+    ranges holding ~equal numbers of records (so skewed item popularity still gives the 8
+    XCDs equal work per sub-step)."""
+    flat = group.long() * n_idx + idx.long()
+    cnt = torch.bincount(flat, minlength=n_groups * n_idx).view(n_groups, n_idx)
+    excl = torch.cumsum(cnt, 1) - cnt
+    tot = cnt.sum(1, keepdim=True).clamp_min(1)
+    blk = torch.clamp((excl * nb) // tot, max=nb - 1)
+    return blk.view(-1)[flat]
+
+
 def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, cell_off: torch.Tensor,
                        W: torch.Tensor, H: torch.Tensor, lr: float, lam: float, chunk: int = 64,
-                       blocks_per_xcd: int = 256, host_off: list | None = None) -> int:
+                       blocks_per_xcd: int = 256, host_off: list | None = None, variant: int = 0) -> int:
     """One SGD pass over ratings laid out in nb x nb cells (cell-major, user-sorted inside a
     cell; ``cell_off`` = nb*nb+1 int64 offsets on W's device). Sub-step s trains the nb
     row- and column-disjoint cells (x, (x+s) mod nb): on the GPU one XCD per cell
     (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
-    ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path)."""
+    ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path).
+    ``chunk``: ratings per stream (32, 64 or 128 on the GPU); ``variant``: 0, or 1 = non-temporal
+    H stores (slower; see csrc/mf_sgd.hip)."""
     _check(rows, cols, vals, W, H)
     n = rows.numel()
     if n == 0:
@@ -104,7 +118,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
         assert cell_off.device == W.device and cell_off.is_contiguous()
         lib = _lib.kernels()
         st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(), r, nb, chunk,
-                                 blocks_per_xcd, W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr),
+                                 blocks_per_xcd, variant, W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr),
                                  float(lam), _lib.stream_ptr(W.device))
         _lib.check(st, "mf_sgd_xcd")
         return n

@@ -26,7 +26,9 @@ def main():
     ap.add_argument("--lr", type=float, default=0.002)
     ap.add_argument("--lam", type=float, default=0.05)
     ap.add_argument("--layout", choices=("xcd", "flat"), default="xcd")
-    ap.add_argument("--blocks-per-xcd", type=int, default=256)
+    ap.add_argument("--skew", type=float, default=2.0, help="item popularity skew (1 = uniform)")
+    ap.add_argument("--blocks-per-xcd", type=int, default=128)
+    ap.add_argument("--variant", type=int, default=0)
     a = ap.parse_args()
     import torch
 
@@ -37,10 +39,11 @@ def main():
     comm = init_distributed()
     dev = comm.device
     t0 = time.perf_counter()
-    u, i, v = synthetic_ratings(a.users, a.items, a.ratings, seed=7, device=dev)
+    u, i, v = synthetic_ratings(a.users, a.items, a.ratings, seed=7, device=dev, skew=a.skew)
     gen_s = time.perf_counter() - t0
     cfg = SGDConfig(rank=a.rank, lam=a.lam, lr=a.lr, epochs=a.warmup + a.epochs, chunk=a.chunk, test_every=0,
-                    xcd_blocks=a.layout == "xcd", blocks_per_xcd=a.blocks_per_xcd)
+                    xcd_blocks=a.layout == "xcd", blocks_per_xcd=a.blocks_per_xcd,
+                    kernel_variant=a.variant)
     m = SGDCollectiveMapper(comm, cfg, a.users, a.items, (u, i, v), None)
     m.init_model(KeyValReader([]))
     del u, i, v
@@ -74,7 +77,7 @@ def main():
                           "value": n / dt, "unit": "updates/s", "n_gpus": comm.world_size, "epochs": a.epochs,
                           "s_per_epoch": dt / a.epochs, "train_rmse": tr, "data_gen_s": gen_s,
                           "ratings": a.ratings, "rank": a.rank, "dtype": "fp32 factors",
-                          "layout": a.layout, "chunk": a.chunk, "blocks_per_xcd": a.blocks_per_xcd}), flush=True)
+                          "layout": a.layout, "skew": a.skew, "chunk": a.chunk, "blocks_per_xcd": a.blocks_per_xcd, "variant": a.variant}), flush=True)
     shutdown()
 
 

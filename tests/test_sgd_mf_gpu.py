@@ -71,12 +71,14 @@ def _cells(nu, ni, n, r, seed):
 @pytest.mark.parametrize("r", [16, 128])
 def test_sgd_xcd_one_stream_per_cell_matches_cpu(cuda, r):
     """chunk >= cell size: one stream per cell, and the 8 cells of a sub-step share no user
-    and no item, so the XCD-blocked kernel is deterministic and equals the CPU schedule."""
+    and no item, so the XCD-blocked kernel is deterministic and equals the CPU schedule
+    (including the in-register forwarding of repeated items: 64 users x 48 items)."""
     R, C, V, off, W0, H0 = _cells(64, 48, 4000, r, 1)
+    assert int((off[1:] - off[:-1]).max()) <= 128
     Wc, Hc = W0.clone(), H0.clone()
     MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.01, 0.05)
     Wg, Hg = W0.to(cuda), H0.to(cuda)
-    MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=1 << 20,
+    MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=128,
                           blocks_per_xcd=4)
     torch.cuda.synchronize()
     assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
