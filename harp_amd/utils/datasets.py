@@ -3,17 +3,84 @@
 Reference: core/harp-daal-interface/.../datasource/HarpDAALDataSource.java:76-775
 (multithreaded dense CSV -> HomogenNumericTable, CSR files -> CSRNumericTable, COO
 lists, regroupCOOList) and data_gen/DataGenerator.java:56-249 (synthetic dense / label
-CSV generators). Text parsing is host work: files are parsed with numpy (no pickle),
-split across a thread pool per file, and returned as tensors ready to move to the GPU.
+CSV generators).
+
+Text parsing is host work done natively: ``csrc/host/loaders.cpp`` (in
+``libharp_runtime.so``) mmaps each file, splits it into line-aligned byte ranges and
+parses every range on its own thread straight into the numpy buffer (the reference's
+MTReader runs one Java thread per *file*). The pure-Python parsers below are the fallback
+when the runtime library is not built (or ``HARP_NATIVE_LOADERS=0``) and the oracle of the
+loader tests.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
+
+
+_I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+def _native():
+    """The host runtime with the loader symbols bound, or None (then Python parsing)."""
+    if os.environ.get("HARP_NATIVE_LOADERS", "1") == "0":
+        return None
+    from ..ops import _lib
+
+    rt = _lib.runtime()
+    if rt is None or not hasattr(rt, "harp_text_open"):
+        return None
+    if not getattr(rt, "_loaders_bound", False):
+        vp, c = ctypes.c_void_p, ctypes.c_char
+        rt.harp_text_open.argtypes, rt.harp_text_open.restype = [ctypes.c_char_p, ctypes.c_int], vp
+        rt.harp_text_close.argtypes, rt.harp_text_close.restype = [vp], None
+        rt.harp_dense_shape.argtypes = [vp, c, _I64P, _I64P]
+        rt.harp_dense_fill.argtypes = [vp, c, vp, ctypes.c_int64]
+        rt.harp_coo_count.argtypes = [vp, _I64P]
+        rt.harp_coo_fill.argtypes = [vp, c, vp, vp, vp]
+        rt.harp_libsvm_count.argtypes = [vp, _I64P, _I64P, _I64P]
+        rt.harp_libsvm_fill.argtypes = [vp, vp, vp, vp, vp]
+        for f in ("harp_dense_shape", "harp_dense_fill", "harp_coo_count", "harp_coo_fill", "harp_libsvm_count",
+                  "harp_libsvm_fill"):
+            getattr(rt, f).restype = ctypes.c_int
+        rt._loaders_bound = True
+    return rt
+
+
+class _Text:
+    """mmap'ed, range-split text file of the native loader."""
+
+    def __init__(self, rt, path: str, threads: int):
+        self.rt = rt
+        self.h = rt.harp_text_open(os.fsencode(path), int(threads))
+        if not self.h:
+            raise OSError(f"cannot open {path}")
+
+    def __enter__(self):
+        return self.h
+
+    def __exit__(self, *exc):
+        self.rt.harp_text_close(self.h)
+
+
+def _check(st: int, path: str) -> None:
+    if st != 0:
+        raise ValueError(f"{path}: malformed numeric field")
+
+
+def _native_dense(rt, path: str, threads: int, sep: str = ",") -> np.ndarray:
+    with _Text(rt, path, threads) as h:
+        r, c = ctypes.c_int64(0), ctypes.c_int64(0)
+        rt.harp_dense_shape(h, sep.encode(), ctypes.byref(r), ctypes.byref(c))
+        out = np.zeros((r.value, c.value), dtype=np.float64)
+        if out.size:
+            _check(rt.harp_dense_fill(h, sep.encode(), out.ctypes.data, c.value), path)
+    return out
 
 
 def _parse_dense(path: str) -> np.ndarray:
@@ -39,8 +106,12 @@ def list_files(path: str) -> List[str]:
 def load_dense_csv(path: str, threads: int = 8) -> torch.Tensor:
     """All files of ``path`` (a file or a directory), rows concatenated in file order."""
     files = list_files(path)
-    with ThreadPoolExecutor(max_workers=max(1, min(threads, len(files)))) as ex:
-        parts = list(ex.map(_parse_dense, files))
+    rt = _native()
+    if rt is not None:
+        parts = [_native_dense(rt, f, threads) for f in files]
+    else:
+        with ThreadPoolExecutor(max_workers=max(1, min(threads, len(files)))) as ex:
+            parts = list(ex.map(_parse_dense, files))
     parts = [p for p in parts if p.size]
     return torch.from_numpy(np.concatenate(parts)) if parts else torch.zeros((0, 0), dtype=torch.float64)
 
@@ -63,8 +134,26 @@ def load_daal_csr(path: str, n_cols: Optional[int] = None) -> torch.Tensor:
                                    size=(len(ro) - 1, nc))
 
 
-def load_coo(path: str, one_based: bool = True, sep: Optional[str] = None):
+def load_coo(path: str, one_based: bool = True, sep: Optional[str] = None, threads: int = 8):
     """``row col value`` lines (Matrix Market body / Harp MF input) -> (rows, cols, vals)."""
+    off = 1 if one_based else 0
+    rt = _native()
+    if rt is not None and (sep is None or len(sep) == 1):
+        rs, cs, vs = [], [], []
+        for fn in list_files(path):
+            with _Text(rt, fn, threads) as h:
+                n = ctypes.c_int64(0)
+                rt.harp_coo_count(h, ctypes.byref(n))
+                R = np.empty(n.value, dtype=np.int64)
+                C = np.empty(n.value, dtype=np.int64)
+                V = np.empty(n.value, dtype=np.float64)
+                if n.value:
+                    _check(rt.harp_coo_fill(h, (sep or ",").encode(), R.ctypes.data, C.ctypes.data, V.ctypes.data), fn)
+            rs.append(R)
+            cs.append(C)
+            vs.append(V)
+        cat = (lambda xs, dt: torch.from_numpy(np.concatenate(xs)) if xs else torch.zeros(0, dtype=dt))
+        return cat(rs, torch.long) - off, cat(cs, torch.long) - off, cat(vs, torch.float64)
     r, c, v = [], [], []
     for fn in list_files(path):
         with open(fn) as f:
@@ -75,13 +164,34 @@ def load_coo(path: str, one_based: bool = True, sep: Optional[str] = None):
                 r.append(int(t[0]))
                 c.append(int(t[1]))
                 v.append(float(t[2]))
-    off = 1 if one_based else 0
     return (torch.tensor(r, dtype=torch.long) - off, torch.tensor(c, dtype=torch.long) - off,
             torch.tensor(v, dtype=torch.float64))
 
 
-def load_libsvm(path: str, n_features: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+def load_libsvm(path: str, n_features: Optional[int] = None, threads: int = 8) -> Tuple[torch.Tensor, torch.Tensor]:
     """libsvm ``label idx:val ...`` rows -> (dense X, y)."""
+    rt = _native()
+    if rt is not None:
+        parts = []
+        for fn in list_files(path):
+            with _Text(rt, fn, threads) as h:
+                r, z, m = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+                _check(rt.harp_libsvm_count(h, ctypes.byref(r), ctypes.byref(z), ctypes.byref(m)), fn)
+                y = np.empty(r.value, dtype=np.float64)
+                ip = np.zeros(r.value + 1, dtype=np.int64)
+                ix = np.empty(z.value, dtype=np.int64)
+                va = np.empty(z.value, dtype=np.float64)
+                _check(rt.harp_libsvm_fill(h, y.ctypes.data, ip.ctypes.data, ix.ctypes.data, va.ctypes.data), fn)
+            parts.append((y, ip, ix, va, m.value))
+        d = n_features or max((p[4] for p in parts), default=0)
+        Xs = []
+        for y, ip, ix, va, _ in parts:
+            X = torch.zeros((y.size, d), dtype=torch.float64)
+            rows = torch.repeat_interleave(torch.arange(y.size), torch.from_numpy(np.diff(ip)))
+            X[rows, torch.from_numpy(ix)] = torch.from_numpy(va)
+            Xs.append(X)
+        return (torch.cat(Xs) if Xs else torch.zeros((0, d), dtype=torch.float64),
+                torch.from_numpy(np.concatenate([p[0] for p in parts])) if parts else torch.zeros(0))
     ys, rows = [], []
     for fn in list_files(path):
         with open(fn) as f:
