@@ -77,12 +77,14 @@ def kernels():
 
 
 def runtime():
-    """Host C++ runtime library (checkpoint I/O, codec, block scheduler) or None."""
+    """Host C++ runtime library (text loaders, exact CPU samplers / SGD oracles) or None.
+    ``HARP_RUNTIME_LIB`` selects another build of it (e.g. the sanitizer build)."""
     global _rt
-    if _rt is None and os.path.exists(RUNTIME_LIB):
+    path = os.environ.get("HARP_RUNTIME_LIB", RUNTIME_LIB)
+    if _rt is None and os.path.exists(path):
         with _lock:
             if _rt is None:
-                _rt = ctypes.CDLL(RUNTIME_LIB)
+                _rt = ctypes.CDLL(path)
     return _rt
 
 

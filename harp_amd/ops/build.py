@@ -4,8 +4,11 @@
   by hipcc for gfx950 only (``--offload-arch=gfx950``), exporting ``extern "C"``
   launchers that take raw device pointers + a ``hipStream_t``.
 * ``harp_amd/_native/libharp_runtime.so`` — host-side C++ runtime pieces
-  (``csrc/host/*.cpp``: partition-table checkpoint I/O, big-endian codec, 2-D block
-  scheduler), built with g++.
+  (``csrc/host/*.cpp``: multithreaded text loaders, exact sequential CPU samplers / SGD
+  used on CPU workers and as GPU-kernel oracles), built with g++.
+* ``build/sanitize/libharp_runtime_{asan,tsan}.so`` (``--sanitize asan|tsan``, not shipped)
+  — the same host sources under AddressSanitizer + UBSan or ThreadSanitizer, for
+  ``tests/test_sanitizers.py`` (host code only: GPU sanitizers are not used).
 
 Both are loaded with ctypes *after* ``import torch`` so the kernels launch through the
 HIP runtime torch already loaded (same soname ``libamdhip64.so.7``).
@@ -89,10 +92,34 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     return RUNTIME_LIB
 
 
+SANITIZE_DIR = os.path.join(ROOT, "build", "sanitize")
+_SAN_FLAGS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def build_runtime_sanitized(kind: str = "asan", force: bool = False) -> str:
+    """Host runtime under a sanitizer (loaded with the sanitizer runtime LD_PRELOADed)."""
+    os.makedirs(SANITIZE_DIR, exist_ok=True)
+    out = os.path.join(SANITIZE_DIR, f"libharp_runtime_{kind}.so")
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    headers = glob.glob(os.path.join(CSRC, "host", "*.h"))
+    if force or _stale(out, srcs + headers):
+        flags = [f for f in CXX_FLAGS if f != "-O3"] + ["-O1", "-g"] + _SAN_FLAGS[kind]
+        tmp = f"{out}.{os.getpid()}.tmp"
+        _run([CXX] + flags + ["-shared", "-o", tmp] + srcs)
+        os.replace(tmp, out)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = True) -> None:
     build_kernels(force=force, verbose=verbose)
     build_runtime(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if "--sanitize" in sys.argv:
+        print(build_runtime_sanitized(sys.argv[sys.argv.index("--sanitize") + 1], force="--force" in sys.argv))
+    else:
+        build_all(force="--force" in sys.argv)
