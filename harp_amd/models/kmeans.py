@@ -25,7 +25,9 @@ log (KMeansCollectiveMapper.java:191-193).
 """
 from __future__ import annotations
 
+import json
 import math
+import os
 import time
 from dataclasses import asdict, dataclass, field
 from typing import List, Optional
@@ -53,6 +55,8 @@ class KMeansConfig:
     data_hi: float = 1000.0
     variant: int = K.DEFAULT_VARIANT   # HIP kernel tiling variant
     objective_every: int = 1           # compute the objective every k iterations (0: never)
+    checkpoint_dir: str = ""           # .hpt checkpoints of the centroid table (resume on restart)
+    checkpoint_every: int = 0          # iterations between checkpoints (0: never)
 
 
 class BlockPartitioner(Partitioner):
@@ -109,10 +113,52 @@ class KMeansCollectiveMapper(CollectiveMapper):
 
     # -- main ------------------------------------------------------------------------------
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
+        cfg = self.cfg
         self.init_model(reader)
-        for it in range(self.cfg.iterations):
+        start = self.resume() if cfg.checkpoint_dir else 0
+        for it in range(start, cfg.iterations):
             self.step(it)
+            self.inject_fault(it)
+            if cfg.checkpoint_dir and cfg.checkpoint_every and (it + 1) % cfg.checkpoint_every == 0:
+                self.checkpoint(it)
         self.finish()
+
+    # -- checkpoint / resume ------------------------------------------
+    def checkpoint(self, it: int) -> str:
+        """Write the centroid table after iteration ``it`` as per-rank ``.hpt`` files in
+        ``<dir>/it-<it>/`` (+ manifest with the objective history); once every rank has
+        written, rank 0 atomically points ``<dir>/LATEST`` at it."""
+        from ..utils.checkpoint import save_checkpoint
+
+        if self.cfg.strategy == "rotation":
+            raise NotImplementedError("checkpoint of the model-parallel rotation strategy")
+        sub = os.path.join(self.cfg.checkpoint_dir, f"it-{it:06d}")
+        t = PackedTable(self.ids, self.c, table_id=0, combiner=self.sumop)
+        save_checkpoint(sub, {"centroids": t}, self.get_self_id(), self.get_num_workers(), it,
+                        extra={"objective": list(self.objective)}, comm=self.comm)
+        if self.is_master():
+            tmp = os.path.join(self.cfg.checkpoint_dir, "LATEST.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"dir": os.path.basename(sub), "iteration": it}, f)
+            os.replace(tmp, os.path.join(self.cfg.checkpoint_dir, "LATEST"))
+        return sub
+
+    def resume(self) -> int:
+        """Load the latest checkpoint if one exists; returns the first iteration to run."""
+        from ..utils.checkpoint import load_checkpoint
+
+        latest = os.path.join(self.cfg.checkpoint_dir, "LATEST")
+        if not os.path.exists(latest):
+            return 0
+        with open(latest) as f:
+            sub = os.path.join(self.cfg.checkpoint_dir, json.load(f)["dir"])
+        man, tabs = load_checkpoint(sub, self.get_self_id(), self.get_num_workers(), device=self.device)
+        c = tabs["centroids"]
+        buf = c.buffer if isinstance(c, PackedTable) else torch.stack([p.get() for p in c.get_partitions()])
+        self.c = buf.to(self.device, torch.float32).contiguous()
+        self.op = K.prepare(self.c[: self.cfg.num_centroids].contiguous(), self.dp, self.op)
+        self.objective = list(man["extra"].get("objective", []))
+        return int(man["iteration"]) + 1
 
     def init_model(self, reader: KeyValReader) -> None:
         """Load/generate points, create + broadcast the initial centroids."""

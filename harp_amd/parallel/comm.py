@@ -28,6 +28,14 @@ import torch.distributed as dist
 DATA_MAX_WAIT_TIME_S = float(os.environ.get("HARP_DATA_MAX_WAIT_TIME", "1800"))
 
 
+def collective_timeout_s() -> float:
+    """Collective watchdog: a collective that has not completed after this many seconds
+    fails on every live rank (torch.distributed process-group timeout), the collective
+    returns False and the job can restart from its last checkpoint. Read at call time from
+    ``HARP_DATA_MAX_WAIT_TIME`` (default 1800 s, the reference's DATA_MAX_WAIT_TIME)."""
+    return float(os.environ.get("HARP_DATA_MAX_WAIT_TIME", str(DATA_MAX_WAIT_TIME_S)))
+
+
 class Workers:
     """Topology view (worker/Workers.java)."""
 
@@ -156,7 +164,7 @@ class Communicator:
                 if self.world_size > 1:
                     ranks = [self.global_rank(r) for r in range(self.world_size)]
                     g = dist.new_group(ranks=ranks, backend=self.backend,
-                                       timeout=datetime.timedelta(seconds=DATA_MAX_WAIT_TIME_S))
+                                       timeout=datetime.timedelta(seconds=collective_timeout_s()))
                 else:
                     g = None
                 ch = Communicator(g, self.device, name=f"{self.name}/{key}")

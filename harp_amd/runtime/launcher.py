@@ -30,7 +30,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from ..parallel.comm import DATA_MAX_WAIT_TIME_S, Communicator
+from ..parallel.comm import Communicator, collective_timeout_s
 from .inputformat import multi_file_splits
 from .mapper import CollectiveMapper, Context, KeyValReader
 
@@ -41,9 +41,12 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = DATA_MAX_WAIT_TIME_S) -> Communicator:
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> Communicator:
     """Initialise torch.distributed from the environment (torchrun contract) and pin
-    this process to GPU ``LOCAL_RANK``. Returns the world communicator."""
+    this process to GPU ``LOCAL_RANK``. Returns the world communicator. ``timeout_s``
+    (default :func:`collective_timeout_s`) is the collective watchdog."""
+    if timeout_s is None:
+        timeout_s = collective_timeout_s()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -84,7 +87,8 @@ def _to_cpu(obj):
 
 
 def _worker(rank: int, world: int, port: int, backend: str, target: Callable, args: tuple,
-            result_q) -> None:
+            result_q, env: Optional[Dict[str, str]] = None) -> None:
+    os.environ.update(env or {})
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     try:
@@ -102,18 +106,45 @@ def _worker(rank: int, world: int, port: int, backend: str, target: Callable, ar
 
 
 def launch(target: Callable, num_workers: int, args: tuple = (), backend: str = "gloo",
-           timeout: float = 600.0) -> List[Any]:
+           timeout: float = 600.0, retries: int = 0, env: Optional[Dict[str, str]] = None,
+           grace_s: float = 10.0) -> List[Any]:
     """Run ``target(comm, *args)`` on ``num_workers`` local ranks; return results by rank.
 
-    ``target`` must be importable (module-level) so it can be pickled to the workers."""
+    ``target`` must be importable (module-level) so it can be pickled to the workers.
+    Failure handling: when a rank fails or dies, the others get ``grace_s``
+    seconds to report (a dead peer makes their next collective fail, or the collective
+    watchdog fires), then the gang is terminated; with ``retries`` the whole job is started
+    again (``HARP_ATTEMPT`` = 1, 2, ... in the workers' environment) — the reference's
+    whole-job resubmission (contrib KmeansMapCollective jobRetryCount); applications resume
+    from their last checkpoint."""
+    for attempt in range(retries + 1):
+        e = dict(env or {}, HARP_ATTEMPT=str(attempt))
+        try:
+            return _launch_once(target, num_workers, args, backend, timeout, e, grace_s)
+        except Exception:
+            if attempt == retries:
+                raise
+    raise AssertionError("unreachable")
+
+
+def _launch_once(target, num_workers, args, backend, timeout, env, grace_s) -> List[Any]:
     import torch.multiprocessing as mp
 
     if num_workers == 1:
-        return [target(Communicator(None, torch.device("cpu") if backend == "gloo" else None), *args)]
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            return [target(Communicator(None, torch.device("cpu") if backend == "gloo" else None), *args)]
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, num_workers, port, backend, target, args, q), daemon=False)
+    procs = [ctx.Process(target=_worker, args=(r, num_workers, port, backend, target, args, q, env), daemon=False)
              for r in range(num_workers)]
     for p in procs:
         p.start()
@@ -128,19 +159,25 @@ def launch(target: Callable, num_workers: int, args: tuple = (), backend: str = 
         if not q.empty():
             rank, status, val = q.get()
             (results.__setitem__(rank, pickle.loads(val)) if status == "ok" else errors.append((rank, val)))
+            if errors:  # a failed gang: the rest get a grace period, then are stopped
+                deadline = min(deadline, _t.monotonic() + grace_s)
         elif all(not p.is_alive() for p in procs) and q.empty():
             break
+        elif any(p.exitcode not in (None, 0) for p in procs):  # died without reporting
+            deadline = min(deadline, _t.monotonic() + grace_s)
+            _t.sleep(0.01)
         else:
             _t.sleep(0.01)
     for p in procs:
-        p.join(timeout=max(1.0, deadline - _t.monotonic()))
+        p.join(timeout=max(0.5, deadline - _t.monotonic()))
         if p.is_alive():
             p.terminate()
             p.join(5)
     if errors:
         raise RuntimeError(f"worker(s) failed: {errors}")
     if len(results) != num_workers:
-        raise RuntimeError(f"only {len(results)}/{num_workers} workers reported (timeout or crash)")
+        codes = [p.exitcode for p in procs]
+        raise RuntimeError(f"only {len(results)}/{num_workers} workers reported (timeout or crash; exit codes {codes})")
     return [results[r] for r in range(num_workers)]
 
 

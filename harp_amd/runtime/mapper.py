@@ -15,6 +15,7 @@ RCCL's per-communicator issue order does the matching the reference's mailboxes 
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Any, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
@@ -188,6 +189,29 @@ class CollectiveMapper:
 
     def send_message(self, ctx: str, target: int, body: Any) -> bool:
         return self.send_event(Event(EventType.MESSAGE, ctx, self.get_self_id(), target, body))
+
+    # -- fault injection (tests) --------------------------------------------------
+    def inject_fault(self, iteration: int) -> None:
+        """``HARP_FAULT="rank=R,iter=I,kind=exit|hang|raise[,attempt=A][,seconds=S]"`` makes
+        rank R fail after iteration I of job attempt A (default 0, see ``launch(retries)``):
+        ``exit`` kills the process (a dead peer), ``hang`` stops it for S seconds (a stuck
+        peer: the others' collective watchdog fires), ``raise`` fails the mapper."""
+        spec = os.environ.get("HARP_FAULT")
+        if not spec:
+            return
+        kv = dict(x.split("=", 1) for x in spec.split(",") if "=" in x)
+        if int(kv.get("rank", -1)) != self.get_self_id() or int(kv.get("iter", -1)) != iteration:
+            return
+        if int(kv.get("attempt", 0)) != int(os.environ.get("HARP_ATTEMPT", "0")):
+            return
+        kind = kv.get("kind", "exit")
+        log.error("injected fault %s on rank %d at iteration %d", kind, self.get_self_id(), iteration)
+        if kind == "exit":
+            os._exit(17)
+        if kind == "hang":
+            time.sleep(float(kv.get("seconds", 3600)))
+            return
+        raise RuntimeError(f"injected fault at iteration {iteration}")
 
     # -- memory / logging ------------------------------------------------------------------
     def free_memory(self) -> None:
