@@ -36,6 +36,7 @@ def main() -> int:
     ap.add_argument("--strategy", default="allreduce")
     ap.add_argument("--variant", type=int, default=None)
     ap.add_argument("--backend", default=None, help="override (e.g. gloo to rehearse >1 rank on one GPU)")
+    ap.add_argument("--graph", action="store_true", help="replay each iteration's kernels from HIP graphs")
     args = ap.parse_args()
 
     import torch
@@ -63,7 +64,7 @@ def main() -> int:
     n_local = N // P + (1 if rank < N % P else 0)
     cfg = KMeansConfig(num_points=n_local, num_centroids=args.centroids, dim=args.dim, iterations=10**9,
                        strategy=args.strategy, objective_every=0,
-                       variant=K.DEFAULT_VARIANT if args.variant is None else args.variant)
+                       variant=K.DEFAULT_VARIANT if args.variant is None else args.variant, graph=args.graph)
     m = KMeansCollectiveMapper(comm, cfg)
     m.init_model(KeyValReader([]))
     for it in range(args.warmup):
@@ -118,6 +119,7 @@ def main() -> int:
             "phase_ms_per_iter": {k: round(v / args.steps * 1e3, 3) for k, v in phases.items()},
             "mean_sq_dist": float(o.item()) / N,
             "kernel_variant": cfg.variant,
+            "hip_graph": bool(args.graph),
         }
         print(json.dumps(rec), flush=True)
     shutdown()

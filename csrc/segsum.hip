@@ -179,10 +179,17 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restri
 
 }  // namespace
 
-HARP_EXPORT long harp_bucket_chunk() { return 65536; }
+// Labels per histogram chunk: 65536 for large n; smaller for small n so the histogram and
+// scatter passes still launch >= ~1500 workgroups (6 rounds over 256 CUs); >= 4096 keeps
+// the per-chunk K-cursor load (K ints) amortised.
+HARP_EXPORT long harp_bucket_chunk(long n) {
+  long c = 65536;
+  while (c > 4096 && (n + c - 1) / c < 1536) c >>= 1;
+  return c;
+}
 
 HARP_EXPORT long harp_bucket_workspace_ints(long n, int K) {
-  const long chunk = 65536;
+  const long chunk = harp_bucket_chunk(n);
   const long nch = (n + chunk - 1) / chunk;
   const long nseg = (nch + SEG - 1) / SEG;
   // H[nch][K] + T[nseg][K] + counts[K] + start[K+1] + perm[n]
@@ -194,7 +201,7 @@ HARP_EXPORT long harp_bucket_workspace_ints(long n, int K) {
 HARP_EXPORT int harp_bucket_labels(const int* lab, long n, int K, int* ws, long* start_off, long* perm_off,
                                    hipStream_t s) {
   if (n <= 0 || K <= 0 || K > 16384) return HARP_EBADARG;
-  const long chunk = 65536;
+  const long chunk = harp_bucket_chunk(n);
   const int nch = (int)((n + chunk - 1) / chunk);
   const int nseg = (nch + SEG - 1) / SEG;
   int* H = ws;

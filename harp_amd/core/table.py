@@ -152,8 +152,39 @@ class PackedTable(Table):
         buf = torch.stack([p if isinstance(p, torch.Tensor) else p.tensor for p in parts])
         return cls(ids, buf, table.table_id, table.combiner)
 
+    # Partition views are created lazily: the dense collectives move ``buffer`` as one
+    # RCCL call and never touch per-partition objects (building 10^4 tensor views per call
+    # cost ~15 ms of host time per K-means iteration at K = 1e4).
+    @property
+    def _parts(self) -> Dict[int, Partition]:
+        if self._parts_cache is None:
+            self._parts_cache = {pid: Partition(pid, self.buffer[i]) for i, pid in enumerate(self._ids)}
+        return self._parts_cache
+
+    @_parts.setter
+    def _parts(self, value) -> None:
+        self._parts_cache = value
+
     def _rebuild_parts(self) -> None:
-        self._parts = {pid: Partition(pid, self.buffer[i]) for i, pid in enumerate(self._ids)}
+        self._parts_cache = None
+
+    def __len__(self) -> int:
+        return len(self._ids)
+
+    def get_num_partitions(self) -> int:
+        return len(self._ids)
+
+    def get_partition_ids(self) -> List[int]:
+        return list(self._ids)
+
+    def __contains__(self, pid) -> bool:
+        return int(pid) in self._row
+
+    def is_empty(self) -> bool:
+        return not self._ids
+
+    def sorted_ids(self) -> List[int]:
+        return sorted(self._ids)
 
     @property
     def ids(self) -> List[int]:

@@ -57,6 +57,7 @@ class KMeansConfig:
     objective_every: int = 1           # compute the objective every k iterations (0: never)
     checkpoint_dir: str = ""           # .hpt checkpoints of the centroid table (resume on restart)
     checkpoint_every: int = 0          # iterations between checkpoints (0: never)
+    graph: bool = False                # replay the iteration's local kernels from HIP graphs
 
 
 class BlockPartitioner(Partitioner):
@@ -195,9 +196,11 @@ class KMeansCollectiveMapper(CollectiveMapper):
         cfg = self.cfg
         if cfg.strategy == "rotation":
             return self._rotation_step(it)
+        want_obj = cfg.objective_every > 0 and (it % cfg.objective_every == 0 or it == cfg.iterations - 1)
+        if cfg.graph and not want_obj and cfg.strategy == "allreduce" and self.device.type == "cuda":
+            return self._graph_step(it)
         timer = self.metrics.timer
         t_it = time.perf_counter()
-        want_obj = cfg.objective_every > 0 and (it % cfg.objective_every == 0 or it == cfg.iterations - 1)
         with timer.phase("compute"):
             self.sums.zero_()
             _, obj = K.assign(self.X, self.op, sums=self.sums, labels=self.lab, want_objective=want_obj,
@@ -213,6 +216,63 @@ class KMeansCollectiveMapper(CollectiveMapper):
             self.objective.append(float(ot.item()))
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
 
+    def _sum_table(self, sums: torch.Tensor) -> PackedTable:
+        """The partial-sum table of the allreduce strategy, built once over the persistent
+        ``sums`` buffer: its layout is verified across ranks on the first call only
+        (``static_layout``), later calls are a single RCCL all-reduce."""
+        t = getattr(self, "_sums_pt", None)
+        if t is None or t.buffer is not sums:
+            t = PackedTable(self.ids, sums, combiner=self.sumop)
+            t.static_layout = True
+            self._sums_pt = t
+        return t
+
+    # -- HIP-graph iteration ------------------------------------------------------------
+    def _graph_step(self, it: int) -> None:
+        """The allreduce iteration with its device work replayed from two HIP graphs:
+        [zero sums, fused assign, label bucketing, row gather-sum] and [normalize, operand
+        prepare]; only the RCCL all-reduce between them is issued eagerly. Every launch in
+        the graphs writes fixed buffers (sums, labels, centroids, the kernel operand), so the
+        captured pointers stay valid; the one workspace (bucketing) is allocated by a warm-up
+        run before capture."""
+        if getattr(self, "_graphs", None) is None:
+            self._capture_graphs()
+        timer = self.metrics.timer
+        t_it = time.perf_counter()
+        with timer.phase("compute"):
+            self._graphs[0].replay()
+        with timer.phase("sync"):
+            if not self.allreduce("main", f"allreduce-{it}", self._sum_table(self.sums)):
+                raise IOError("allreduce failed")
+        with timer.phase("prepare"):
+            self._graphs[1].replay()
+        self.history.append({"iter": it, "s": time.perf_counter() - t_it})
+
+    def _capture_graphs(self) -> None:
+        cfg = self.cfg
+        d, k = cfg.dim, cfg.num_centroids
+
+        def local():
+            self.sums.zero_()
+            K.assign(self.X, self.op, sums=self.sums, labels=self.lab, want_objective=False, variant=cfg.variant)
+
+        def post():
+            K.normalize(self.sums, self.c, d)
+            K.prepare(self.c[:k], self.dp, self.op)
+
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            local()  # warm-up: allocates the bucketing workspace outside the graph
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graphs = []
+        for fn in (local, post):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            graphs.append(g)
+        self._graphs = graphs
+
     def finish(self) -> None:
         k = self.cfg.num_centroids
         if self.cfg.strategy == "rotation" and hasattr(self, "c_rot"):
@@ -226,8 +286,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
         s = self.cfg.strategy
         Kp = sums.shape[0]
         if s == "allreduce":
-            t = PackedTable(ids, sums, combiner=sumop)
-            t.static_layout = True
+            t = self._sum_table(sums)
             if not self.allreduce("main", f"allreduce-{it}", t):
                 raise IOError("allreduce failed")
             return K.normalize(t.buffer, c, d)

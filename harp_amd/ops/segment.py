@@ -14,7 +14,7 @@ import torch
 from . import _lib
 
 _lib.register({
-    "harp_bucket_chunk": [],
+    "harp_bucket_chunk": [_lib.c_long],
     "harp_bucket_workspace_ints": [_lib.c_long, _lib.c_int],
     "harp_bucket_labels": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                            _lib.c_void_p],

@@ -116,3 +116,22 @@ def test_bucket_labels_and_rowsum(cuda):
     segment.bucket_rowsum(X, perm, start, out)
     ref = torch.zeros(K, dp, dtype=torch.float64, device=cuda).index_add_(0, lab.long(), X.double())
     assert torch.allclose(out.double(), ref, rtol=1e-5, atol=1e-2)
+
+
+def test_kmeans_hip_graph_iterations_match_eager(cuda):
+    """Iterations replayed from HIP graphs give the same centroids as eager launches."""
+    from harp_amd.models.kmeans import KMeansCollectiveMapper, KMeansConfig
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    out = {}
+    for graph in (False, True):
+        cfg = KMeansConfig(num_points=50000, num_centroids=300, dim=100, iterations=6, strategy="allreduce",
+                           objective_every=0, graph=graph)
+        m = KMeansCollectiveMapper(Communicator(None, cuda), cfg)
+        m.init_model(KeyValReader([]))
+        for it in range(cfg.iterations):
+            m.step(it)
+        torch.cuda.synchronize()
+        out[graph] = m.c[:300].clone()
+    assert torch.allclose(out[True], out[False], rtol=1e-5, atol=1e-3), (out[True] - out[False]).abs().max()
