@@ -336,12 +336,15 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
 // c = user_block * 8 + item_block (cell-major, user-sorted inside a cell). The blocks that
 // share an XCD (same blockIdx.x % 8) take rounds of 16 consecutive streams of CH ratings:
 // the round's 16*CH index triples are one contiguous, coalesced copy into LDS, then each
-// 16-lane subgroup runs one stream.
+// 16-lane subgroup runs one stream. `win` (optional, 2 x 64 int64): cell c trains only the
+// window of win[64 + c] ratings starting at win[c], wrapping around the cell — the
+// fixed-fraction mode standing in for the reference's timer-bounded rotation steps.
 template <int R, int CH, bool NTS = false>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
-                                                         int step, float* __restrict__ W, int ldw,
-                                                         float* __restrict__ H, int ldh, float lr, float lam) {
+                                                         const long* __restrict__ win, int step,
+                                                         float* __restrict__ W, int ldw, float* __restrict__ H, int ldh,
+                                                         float lr, float lam) {
   __shared__ int sR[16 * CH], sC[16 * CH];
   __shared__ float sV[16 * CH];
   const int x = blockIdx.x % XCDS;
@@ -349,7 +352,9 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
   const long per_xcd = gridDim.x / XCDS;
   const int cell = x * XCDS + (x + step) % XCDS;
   const long a = off[cell];
-  const long n = off[cell + 1] - a;
+  const long ncell = off[cell + 1] - a;
+  const long w0 = win ? win[cell] : 0;
+  const long n = win ? win[XCDS * XCDS + cell] : ncell;
   const long nst = (n + CH - 1) / CH;
   const int sl = threadIdx.x & 15;
   const int sub = threadIdx.x >> 4;  // 16 streams per 256-thread block
@@ -358,16 +363,18 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
     __syncthreads();  // the previous round is done with the LDS triples
     for (int k = threadIdx.x; k < 16 * CH; k += 256) {
       if (r0 + k < n) {
-        sR[k] = rows[a + r0 + k];
-        sC[k] = cols[a + r0 + k];
-        sV[k] = vals[a + r0 + k];
+        long q = w0 + r0 + k;
+        if (q >= ncell) q -= ncell;
+        sR[k] = rows[a + q];
+        sC[k] = cols[a + q];
+        sV[k] = vals[a + q];
       }
     }
     __syncthreads();
     const long mine = n - (r0 + (long)sub * CH);
     if (mine > 0)
       sgd_stream_lds<R, NTS>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
-                        (unsigned)ldw, H, (unsigned)ldh, lr, lam);
+                             (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
 }
 
@@ -410,11 +417,11 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
 }
 
 template <int R, int CH, bool NTS = false>
-int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, int steps, int blocks_per_xcd,
-                   float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
+int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win, int steps,
+                   int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
     mf_sgd_xcd_kernel<R, CH, NTS><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-        rows, cols, vals, off, step, W, ldw, H, ldh, lr, lam);
+        rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -456,12 +463,13 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 // is a DEVICE array of 65 int64 cell offsets into rows/cols/vals (every cell < 2^31 ratings).
 // `chunk` (ratings per stream and round) is 32, 64 or 128; `variant` 1 = non-temporal H
 // stores (chunk 64 only; measured 23 % slower, kept for the record).
-HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, int r,
-                                int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw, float* H,
-                                int ldh, float lr, float lam, hipStream_t s) {
+// `win`: optional DEVICE array [2 x 64] of per-cell window starts and lengths (NULL = all).
+HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
+                                int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
+                                float* H, int ldh, float lr, float lam, hipStream_t s) {
   if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant < 0 || variant > 1)
     return HARP_EBADARG;
-#define SGDX_ARGS rows, cols, vals, off, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
+#define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
 #define SGDX_CALL(RR)                                                                          \
   (variant == 1 ? (chunk == 64 ? launch_sgd_xcd<RR, 64, true>(SGDX_ARGS) : HARP_EBADARG)            \
                 : chunk == 32 ? launch_sgd_xcd<RR, 32>(SGDX_ARGS)                                   \

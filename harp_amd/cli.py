@@ -187,7 +187,8 @@ def _run_sgd(comm, cfg):
     from .models.sgd_mf import SGDConfig, row_owner, run_sgd
 
     u, i, v, nu, ni, test = _mf_data(comm, cfg)
-    sc = SGDConfig(rank=cfg["rank"], lam=cfg["lam"], lr=cfg["epsilon"], epochs=cfg["iterations"])
+    sc = SGDConfig(rank=cfg["rank"], lam=cfg["lam"], lr=cfg["epsilon"], epochs=cfg["iterations"],
+                   train_fraction=min(1.0, max(cfg["train_ratio"], 1) / 100.0))
     u, i, v = shuffle_coo(comm, row_owner(u, comm.world_size, sc.seed), u, i, v.float())
     if test is not None:
         tu, ti, tv = test

@@ -39,6 +39,7 @@ class SGDConfig:
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
     kernel_variant: int = 0    # blocked kernel variant (reserved)
+    train_fraction: float = 1.0  # per rotation step each cell trains this fraction (window advances per epoch)
     random_order: bool = False  # random rotation orders (RotationUtil) vs ring
     test_every: int = 5        # rmseIteInterval
     seed: int = 0
@@ -217,9 +218,13 @@ class SGDCollectiveMapper(CollectiveMapper):
                 with timer.phase("compute"):
                     if cfg.xcd_blocks:
                         r_, c_, v_, off, hoff = self.train.get_cells(gs)
+                        win = MF.cell_windows(hoff, cfg.train_fraction, epoch) if cfg.train_fraction < 1.0 else None
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
-                                                   cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant)
+                                                   cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
+                                                   window=win)
                     else:
+                        if cfg.train_fraction < 1.0:
+                            raise ValueError("train_fraction < 1 needs the XCD-blocked layout")
                         n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
                 with timer.phase("rotate"):
                     self.rot.start(k, self.schedule.rotation_map(epoch, s))

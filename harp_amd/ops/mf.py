@@ -8,6 +8,8 @@ within the resident H slice, int32), ``vals`` (float32).
 from __future__ import annotations
 
 import ctypes
+import math
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -19,9 +21,9 @@ _lib.register({
     "harp_mf_sgd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
                     _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_void_p],
     "harp_mf_xcds": [],
-    "harp_mf_sgd_xcd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_int,
-                        _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float,
-                        _lib.c_void_p],
+    # rows, cols, vals, off, win, r, steps, chunk, blocks_per_xcd, variant, W, ldw, H, ldh, lr, lam, stream
+    "harp_mf_sgd_xcd": [_lib.c_void_p] * 5 + [_lib.c_int] * 5 + [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
+                                                                 _lib.c_float, _lib.c_float, _lib.c_void_p],
     "harp_mf_rmse_blocks": [],
     "harp_mf_rmse": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int,
                      _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
@@ -97,14 +99,18 @@ def balanced_blocks(group: torch.Tensor, idx: torch.Tensor, n_groups: int, n_idx
 
 def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, cell_off: torch.Tensor,
                        W: torch.Tensor, H: torch.Tensor, lr: float, lam: float, chunk: int = 64,
-                       blocks_per_xcd: int = 256, host_off: list | None = None, variant: int = 0) -> int:
+                       blocks_per_xcd: int = 256, host_off: list | None = None, variant: int = 0,
+                       window: Optional[Tuple[List[int], List[int]]] = None) -> int:
     """One SGD pass over ratings laid out in nb x nb cells (cell-major, user-sorted inside a
     cell; ``cell_off`` = nb*nb+1 int64 offsets on W's device). Sub-step s trains the nb
     row- and column-disjoint cells (x, (x+s) mod nb): on the GPU one XCD per cell
     (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
     ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path).
     ``chunk``: ratings per stream (32, 64 or 128 on the GPU); ``variant``: 0, or 1 = non-temporal
-    H stores (slower; see csrc/mf_sgd.hip)."""
+    H stores (slower; see csrc/mf_sgd.hip).
+    ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
+    ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
+    Returns the number of ratings trained."""
     _check(rows, cols, vals, W, H)
     n = rows.numel()
     if n == 0:
@@ -112,26 +118,59 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     r = W.shape[1]
     nb = XCDS
     assert cell_off.numel() == nb * nb + 1 and cell_off.dtype == torch.int64
+    trained = n if window is None else int(sum(window[1]))
     if _lib.use_native(W):
         if r not in SUPPORTED_RANKS:
             raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS}, got {r}")
         assert cell_off.device == W.device and cell_off.is_contiguous()
+        win = None
+        if window is not None:
+            win = torch.tensor(list(window[0]) + list(window[1]), dtype=torch.int64).pin_memory()
+            win = win.to(W.device, non_blocking=True)
         lib = _lib.kernels()
-        st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(), r, nb, chunk,
+        st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
+                                 _lib.ptr(win), r, nb, chunk,
                                  blocks_per_xcd, variant, W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr),
                                  float(lam), _lib.stream_ptr(W.device))
         _lib.check(st, "mf_sgd_xcd")
-        return n
+        if win is not None:
+            win.record_stream(torch.cuda.current_stream(W.device))
+        return trained
     off = host_off if host_off is not None else cell_off.tolist()
     rt = _rt()
+
+    def seg(a, m):
+        if m > 0:
+            rt.harp_mf_sgd_cpu(rows[a:].data_ptr(), cols[a:].data_ptr(), vals[a:].data_ptr(), m, r,
+                               W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam))
+
     for s in range(nb):
         for x in range(nb):
             c = x * nb + (x + s) % nb
             a, b = off[c], off[c + 1]
-            if b > a:
-                rt.harp_mf_sgd_cpu(rows[a:].data_ptr(), cols[a:].data_ptr(), vals[a:].data_ptr(), b - a, r,
-                                   W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam))
-    return n
+            if window is None:
+                seg(a, b - a)
+            else:
+                w0, L = int(window[0][c]), int(window[1][c])
+                first = min(L, (b - a) - w0)
+                seg(a + w0, first)
+                seg(a, L - first)
+    return trained
+
+
+def cell_windows(cell_off: List[int], fraction: float, epoch: int) -> Tuple[List[int], List[int]]:
+    """Fixed-fraction mode: every cell trains ceil(fraction * size) ratings per visit, the
+    window advancing by its length each epoch, so all ratings are trained once per
+    ceil(1 / fraction) epochs (deterministic stand-in for the reference's timer-bounded
+    rotation steps, whose timer is tuned to cover ``trainRatio`` % of the ratings:
+    SGDCollectiveMapper.java:623-668)."""
+    starts, lens = [], []
+    for c in range(len(cell_off) - 1):
+        m = cell_off[c + 1] - cell_off[c]
+        L = min(m, math.ceil(fraction * m))
+        starts.append((epoch * L) % m if m else 0)
+        lens.append(L)
+    return starts, lens
 
 
 def sse(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: torch.Tensor, H: torch.Tensor):

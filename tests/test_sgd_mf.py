@@ -128,3 +128,28 @@ def test_sgd_flat_and_blocked_layouts_both_converge(small):
     for blocked in (False, True):
         assert out[blocked]["rmse"][-1][2] < 0.6, out[blocked]["rmse"]
     assert abs(out[True]["rmse"][-1][2] - out[False]["rmse"][-1][2]) < 0.05
+
+
+def test_cell_windows_cover_every_rating():
+    from harp_amd.ops import mf as MF
+
+    off = [0, 10, 10, 37, 100]
+    seen = [set() for _ in range(4)]
+    for ep in range(4):  # fraction 0.3 -> ceil(1/0.3) = 4 epochs per full pass
+        st, ln = MF.cell_windows(off, 0.3, ep)
+        for c in range(4):
+            m = off[c + 1] - off[c]
+            assert ln[c] == min(m, -(-3 * m // 10))
+            seen[c] |= {(st[c] + k) % m for k in range(ln[c])} if m else set()
+    assert all(len(seen[c]) == off[c + 1] - off[c] for c in range(4))
+
+
+def test_sgd_fixed_fraction_mode(small):
+    """trainRatio-style fraction: each rotation step trains 50 % of every cell; two epochs
+    train every rating once and the model still converges."""
+    nu, ni, train, test = small
+    cfg = SGDConfig(rank=16, lam=0.05, lr=0.01, epochs=24, test_every=24, train_fraction=0.5)
+    res = launch(_job, 2, args=(cfg, nu, ni, train, test), timeout=300)
+    n = train[0].numel()
+    assert abs(sum(r["trained"] for r in res) - 12 * n) <= 2 * 64 * 2 * 24  # ceil per cell
+    assert res[0]["rmse"][-1][2] < 0.6

@@ -102,3 +102,19 @@ def test_sgd_xcd_many_streams_close_to_cpu(cuda):
     print(f"sse initial {e0:.4g} cpu {e_cpu:.4g} gpu-xcd {e_gpu:.4g}")
     assert e_gpu < 0.5 * e0
     assert abs(e_gpu - e_cpu) < 0.1 * e_cpu, (e_gpu, e_cpu)
+
+
+def test_sgd_xcd_windows_match_cpu(cuda):
+    """Fixed-fraction windows (wrapping around each cell) give the CPU schedule's result."""
+    R, C, V, off, W0, H0 = _cells(64, 48, 4000, 32, 3)
+    host = off.tolist()
+    win = MF.cell_windows(host, 0.4, epoch=2)  # starts past the middle: windows wrap
+    assert any(s + l > host[c + 1] - host[c] for c, (s, l) in enumerate(zip(*win)))
+    Wc, Hc = W0.clone(), H0.clone()
+    nc = MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.01, 0.05, window=win)
+    Wg, Hg = W0.to(cuda), H0.to(cuda)
+    ng = MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=128,
+                               blocks_per_xcd=4, window=win)
+    torch.cuda.synchronize()
+    assert nc == ng == sum(win[1])
+    assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
