@@ -8,24 +8,25 @@
 //
 // Design (MI355X-first):
 //  * one 16-lane subgroup = one sequential update stream; r/16 factors per lane, so a dot
-//    product is 16/r FMAs per lane + a 4-step xor reduction inside the subgroup; a wave runs
-//    four independent streams.
+//    product is r/16 packed FMAs per lane + a 4-step DPP row reduction; a wave runs four
+//    independent streams.
 //  * each stream owns a contiguous run of the slice's ratings sorted by USER: the user's
 //    w row stays in registers while its ratings stream past and is written back once per
-//    run; H rows are read and written per rating, lock-free across streams (Hogwild, as
-//    DAAL-SGD).
-//  * the next rating's (row, col, value) and H row are prefetched while the current one
-//    updates, so the dependent-load latency of the chain is overlapped.
-//  * XCD blocking (mf_sgd_xcd_kernel): the 8 XCDs have private, mutually non-coherent L2s.
-//    A flat Hogwild launch lets every XCD cache its own copy of hot H rows, so concurrent
-//    updates of one item from different XCDs overwrite each other at write-back, and every
-//    H access is served from the Infinity Fabric / MALL. The blocked layout cuts the
-//    resident slice into 8 x 8 (user block, item block) cells; in sub-step s the blocks of
-//    one XCD (blockIdx.x % 8 == x: blocks are dealt round-robin over the XCDs) train cell
-//    (x, (x + s) mod 8). The 8 cells of a sub-step share no user and no item, so each H
-//    block (~1/8 of the slice, well inside one XCD's 4 MB L2) is updated by one XCD only,
-//    and the kernel boundary between sub-steps publishes it — the Harp rotation schedule
-//    (dymoro), applied one level down, across the XCDs of a GPU.
+//    run; H rows are read (from L2, bypassing the CU's L1) and written per rating,
+//    lock-free across streams (Hogwild, as DAAL-SGD).
+//  * XCD blocking (mf_sgd_xcd_kernel, the production path): the 8 XCDs have private,
+//    mutually non-coherent L2s. A flat Hogwild launch lets every XCD cache its own copy of
+//    hot H rows, so concurrent updates of one item from different XCDs overwrite each other
+//    at write-back, and H is served from the Infinity Fabric / MALL. The blocked layout
+//    cuts the resident slice into 8 x 8 equal-work (user block, item block) cells; in
+//    sub-step s the blocks of one XCD (blocks sharing blockIdx.x % 8 share an XCD) train
+//    cell (x, (x + s) mod 8). The 8 cells of a sub-step share no user and no item, so each
+//    H block (~1/8 of the slice, inside one XCD's 4 MB L2) is updated by one XCD only, and
+//    the kernel boundary between sub-steps publishes it — the Harp rotation schedule
+//    (dymoro), applied one level down, across the XCDs of a GPU. Index triples are staged
+//    through LDS and H rows prefetched two ratings ahead (sgd_stream_lds).
+//  * the flat kernel (mf_sgd_kernel) keeps the original one-stream-per-chunk launch for
+//    comparison and for unblocked rating sets.
 #include "common.h"
 
 namespace {
