@@ -158,8 +158,15 @@ struct DocRow<unsigned short> {
   }
 };
 
-template <int TPL, class DT>  // topics per lane; K_pad = 64 * TPL
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ? 4 : 5, 8))) void lda_cgs_kernel(
+// PF = 1: the doc-topic row of the NEXT token is loaded (raw) while this token samples, so
+// the random HBM row fetch leaves the per-token critical path; a row of the same document
+// is patched in registers with this token's topic move (the load was issued before this
+// token's atomics: same-wave program order), other documents' rows are Hogwild as before.
+// Measured (profiles/r1_lda/ldapf): 0.90e9 vs 1.17e9 tokens/s for PF = 0 at K = 1000 —
+// the extra 16 VGPRs drop occupancy from 4 to 3 waves/SIMD, and more resident waves hide
+// the row latency better than one-token-ahead prefetch; PF = 0 stays the default.
+template <int TPL, class DT, int PF = 0>  // topics per lane; K_pad = 64 * TPL
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ? 4 - PF : 5 - PF, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
@@ -199,21 +206,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ?
     for (int t = 0; t < TPL; ++t) qw[t] = (nwf[t] + beta) * s_inv[k0 + t];
     int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
                                            // waits on ONE memory round trip, not two
+    unsigned rn[TPL];  // PF: raw doc row of the next token (in flight)
+    int d_nn = 0, z_nn = 0, pz = -1, pnz = -1;
+    if constexpr (PF) {
+      DocRow<DT>::template load_raw<TPL>(ndk + (long)d_next * ldd, k0, rn);
+      if (a + 1 < b) {
+        d_nn = tdoc[a + 1];
+        z_nn = tz[a + 1];
+      }
+    }
     for (long i = a; i < b; ++i) {
       const int d = d_next;
       const int z = z_next;
-      if (i + 1 < b) {
-        d_next = tdoc[i + 1];
-        z_next = tz[i + 1];
-      }
       DT* drow = ndk + (long)d * ldd;
       float nd[TPL];
-      {
+      if constexpr (PF) {
+        unsigned rc[TPL];
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) rc[t] = rn[t];
+        if (pz >= 0) DocRow<DT>::template patch<TPL>(rc, lane, pz, pnz);  // previous token, same doc
+        if (i + 1 < b) {
+          d_next = d_nn;
+          z_next = z_nn;
+          DocRow<DT>::template load_raw<TPL>(ndk + (long)d_next * ldd, k0, rn);
+          if (i + 2 < b) {
+            d_nn = tdoc[i + 2];
+            z_nn = tz[i + 2];
+          }
+        }
+        int ndi[TPL];
+        DocRow<DT>::template unpack<TPL>(rc, ndi);
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
+      } else {
+        if (i + 1 < b) {
+          d_next = tdoc[i + 1];
+          z_next = tz[i + 1];
+        }
         int ndi[TPL];
         DocRow<DT>::template load<TPL>(drow, k0, ndi);
 #pragma unroll
         for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
-      }      // remove the token: only lane z / TPL changes, at the uniform slot z % TPL (a
+      }
+      // remove the token: only lane z / TPL changes, at the uniform slot z % TPL (a
       // scalar branch picks the slot; one lane updates three registers)
       const int zl = z / TPL, zt = z % TPL;
       const float inv_z = s_inv[z];
@@ -271,6 +306,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ?
           atomicAdd(&s_delta[nz], 1);
         }
       }
+      if constexpr (PF) {  // the prefetched next row predates this move: patch it if same doc
+        pz = (d_next == d && i + 1 < b) ? z : -1;
+        pnz = nz;
+      }
     }
     // flush this chunk's word-row delta
 #pragma unroll
@@ -300,7 +339,7 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 }  // namespace
 
 namespace {
-template <class DT>
+template <class DT, int PF>
 int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
                int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
                unsigned long long seed, hipStream_t s) {
@@ -309,15 +348,15 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
   const dim3 g((unsigned)blocks), bl(256);
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
-    lda_cgs_kernel<4, DT><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<4, DT, PF><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                            nk_delta, K, alpha, beta, seed);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
-    lda_cgs_kernel<8, DT><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<8, DT, PF><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                            nk_delta, K, alpha, beta, seed);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
-    lda_cgs_kernel<16, DT><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<16, DT, PF><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                             nk_delta, K, alpha, beta, seed);
   }
   return harp_launch_status();
@@ -325,21 +364,26 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
 }  // namespace
 
 // ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8)
+// variant: 0 = doc row loaded per token, 1 = next token's doc row prefetched (see PF)
 HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
                              void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
-                             int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
+                             int K, float alpha, float beta, unsigned long long seed, int variant, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  if (K <= 0 || K > 1024 || ldw % 4) return HARP_EBADARG;
+  if (K <= 0 || K > 1024 || ldw % 4 || variant < 0 || variant > 1) return HARP_EBADARG;
+#define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks
+#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
-    return launch_cgs<int>(tdoc, tword, tz, chunk_start, nchunks, (int*)ndk, ldd, nwk, ldw, inv_nk, nk_delta, K,
-                           alpha, beta, seed, s);
+    return variant ? launch_cgs<int, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+                   : launch_cgs<int, 0>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL);
   }
   if (ndk_bits == 16) {
     if (ldd % 8) return HARP_EBADARG;
-    return launch_cgs<unsigned short>(tdoc, tword, tz, chunk_start, nchunks, (unsigned short*)ndk, ldd, nwk, ldw,
-                                      inv_nk, nk_delta, K, alpha, beta, seed, s);
+    return variant ? launch_cgs<unsigned short, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+                   : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
   }
+#undef CGS_ARGS
+#undef CGS_TAIL
   return HARP_EBADARG;
 }
 

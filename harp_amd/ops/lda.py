@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -10,10 +11,14 @@ from . import _lib
 _lib.register({
     "harp_lda_cgs": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int,
                      _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
-                     _lib.c_float, _lib.c_ulonglong, _lib.c_void_p],
+                     _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
     "harp_lda_count": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_int,
                        _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
 })
+
+
+# 1 = the next token's doc-topic row is prefetched during sampling (csrc/lda.hip PF)
+SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "0"))
 
 
 def padded_topics(K: int) -> int:
@@ -85,7 +90,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
         st = _lib.kernels().harp_lda_cgs(tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(),
                                          chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
-                                         seed & 0xFFFFFFFFFFFFFFFF, _lib.stream_ptr(dev))
+                                         seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT, _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
         return delta
     rt = _lib.runtime()
