@@ -165,8 +165,8 @@ struct DocRow<unsigned short> {
 // Measured (profiles/r1_lda/ldapf): 0.90e9 vs 1.17e9 tokens/s for PF = 0 at K = 1000 —
 // the extra 16 VGPRs drop occupancy from 4 to 3 waves/SIMD, and more resident waves hide
 // the row latency better than one-token-ahead prefetch; PF = 0 stays the default.
-template <int TPL, class DT, int PF = 0>  // topics per lane; K_pad = 64 * TPL
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPL == 16 ? 4 - PF : 5 - PF, 8))) void lda_cgs_kernel(
+template <int TPL, class DT, int PF = 0, int XW = 0>  // topics per lane; K_pad = 64 * TPL; XW: +waves/SIMD
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 ? 4 - PF + XW : 5 - PF + XW) < 8 ? (TPL == 16 ? 4 - PF + XW : 5 - PF + XW) : 8, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
@@ -339,7 +339,7 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 }  // namespace
 
 namespace {
-template <class DT, int PF>
+template <class DT, int PF, int XW = 0>
 int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
                int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
                unsigned long long seed, hipStream_t s) {
@@ -348,15 +348,15 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
   const dim3 g((unsigned)blocks), bl(256);
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
-    lda_cgs_kernel<4, DT, PF><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<4, DT, PF, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                            nk_delta, K, alpha, beta, seed);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
-    lda_cgs_kernel<8, DT, PF><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<8, DT, PF, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                            nk_delta, K, alpha, beta, seed);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
-    lda_cgs_kernel<16, DT, PF><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<16, DT, PF, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                             nk_delta, K, alpha, beta, seed);
   }
   return harp_launch_status();
@@ -364,23 +364,32 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
 }  // namespace
 
 // ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8)
-// variant: 0 = doc row loaded per token, 1 = next token's doc row prefetched (see PF)
+// variant: 0 = doc row loaded per token, 1 = next token's doc row prefetched (see PF),
+// 2..5 = variant 0 held to 1..4 more waves per SIMD (fewer VGPRs, some spilled)
 HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
                              void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
                              int K, float alpha, float beta, unsigned long long seed, int variant, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  if (K <= 0 || K > 1024 || ldw % 4 || variant < 0 || variant > 1) return HARP_EBADARG;
+  if (K <= 0 || K > 1024 || ldw % 4 || variant < 0 || variant > 5) return HARP_EBADARG;
 #define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks
 #define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
-    return variant ? launch_cgs<int, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
-                   : launch_cgs<int, 0>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL);
+    return variant == 1   ? launch_cgs<int, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+           : variant == 2 ? launch_cgs<int, 0, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+           : variant == 3 ? launch_cgs<int, 0, 2>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+           : variant == 4 ? launch_cgs<int, 0, 3>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+           : variant == 5 ? launch_cgs<int, 0, 4>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+                          : launch_cgs<int, 0>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL);
   }
   if (ndk_bits == 16) {
     if (ldd % 8) return HARP_EBADARG;
-    return variant ? launch_cgs<unsigned short, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
-                   : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
+    return variant == 1   ? launch_cgs<unsigned short, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+           : variant == 2 ? launch_cgs<unsigned short, 0, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+           : variant == 3 ? launch_cgs<unsigned short, 0, 2>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+           : variant == 4 ? launch_cgs<unsigned short, 0, 3>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+           : variant == 5 ? launch_cgs<unsigned short, 0, 4>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+                          : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
   }
 #undef CGS_ARGS
 #undef CGS_TAIL
