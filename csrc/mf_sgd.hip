@@ -340,8 +340,8 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
 // 16-lane subgroup runs one stream. `win` (optional, 2 x 64 int64): cell c trains only the
 // window of win[64 + c] ratings starting at win[c], wrapping around the cell — the
 // fixed-fraction mode standing in for the reference's timer-bounded rotation steps.
-template <int R, int CH, bool NTS = false>
-__global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
+template <int R, int CH, bool NTS = false, int MINW = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
                                                          const long* __restrict__ win, int step,
                                                          float* __restrict__ W, int ldw, float* __restrict__ H, int ldh,
@@ -417,11 +417,11 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
-template <int R, int CH, bool NTS = false>
+template <int R, int CH, bool NTS = false, int MINW = 1>
 int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win, int steps,
                    int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
-    mf_sgd_xcd_kernel<R, CH, NTS><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+    mf_sgd_xcd_kernel<R, CH, NTS, MINW><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
         rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
@@ -463,16 +463,21 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 // All `steps` (= 8) sub-steps of the XCD-blocked schedule over one resident slice: `off`
 // is a DEVICE array of 65 int64 cell offsets into rows/cols/vals (every cell < 2^31 ratings).
 // `chunk` (ratings per stream and round) is 32, 64 or 128; `variant` 1 = non-temporal H
-// stores (chunk 64 only; measured 23 % slower, kept for the record).
+// stores (chunk 64 only; measured 23 % slower, kept for the record); 2 / 3 / 4 = at least
+// 6 / 7 / 8 waves per SIMD (chunk 64; VGPRs trimmed, possibly spilled).
 // `win`: optional DEVICE array [2 x 64] of per-cell window starts and lengths (NULL = all).
 HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
                                 int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
                                 float* H, int ldh, float lr, float lam, hipStream_t s) {
-  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant < 0 || variant > 1)
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant < 0 || variant > 4)
     return HARP_EBADARG;
 #define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
 #define SGDX_CALL(RR)                                                                          \
   (variant == 1 ? (chunk == 64 ? launch_sgd_xcd<RR, 64, true>(SGDX_ARGS) : HARP_EBADARG)            \
+   : variant >= 2 ? (chunk != 64 ? HARP_EBADARG                                                      \
+                     : variant == 2 ? launch_sgd_xcd<RR, 64, false, 6>(SGDX_ARGS)                    \
+                     : variant == 3 ? launch_sgd_xcd<RR, 64, false, 7>(SGDX_ARGS)                    \
+                                    : launch_sgd_xcd<RR, 64, false, 8>(SGDX_ARGS))                   \
                 : chunk == 32 ? launch_sgd_xcd<RR, 32>(SGDX_ARGS)                                   \
                               : chunk == 64 ? launch_sgd_xcd<RR, 64>(SGDX_ARGS)                     \
                                             : chunk == 128 ? launch_sgd_xcd<RR, 128>(SGDX_ARGS)     \
