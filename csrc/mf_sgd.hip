@@ -31,17 +31,30 @@
 
 namespace {
 
+// Factor-row layout inside a 16-lane stream: lane sl holds the float4 chunks at
+// row + 64*q + 4*sl (q < EPL/4), or for EPL % 4 != 0 the floats at row + 16*k + sl. Every
+// wave instruction then reads / writes whole contiguous 256-B (64-B) row segments — full
+// 128-B L2 lines. (The first layout, lane-contiguous chunks of EPL floats, made each
+// dwordx4 instruction touch every other 16 B: half-filled sectors, twice the L2 write
+// requests, and the texture addresser 86 % busy — profiles/r1_sgd_xcd/sgdpmc.) Any
+// layout works as long as W and H use the same one: the update is elementwise and the
+// dot product sums over all factors.
+template <int EPL>
+__device__ __forceinline__ unsigned lane_off(int sl) {
+  return EPL % 4 == 0 ? 4u * (unsigned)sl : (unsigned)sl;
+}
+
 template <int EPL>
 __device__ __forceinline__ void load_row(const float* __restrict__ p, float (&x)[EPL]) {
   if constexpr (EPL % 4 == 0) {
 #pragma unroll
     for (int k = 0; k < EPL; k += 4) {
-      const floatx4 v = *(const floatx4*)(p + k);
+      const floatx4 v = *(const floatx4*)(p + 16 * k);
       x[k] = v[0]; x[k + 1] = v[1]; x[k + 2] = v[2]; x[k + 3] = v[3];
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) x[k] = p[k];
+    for (int k = 0; k < EPL; ++k) x[k] = p[16 * k];
   }
 }
 
@@ -53,12 +66,12 @@ __device__ __forceinline__ void load_row_l2(const float* __restrict__ p, float (
   if constexpr (EPL % 4 == 0) {
 #pragma unroll
     for (int k = 0; k < EPL; k += 4) {
-      const floatx4 v = __builtin_nontemporal_load((const floatx4*)(p + k));
+      const floatx4 v = __builtin_nontemporal_load((const floatx4*)(p + 16 * k));
       x[k] = v[0]; x[k + 1] = v[1]; x[k + 2] = v[2]; x[k + 3] = v[3];
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) x[k] = __builtin_nontemporal_load(p + k);
+    for (int k = 0; k < EPL; ++k) x[k] = __builtin_nontemporal_load(p + 16 * k);
   }
 }
 
@@ -67,10 +80,10 @@ __device__ __forceinline__ void store_row_nt(float* __restrict__ p, const float 
   if constexpr (EPL % 4 == 0) {
 #pragma unroll
     for (int k = 0; k < EPL; k += 4)
-      __builtin_nontemporal_store(floatx4{x[k], x[k + 1], x[k + 2], x[k + 3]}, (floatx4*)(p + k));
+      __builtin_nontemporal_store(floatx4{x[k], x[k + 1], x[k + 2], x[k + 3]}, (floatx4*)(p + 16 * k));
   } else {
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) __builtin_nontemporal_store(x[k], p + k);
+    for (int k = 0; k < EPL; ++k) __builtin_nontemporal_store(x[k], p + 16 * k);
   }
 }
 
@@ -78,10 +91,10 @@ template <int EPL>
 __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&x)[EPL]) {
   if constexpr (EPL % 4 == 0) {
 #pragma unroll
-    for (int k = 0; k < EPL; k += 4) *(floatx4*)(p + k) = floatx4{x[k], x[k + 1], x[k + 2], x[k + 3]};
+    for (int k = 0; k < EPL; k += 4) *(floatx4*)(p + 16 * k) = floatx4{x[k], x[k + 1], x[k + 2], x[k + 3]};
   } else {
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) p[k] = x[k];
+    for (int k = 0; k < EPL; ++k) p[16 * k] = x[k];
   }
 }
 
@@ -138,7 +151,7 @@ __device__ __forceinline__ void sgd_stream(const int* __restrict__ rows, const i
   constexpr int EPL = R / 16;
   constexpr int PAIRS = EPL / 2;
   const float decay = 1.0f - lr * lam;
-  const unsigned lo = (unsigned)sl * EPL;
+  const unsigned lo = lane_off<EPL>(sl);
   float w[EPL], h[EPL], hA[EPL], hB[EPL];
   unsigned base = u0;
   int bR = 0, bC = 0, nR = 0, nC = 0;
@@ -260,7 +273,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
   constexpr int EPL = R / 16;
   constexpr int PAIRS = EPL / 2;
   const float decay = 1.0f - lr * lam;
-  const unsigned lo = (unsigned)sl * EPL;
+  const unsigned lo = lane_off<EPL>(sl);
   float w[EPL], h[EPL], hp[EPL], hA[EPL], hB[EPL];
   unsigned cur = (unsigned)sR[0], col0 = (unsigned)sC[0], colp = 0xffffffffu;
   float v0 = sV[0];
@@ -390,8 +403,8 @@ __global__ __launch_bounds__(256) void mf_rmse_kernel(const int* __restrict__ ro
   float acc = 0.f;
   for (long i = (((long)blockIdx.x * blockDim.x + threadIdx.x) >> 4); i < n; i += nsub) {
     float w[EPL], h[EPL];
-    load_row<EPL>(W + (long)rows[i] * ldw + sl * EPL, w);
-    load_row<EPL>(H + (long)cols[i] * ldh + sl * EPL, h);
+    load_row<EPL>(W + (long)rows[i] * ldw + lane_off<EPL>(sl), w);
+    load_row<EPL>(H + (long)cols[i] * ldh + lane_off<EPL>(sl), h);
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) dot = fmaf(w[k], h[k], dot);
