@@ -1,9 +1,9 @@
 set -o pipefail
-O=gpurun_out/sgdlayout
+O=gpurun_out/ldamap
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_sgd_mf_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1 || exit 1
-for v in 0 2; do
-  timeout -k 10 240 python scripts/bench_sgd.py --epochs 3 --variant $v > $O/v$v.log 2>&1 || exit 1
+for v in 0 1 3; do
+  HARP_LDA_VARIANT=$v timeout -k 10 300 python -u -m pytest tests/test_lda_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test_v$v.log 2>&1 || exit 1
 done
-timeout -k 10 240 python scripts/bench_sgd.py --epochs 3 --layout flat > $O/flat.log 2>&1 || exit 1
-timeout -k 10 240 python scripts/bench_sgd.py --epochs 3 --skew 1 > $O/skew1.log 2>&1 || exit 1
+for v in 0 2 3 4; do
+  HARP_LDA_VARIANT=$v timeout -k 10 400 python scripts/bench_lda.py --iters 3 > $O/bench_v$v.log 2>&1 || exit 1
+done
