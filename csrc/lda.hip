@@ -336,6 +336,198 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Sparse-doc sampler (any K <= 16384; the only path for K > 1024 — BASELINE #5 runs
+// K = 10,000). The reference's SparseLDA (LDAMPTask.java:85-330) splits
+//   p(t) ~ (n_dt + alpha) * qw_t,   qw_t = (n_wt + beta) / (n_t + V beta)
+// into a doc bucket sum_t n_dt qw_t and a smoothing bucket alpha * sum_t qw_t. Here the
+// doc bucket is formed WITHOUT doc-topic counts: sum_t n_dt qw_t == sum over the doc's
+// other tokens j of qw[z_j], so a token reads its document's topic list (zdoc, doc
+// order, 2 B per token: a few hundred bytes, not a K-wide row) and gathers qw from LDS.
+//  * ONE workgroup per word chunk; the word's qw[Kp] row lives in LDS (4 B x Kp: 40 KB at
+//    K = 10,000, four 8-wave workgroups per CU) and the workgroup's waves sample the
+//    chunk's tokens round-robin. qw is linear in the count (a move changes qw_t by exactly
+//    +-1/(n_t + V beta)), so moves are LDS float atomics on qw itself and no count row is
+//    kept (an 8 B/topic {count, qw} layout fitted only two workgroups per CU: 0.85e9 vs
+//    1.14e9 tokens/s at K = 10,000).
+//  * the smoothing bucket is a two-level draw: per-64-topic block sums of qw (LDS, moved
+//    by exactly +-1/(n_t + V beta) per token move, rebuilt per chunk) pick the block with
+//    one wave scan, a second scan over the block's 64 topics picks the topic — ~60
+//    instructions instead of a K-wide scan (which bounded the first version at
+//    3.5e8 tokens/s for K = 10,000);
+//  * doc-bucket draws scan the doc list; the lane holding the draw walks its elements;
+//  * chunks are handed out by an atomic work counter in ``order`` (longest first): the
+//    grid is only the resident workgroups, and a static chunk stride left the CUs
+//    waiting on the few longest words;
+//  * the next token's ids are fetched one token ahead (the doc range read is otherwise
+//    a chain of three dependent memory round trips);
+//  * zdoc and the word row are read with non-temporal loads (past the CU L1, which other
+//    CUs' writes do not invalidate);
+//  * word-row moves go straight to the global n_wk row (two atomics) so chunks of one
+//    word on different workgroups stay exact; doc-topic counts (when kept) and topic-sum
+//    deltas are updated with atomics as in the dense kernel.
+template <int WAVES, class DT>
+__global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
+    const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
+    const long* __restrict__ chunk_start, long nchunks, const int* __restrict__ order, int* __restrict__ work,
+    const long* __restrict__ tpos, const long* __restrict__ doc_off, unsigned short* __restrict__ zdoc,
+    DT* __restrict__ ndk, int ldd,
+    int* __restrict__ nwk, int ldw, const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, int Kp,
+    float alpha, float beta, unsigned long long seed) {
+  extern __shared__ float smem[];
+  float* s_qw = smem;
+  __shared__ float s_bs[256];  // per-64-topic block sums of qw (Kp <= 16384)
+  __shared__ float s_q;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int nb = Kp >> 6;
+  __shared__ int s_c;
+  for (;;) {
+    __syncthreads();  // the previous chunk's samplers are done with the LDS rows (and s_c)
+    if (threadIdx.x == 0) s_c = atomicAdd(work, 1);
+    __syncthreads();
+    if (s_c >= nchunks) break;
+    const long c = order ? order[s_c] : s_c;
+    const long a = chunk_start[c], b = chunk_start[c + 1];
+    int* wrow = nwk + (long)tword[a] * ldw;
+    for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
+      s_qw[t] = t < K ? ((float)__builtin_nontemporal_load(wrow + t) + beta) * inv_nk[t] : 0.f;
+    }
+    __syncthreads();
+    for (int k = wv; k < nb; k += WAVES) {
+      const float v = wave_incl_scan(s_qw[64 * k + lane], lane);
+      if (lane == 63) s_bs[k] = v;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      float v = 0.f;
+      for (int k = lane; k < nb; k += 64) v += s_bs[k];
+      v = wave_incl_scan(v, lane);
+      if (lane == 63) s_q = v;
+    }
+    __syncthreads();
+    long i = a + wv;
+    int d = 0, z = 0;
+    long p = 0, lo = 0, hi = 0;
+    float inv_z = 0.f;
+    if (i < b) {
+      d = tdoc[i];
+      z = tz[i];
+      p = tpos[i];
+      lo = doc_off[d];
+      hi = doc_off[d + 1];
+      inv_z = inv_nk[z];
+    }
+    for (; i < b; i += WAVES) {
+      const long inx = i + WAVES;
+      int dn = 0, zn = 0;
+      long pn = 0;
+      if (inx < b) {
+        dn = tdoc[inx];
+        zn = tz[inx];
+        pn = tpos[inx];
+      }
+      const float qz = s_qw[z] - inv_z;  // z's factor without this token
+      float sb = 0.f;
+      for (long j = lo + lane; j < hi; j += 64) {
+        const int zj = __builtin_nontemporal_load(zdoc + j);
+        sb += j == p ? 0.f : (zj == z ? qz : s_qw[zj]);
+      }
+      const float inclb = wave_incl_scan(sb, lane);
+      const float B = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inclb), 63));
+      const float corr = inv_z;
+      const float A = alpha * fmaxf(s_q - corr, 0.f);
+      const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
+      const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * (A + B);
+      // next token's doc range and topic factor: its ids have arrived by now
+      long lon = 0, hin = 0;
+      float invn = 0.f;
+      if (inx < b) {
+        lon = doc_off[dn];
+        hin = doc_off[dn + 1];
+        invn = inv_nk[zn];
+      }
+      int nz;
+      if (u < B) {  // doc bucket: the topic of one of the doc's other tokens
+        const unsigned long long hit = __ballot(inclb > u);
+        const int src = hit ? (int)__builtin_ctzll(hit) : 63;
+        int f = z;
+        if (lane == src) {
+          float pre = inclb - sb;
+          for (long j = lo + lane; j < hi; j += 64) {
+            if (j == p) continue;
+            const int zj = __builtin_nontemporal_load(zdoc + j);
+            f = zj;
+            pre += zj == z ? qz : s_qw[zj];
+            if (pre > u) break;
+          }
+        }
+        nz = __builtin_amdgcn_readlane(f, src);
+      } else {  // smoothing bucket: block by block sums, then topic within the block
+        const float u2 = (u - B) / alpha;
+        const int zb = z >> 6;
+        float sd = 0.f;
+        for (int k = lane; k < nb; k += 64) sd += s_bs[k] - (k == zb ? corr : 0.f);
+        const float incld = wave_incl_scan(sd, lane);
+        const unsigned long long hit = __ballot(incld > u2);
+        const int src = hit ? (int)__builtin_ctzll(hit) : 63;
+        int fb = nb - 1;
+        float base = 0.f;
+        if (lane == src) {
+          float pre = incld - sd;
+          for (int k = lane; k < nb; k += 64) {
+            const float v = s_bs[k] - (k == zb ? corr : 0.f);
+            fb = k;
+            base = pre;
+            if (pre + v > u2) break;
+            pre += v;
+          }
+        }
+        fb = __builtin_amdgcn_readlane(fb, src);
+        base = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(base), src));
+        const int t = 64 * fb + lane;
+        const float q = t < K ? (t == z ? qz : s_qw[t]) : 0.f;
+        const float inclt = wave_incl_scan(q, lane) + base;
+        const unsigned long long h2 = __ballot(inclt > u2);
+        const unsigned long long pos = __ballot(q > 0.f);
+        const int s2 = h2 ? (int)__builtin_ctzll(h2) : (pos ? 63 - (int)__builtin_clzll(pos) : 0);
+        nz = 64 * fb + s2;
+      }
+      if (nz < 0 || nz >= K) nz = z;
+      if (lane == 0) {
+        tz[i] = nz;
+        if (nz != z) {
+          zdoc[p] = (unsigned short)nz;
+          if (ndk) {
+            DocRow<DT>::add(ndk + (long)d * ldd, z, -1);
+            DocRow<DT>::add(ndk + (long)d * ldd, nz, 1);
+          }
+          const float inv_nz = inv_nk[nz];
+          atomicAdd(&s_qw[z], -inv_z);
+          atomicAdd(&s_qw[nz], inv_nz);
+          atomicAdd(&s_bs[z >> 6], -inv_z);
+          atomicAdd(&s_bs[nz >> 6], inv_nz);
+          atomicAdd(&s_q, inv_nz - inv_z);
+          atomicSub(wrow + z, 1);
+          atomicAdd(wrow + nz, 1);
+          atomicSub(nk_delta + z, 1);
+          atomicAdd(nk_delta + nz, 1);
+        }
+      }
+      // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
+      // one wave are separate threads to the compiler, so order them explicitly
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      d = dn;
+      z = zn;
+      p = pn;
+      lo = lon;
+      hi = hin;
+      inv_z = invn;
+    }
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -394,6 +586,70 @@ HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const l
 #undef CGS_ARGS
 #undef CGS_TAIL
   return HARP_EBADARG;
+}
+
+namespace {
+template <int WAVES, class DT>
+int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, const int* order,
+                  int* work, const long* tpos,
+                  const long* doc_off, unsigned short* zdoc, DT* ndk, int ldd, int* nwk, int ldw, const float* inv_nk,
+                  int* nk_delta, int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
+  const int Kp = (K + 63) / 64 * 64;
+  const size_t lds = 4 * (size_t)Kp;
+  static size_t lds_set = 0;  // raise the dynamic-LDS cap past 64 KB once per instantiation
+  if (lds > 65536 && lds > lds_set) {
+    if (hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return HARP_ELAUNCH;
+    lds_set = lds;
+  }
+  // grid = resident workgroups (LDS- or wave-slot-bound), striding over the chunks
+  long per_cu = 163840 / (long)(lds + 1100);
+  if (per_cu > 32 / WAVES) per_cu = 32 / WAVES;
+  if (per_cu < 1) per_cu = 1;
+  long blocks = nchunks;
+  if (blocks > 256 * per_cu) blocks = 256 * per_cu;
+  lda_cgs_sparse_kernel<WAVES, DT><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
+      tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
+      beta, seed);
+  return harp_launch_status();
+}
+}  // namespace
+
+// Sparse-doc sampler (see lda_cgs_sparse_kernel): tpos[i] = doc-order position of token i
+// in zdoc (uint16 topics, doc_off[d] .. doc_off[d + 1] = doc d); ndk may be null (no
+// doc-topic counts kept); waves: workgroup size in waves (1, 2, 4, 8 or 16; 0 = by K); order: chunk
+// processing order (null = 0..nchunks-1); work: ONE int, zero on entry (chunk counter).
+HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
+                                    const int* order, int* work, const long* tpos, const long* doc_off, unsigned short* zdoc, void* ndk, int ldd,
+                                    int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K,
+                                    float alpha, float beta, unsigned long long seed, int waves, hipStream_t s) {
+  if (nchunks <= 0) return HARP_OK;
+  if (K <= 0 || K > 16384 || ldw < K || (ndk && ldd < K) || !tpos || !doc_off || !zdoc || !work) return HARP_EBADARG;
+  if (waves == 0) {  // auto: enough waves per workgroup to fill 32 wave slots per CU within the LDS budget
+    const long per_cu = 163840 / (4L * ((K + 63) / 64 * 64) + 1100);
+    waves = per_cu >= 8 ? 4 : per_cu >= 4 ? 8 : 16;
+  }
+#define SP_ARGS tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc
+#define SP_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
+  if (ndk_bits == 16) {
+    if (ldd % 2) return HARP_EBADARG;
+    unsigned short* n16 = (unsigned short*)ndk;
+    return waves == 1    ? launch_sparse<1>(SP_ARGS, n16, ldd, SP_TAIL)
+           : waves == 2  ? launch_sparse<2>(SP_ARGS, n16, ldd, SP_TAIL)
+           : waves == 4  ? launch_sparse<4>(SP_ARGS, n16, ldd, SP_TAIL)
+           : waves == 16 ? launch_sparse<16>(SP_ARGS, n16, ldd, SP_TAIL)
+                         : launch_sparse<8>(SP_ARGS, n16, ldd, SP_TAIL);
+  }
+  if (ndk_bits != 32) return HARP_EBADARG;
+  int* n32 = (int*)ndk;
+  return waves == 1    ? launch_sparse<1>(SP_ARGS, n32, ldd, SP_TAIL)
+         : waves == 2  ? launch_sparse<2>(SP_ARGS, n32, ldd, SP_TAIL)
+         : waves == 4  ? launch_sparse<4>(SP_ARGS, n32, ldd, SP_TAIL)
+         : waves == 16 ? launch_sparse<16>(SP_ARGS, n32, ldd, SP_TAIL)
+                       : launch_sparse<8>(SP_ARGS, n32, ldd, SP_TAIL);
+#undef SP_ARGS
+#undef SP_TAIL
 }
 
 HARP_EXPORT int harp_lda_count(const int* tdoc, const int* tword, const int* tz, long n, void* ndk, int ldd,

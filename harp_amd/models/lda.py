@@ -8,8 +8,9 @@ the resident slice; log-likelihood every ``printInterval`` via allreduce (:699-7
 CalcLikelihoodTask.java:60-78 mallet Dirichlet terms).
 
 MI355X design: tokens are bucketed once by word slice and word-sorted into chunks; each
-resident-slice pass is one ``lda_cgs`` kernel (wave per word chunk, register word row,
-wave-scan sampler); slices rotate on private RCCL channels (DeviceRotator) overlapping
+resident-slice pass is one ``lda_cgs`` kernel (K <= 1024: wave per word chunk, register
+word row, wave-scan sampler; larger K: the sparse-doc sampler, workgroup per word chunk
+with the word row in LDS and the doc bucket read from a doc-order topic list); slices rotate on private RCCL channels (DeviceRotator) overlapping
 the next slice's sampling; topic-sum deltas are allreduced once per iteration.
 """
 from __future__ import annotations
@@ -36,7 +37,7 @@ class LDAConfig:
     num_slices: int = 2
     print_interval: int = 5
     seed: int = 0
-    max_chunk: int = 2048
+    max_chunk: int = 0        # tokens per word chunk; 0 = 2048 (dense sampler) / 65536 (sparse)
     block_words: int = 4096   # push/pull strategy: words per model partition
 
 
@@ -75,6 +76,7 @@ class LDACollectiveMapper(CollectiveMapper):
         K = cfg.num_topics
         self.Kp = L.padded_topics(K)
         doc, word = self._tokens
+        self.sparse = L.use_sparse(K, doc.numel())  # same choice on every worker
         mine = (doc % P) == me
         doc, word = doc[mine].to(dev), word[mine].to(dev)
         self.ndoc_local = (self.n_docs - me + P - 1) // P
@@ -97,9 +99,11 @@ class LDACollectiveMapper(CollectiveMapper):
         self.chunks = []
         for s in range(ns):
             a, b = self.offsets[s], self.offsets[s + 1]
-            self.chunks.append(L.build_chunks(self.tword[a:b], cfg.max_chunk))
+            self.chunks.append(L.build_chunks(self.tword[a:b], L.max_chunk(cfg.max_chunk, self.sparse)))
         gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
+        self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local) if self.sparse else None
+        self.orders = [L.chunk_order(c) for c in self.chunks] if self.doc_index is not None else [None] * ns
         # counts: doc-topic local; word-topic global (allreduced once), then each worker keeps
         # the slices of its initial placement
         maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
@@ -137,7 +141,9 @@ class LDACollectiveMapper(CollectiveMapper):
                 if b > a:
                     d = L.cgs_sample(self.tdoc[a:b], self.tword[a:b], self.tz[a:b], self.chunks[gs], self.ndk, slab,
                                      nk_view, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
-                                     (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ k)
+                                     (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ k, self.doc_index,
+                                     self.doc_index.tpos[a:b] if self.doc_index is not None else None,
+                                     self.orders[gs])
                     delta_total += d
                     nk_view = self.nk + delta_total
                     n += b - a
@@ -207,6 +213,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self.Kp = L.padded_topics(K)
         B = self.B = int(getattr(cfg, "block_words", 0) or 4096)
         doc, word = self._tokens
+        self.sparse = L.use_sparse(K, doc.numel())  # same choice on every worker
         mine = (doc % P) == me
         doc, word = doc[mine].to(dev), word[mine].to(dev)
         self.ndoc_local = (self.n_docs - me + P - 1) // P
@@ -217,9 +224,10 @@ class LDAPushPullMapper(LDACollectiveMapper):
         order = torch.argsort(lrow)
         self.tdoc = ldoc[order].contiguous()
         self.tword = lrow[order].to(torch.int32).contiguous()
-        self.chunk_idx = L.build_chunks(self.tword, cfg.max_chunk)
+        self.chunk_idx = L.build_chunks(self.tword, L.max_chunk(cfg.max_chunk, self.sparse))
         gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
+        self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local) if self.sparse else None
         maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
         self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(dev, maxlen), device=dev)
         slab = torch.zeros((len(self.need) * B, self.Kp), dtype=torch.int32, device=dev)
@@ -264,7 +272,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
         n = self.tz.numel()
         if n:
             d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, slab, self.nk,
-                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, (cfg.seed << 40) ^ (it << 20) ^ 0x5A)
+                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, (cfg.seed << 40) ^ (it << 20) ^ 0x5A,
+                             self.doc_index)
         else:
             d = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
         slab -= before

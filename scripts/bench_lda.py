@@ -21,11 +21,13 @@ def main():
     ap.add_argument("--len", type=int, default=100)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--max-chunk", type=int, default=0, help="tokens per word chunk (0: LDAConfig default)")
     ap.add_argument("--strategy", default="rotation", choices=["rotation", "push_pull"])
     a = ap.parse_args()
     import torch
 
     from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, LDAPushPullMapper, synthetic_corpus
+    from harp_amd.ops import lda as L
     from harp_amd.runtime.launcher import init_distributed, shutdown
     from harp_amd.runtime.mapper import KeyValReader
 
@@ -35,6 +37,8 @@ def main():
     toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
     gen = time.perf_counter() - t0
     cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters)
+    if a.max_chunk:
+        cfg.max_chunk = a.max_chunk
     cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper
     m = cls(comm, cfg, nd, V, toks)
     t0 = time.perf_counter()
@@ -65,7 +69,9 @@ def main():
         print(json.dumps({"metric": f"LDA-CGS sampled tokens/sec ({a.strategy})", "value": float(tot.item()) / dt,
                           "unit": "tokens/s", "s_per_iter": dt / a.iters, "n_gpus": comm.world_size,
                           "docs": nd, "vocab": V, "topics": a.topics, "tokens": int(tot.item()) // a.iters,
-                          "loglik_init": ll0, "loglik_end": ll, "init_s": init_s, "gen_s": gen}), flush=True)
+                          "sampler": "sparse" if m.doc_index is not None else "dense",
+                          "sparse_waves": L.SPARSE_WAVES, "max_chunk": L.max_chunk(cfg.max_chunk, m.sparse),
+                          "chunk_order": os.environ.get("HARP_LDA_ORDER", "lpt"), "loglik_init": ll0, "loglik_end": ll, "init_s": init_s, "gen_s": gen}), flush=True)
     shutdown()
 
 

@@ -69,3 +69,46 @@ def test_lda_push_pull(corpus, P):
                                 300, 400, corpus))[0]["loglik"][-1][1]
     # bulk-synchronous snapshot staleness costs a little at this tiny scale (12k tokens)
     assert abs(ll[-1] - rot) / abs(rot) < 0.08
+
+
+def test_doc_index_build_and_sync():
+    g = torch.Generator().manual_seed(0)
+    tdoc = torch.randint(0, 50, (2000,), generator=g, dtype=torch.int32)
+    tz = torch.randint(0, 3000, (2000,), generator=g, dtype=torch.int32)
+    di = L.DocIndex.build(tdoc, tz, 50)
+    assert int(di.doc_off[-1]) == 2000
+    cnt = torch.bincount(tdoc.long(), minlength=50)
+    assert torch.equal(di.doc_off[1:] - di.doc_off[:-1], cnt)
+    # token i sits inside its doc's range and carries its topic
+    assert bool((di.tpos >= di.doc_off[tdoc.long()]).all() and (di.tpos < di.doc_off[tdoc.long() + 1]).all())
+    assert torch.equal(di.zdoc[di.tpos].int(), tz)
+    tz2 = (tz + 7) % 3000
+    di.sync(tz2[100:300], di.tpos[100:300])
+    assert torch.equal(di.zdoc[di.tpos[100:300]].int(), tz2[100:300])
+    assert torch.equal(di.zdoc[di.tpos[:100]].int(), tz[:100])
+
+
+def test_padded_topics_large_k():
+    assert L.padded_topics(1000) == 1024
+    assert L.padded_topics(1025) == 1152 and L.padded_topics(10000) == 10112
+    if L.SAMPLER == "auto":
+        assert L.use_sparse(10000) and not L.use_sparse(1000) and L.use_sparse(1000, 10 ** 8)
+    with pytest.raises(NotImplementedError):
+        L.padded_topics(20000)
+
+
+def test_lda_large_k_cpu_rotation(corpus):
+    """K > 1024 (BASELINE #5 runs K = 10,000): the mapper keeps the doc-order topic view
+    in step with the assignments and the likelihood improves."""
+    from harp_amd.models.lda import LDACollectiveMapper
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    cfg = LDAConfig(num_topics=1500, alpha=0.05, beta=0.01, iterations=4, print_interval=2)
+    m = LDACollectiveMapper(Communicator(), cfg, 300, 400, corpus)
+    m.run(KeyValReader([]))
+    ll = [v for _, v in m.result["loglik"]]
+    assert ll[-1] > ll[0]
+    assert m.doc_index is not None
+    assert torch.equal(m.doc_index.zdoc[m.doc_index.tpos].int(), m.tz)
+    assert int(m.nk.sum()) == m.tz.numel()

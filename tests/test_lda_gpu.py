@@ -61,3 +61,73 @@ def test_packed16_doc_topic_counts_consistent(cuda, K):
     L.count(tdoc, tword, tz, re, None, None)
     assert torch.equal(a16.int() & 0xFFFF, re)
     assert int(d.sum()) == 0
+
+
+@pytest.mark.parametrize("K,forced", [(300, True), (2000, False)])
+def test_lda_sparse_sampler_matches_cpu_quality(cuda, K, forced, monkeypatch):
+    """The sparse-doc sampler (the K > 1024 path; forced at K = 300) improves the
+    likelihood nearly as much as the exact sequential CPU sampler. Its workgroup samples
+    8 tokens of one word at once; on this 120k-token corpus (40 tokens per word) that
+    staleness costs ~15% of the improvement, at the 1e8-token bench scale it is within
+    0.2% of the dense sampler (profiles/r1_lda/sparse)."""
+    from harp_amd.ops import lda as L
+
+    if forced:
+        monkeypatch.setattr(L, "SAMPLER", "sparse")
+    toks = synthetic_corpus(2000, 3000, 20, 60, seed=4)
+    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=12, print_interval=1)
+    g = run_lda(Communicator(None, cuda), cfg, 2000, 3000, toks)
+    c = run_lda(Communicator(None, torch.device("cpu")), cfg, 2000, 3000, toks)
+    gain_g = g["loglik"][-1][1] - g["loglik"][0][1]
+    gain_c = c["loglik"][-1][1] - c["loglik"][0][1]
+    assert gain_g > 0.75 * gain_c, (g["loglik"], c["loglik"])
+
+
+@pytest.mark.parametrize("K,bits,waves", [(100, 16, 8), (3000, 16, 8), (3000, 32, 4), (9000, 16, 16)])
+def test_sparse_sampler_counts_consistent(cuda, K, bits, waves, monkeypatch):
+    """After a sparse sweep every count table equals a recount of the new assignments and
+    the doc-order view matches them."""
+    from harp_amd.ops import lda as L
+
+    monkeypatch.setattr(L, "SPARSE_WAVES", waves)
+    g = torch.Generator(device=cuda).manual_seed(1)
+    nd, V, n = 700, 900, 60000
+    tdoc = torch.randint(0, nd, (n,), generator=g, device=cuda, dtype=torch.int32)
+    tword = torch.sort(torch.randint(0, V, (n,), generator=g, device=cuda, dtype=torch.int32)).values
+    tz = torch.randint(0, K, (n,), generator=g, device=cuda, dtype=torch.int32)
+    Kp = L.padded_topics(K)
+    ndk = torch.zeros((nd, Kp), dtype=torch.int16 if bits == 16 else torch.int32, device=cuda)
+    nwk = torch.zeros((V, Kp), dtype=torch.int32, device=cuda)
+    nk = torch.zeros(Kp, dtype=torch.int32, device=cuda)
+    L.count(tdoc, tword, tz, ndk, nwk, nk)
+    di = L.DocIndex.build(tdoc, tz, nd)
+    chunks = L.build_chunks(tword, 128)
+    z0 = tz.clone()
+    d = L.cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K, 0.1, 0.01, V * 0.01, 11, di)
+    torch.cuda.synchronize()
+    assert int(tz.min()) >= 0 and int(tz.max()) < K
+    assert (tz != z0).float().mean() > 0.2  # the sweep moved tokens
+    r_d = torch.zeros((nd, Kp), dtype=torch.int32, device=cuda)
+    r_w = torch.zeros_like(nwk)
+    r_k = torch.zeros_like(nk)
+    L.count(tdoc, tword, tz, r_d, r_w, r_k)
+    assert torch.equal(ndk.int() & 0xFFFF if bits == 16 else ndk, r_d)
+    assert torch.equal(nwk, r_w)
+    assert torch.equal(nk + d, r_k)
+    assert torch.equal(di.zdoc[di.tpos].int(), tz)
+
+
+@pytest.mark.parametrize("sampler,K", [("dense", 300), ("sparse", 300), ("sparse", 2000), ("sparse", 9000)])
+def test_sampler_conditional_is_exact(cuda, sampler, K):
+    """Independent probe tokens sharing one doc / word state: the histogram of their new
+    topics matches the exact collapsed-Gibbs conditional (chi-square within ~6 sigma)."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "lda_cond_diag", os.path.join(os.path.dirname(__file__), "..", "scripts", "lda_cond_diag.py"))
+    D = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(D)
+    r = D.run(K, 100000, sampler, 8, cuda)
+    assert r["chi2"] < r["df"] + 6 * (2 * r["df"]) ** 0.5 + 10, r
+    assert abs(r["p_doc_topics"] - r["exact_p_doc_topics"]) < 0.01, r
