@@ -626,9 +626,9 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
                                     float alpha, float beta, unsigned long long seed, int waves, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
   if (K <= 0 || K > 16384 || ldw < K || (ndk && ldd < K) || !tpos || !doc_off || !zdoc || !work) return HARP_EBADARG;
-  if (waves == 0) {  // auto: enough waves per workgroup to fill 32 wave slots per CU within the LDS budget
-    const long per_cu = 163840 / (4L * ((K + 63) / 64 * 64) + 1100);
-    waves = per_cu >= 8 ? 4 : per_cu >= 4 ? 8 : 16;
+  if (waves == 0) {  // auto: the smallest workgroup that still puts >= 24 waves on a CU
+    const long per_cu = 163840 / (4L * ((K + 63) / 64 * 64) + 1100);  // LDS-resident workgroups
+    waves = per_cu * 4 >= 24 ? 4 : per_cu * 8 >= 24 ? 8 : 16;
   }
 #define SP_ARGS tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc
 #define SP_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
