@@ -29,6 +29,8 @@
 //    comparison and for unblocked rating sets.
 #include "common.h"
 
+#include <climits>
+
 namespace {
 
 // Factor-row layout inside a 16-lane stream: lane sl holds the float4 chunks at
@@ -449,6 +451,215 @@ int launch_rmse(const int* rows, const int* cols, const float* vals, long n, con
   return harp_launch_status();
 }
 
+// ---- wide ranks (256 < R <= 4096, R % 4 == 0; BASELINE #1 runs rank 2000) -------------
+// ONE wave per update stream: lane l holds the float4 chunks at row + 4*l + 256*q (q < Q),
+// so each wave instruction covers one contiguous 1 KB row segment; chunks at or past R are
+// masked (no padding of the caller's rows needed). The row is too long for the 16-lane
+// streams of the narrow kernels (R / 16 floats per lane); the dot product is a full-wave
+// reduction. The next rating's H row is prefetched before this rating's H store (vmcnt
+// retires in order: the wait for the prefetch never covers the store).
+__device__ __forceinline__ float wave_sum_f(float v) {
+  v = sub16_sum(v);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+template <int Q, bool NT>
+__device__ __forceinline__ void load_wide(const float* __restrict__ p, int lane, int R, floatx4 (&x)[Q]) {
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = 4 * lane + 256 * q;
+    if (c < R) x[q] = NT ? __builtin_nontemporal_load((const floatx4*)(p + c)) : *(const floatx4*)(p + c);
+    else x[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <int Q>
+__device__ __forceinline__ void store_wide(float* __restrict__ p, int lane, int R, const floatx4 (&x)[Q]) {
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = 4 * lane + 256 * q;
+    if (c < R) *(floatx4*)(p + c) = x[q];
+  }
+}
+
+// ratings i0 .. i1 - 1 of the stream; rating i sits at index a + ((w0 + i) mod ncell)
+// (the window wrap of the blocked schedule; a flat stream passes w0 = 0, ncell = huge)
+template <int Q>
+__device__ __forceinline__ void sgd_stream_wide(const int* __restrict__ rows, const int* __restrict__ cols,
+                                                const float* __restrict__ vals, long a, long w0, long ncell, long i0,
+                                                long i1, int lane, int R, float* __restrict__ W, long ldw,
+                                                float* __restrict__ H, long ldh, float lr, float lam) {
+  const float decay = 1.0f - lr * lam;
+  auto at = [&](long i) {
+    long q = w0 + i;
+    if (q >= ncell) q -= ncell;
+    return a + q;
+  };
+  floatx4 w[Q], h[Q], hn[Q];
+  long k = at(i0);
+  int cur = rows[k], col = cols[k];
+  load_wide<Q, false>(W + cur * ldw, lane, R, w);
+  load_wide<Q, true>(H + col * ldh, lane, R, h);
+  for (long i = i0; i < i1; ++i) {
+    const float v = vals[k];
+    const bool more = i + 1 < i1;
+    int nrow = cur, ncol = col;
+    if (more) {
+      k = at(i + 1);
+      nrow = rows[k];
+      ncol = cols[k];
+      if (ncol != col) load_wide<Q, true>(H + ncol * ldh, lane, R, hn);
+    }
+    float d = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      d = fmaf(w[q][0], h[q][0], d);
+      d = fmaf(w[q][1], h[q][1], d);
+      d = fmaf(w[q][2], h[q][2], d);
+      d = fmaf(w[q][3], h[q][3], d);
+    }
+    const float ge = -lr * (wave_sum_f(d) - v);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const floatx4 wk = w[q], hk = h[q];
+      w[q] = ge * hk + decay * wk;
+      h[q] = ge * wk + decay * hk;
+    }
+    store_wide<Q>(H + col * ldh, lane, R, h);
+    if (!more) break;
+    if (nrow != cur) {
+      store_wide<Q>(W + cur * ldw, lane, R, w);
+      cur = nrow;
+      load_wide<Q, false>(W + cur * ldw, lane, R, w);
+    }
+    if (ncol != col) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) h[q] = hn[q];
+      col = ncol;
+    }
+  }
+  store_wide<Q>(W + cur * ldw, lane, R, w);
+}
+
+// flat: wave g runs ratings [g*chunk, (g+1)*chunk)
+template <int Q>
+__global__ __launch_bounds__(256) void mf_sgd_wide_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
+                                                          const float* __restrict__ vals, long n, int chunk, int R,
+                                                          float* __restrict__ W, int ldw, float* __restrict__ H,
+                                                          int ldh, float lr, float lam) {
+  const long g = __builtin_amdgcn_readfirstlane(((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const long i0 = g * (long)chunk;
+  long i1 = i0 + chunk;
+  if (i1 > n) i1 = n;
+  if (i0 >= i1) return;
+  sgd_stream_wide<Q>(rows, cols, vals, 0, 0, LONG_MAX, i0, i1, threadIdx.x & 63, R, W, ldw, H, ldh, lr, lam);
+}
+
+// XCD-blocked sub-step (same cell schedule and windows as mf_sgd_xcd_kernel): the 4 waves
+// of a block take consecutive streams of CH ratings of the XCD's cell
+template <int Q, int CH>
+__global__ __launch_bounds__(256) void mf_sgd_xcd_wide_kernel(const int* __restrict__ rows,
+                                                              const int* __restrict__ cols,
+                                                              const float* __restrict__ vals,
+                                                              const long* __restrict__ off,
+                                                              const long* __restrict__ win, int step, int R,
+                                                              float* __restrict__ W, int ldw, float* __restrict__ H,
+                                                              int ldh, float lr, float lam) {
+  const int x = blockIdx.x % XCDS;
+  const long j = blockIdx.x / XCDS;
+  const long per_xcd = gridDim.x / XCDS;
+  const int cell = x * XCDS + (x + step) % XCDS;
+  const long a = off[cell];
+  const long ncell = off[cell + 1] - a;
+  const long w0 = win ? win[cell] : 0;
+  const long n = win ? win[XCDS * XCDS + cell] : ncell;
+  const long nst = (n + CH - 1) / CH;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (long st = j * 4 + wv; st < nst; st += per_xcd * 4) {
+    const long i0 = st * CH;
+    const long i1 = i0 + CH < n ? i0 + CH : n;
+    sgd_stream_wide<Q>(rows, cols, vals, a, w0, ncell, i0, i1, threadIdx.x & 63, R, W, ldw, H, ldh, lr, lam);
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(256) void mf_rmse_wide_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
+                                                           const float* __restrict__ vals, long n, int R,
+                                                           const float* __restrict__ W, int ldw,
+                                                           const float* __restrict__ H, int ldh,
+                                                           double* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  double acc = 0.0;
+  for (long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
+    floatx4 w[Q], h[Q];
+    load_wide<Q, false>(W + (long)rows[i] * ldw, lane, R, w);
+    load_wide<Q, false>(H + (long)cols[i] * ldh, lane, R, h);
+    float d = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      d += w[q][0] * h[q][0] + w[q][1] * h[q][1] + w[q][2] * h[q][2] + w[q][3] * h[q][3];
+    const float e = vals[i] - wave_sum_f(d);
+    acc += (double)e * e;
+  }
+  double s = lane == 0 ? acc : 0.0;
+  s = wave_sum_d(s);
+  __shared__ double red[4];
+  if (lane == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+int wide_q(int r) { return r <= 512 ? 2 : r <= 1024 ? 4 : r <= 2048 ? 8 : 16; }
+bool wide_ok(int r) { return r > 256 && r <= 4096 && r % 4 == 0; }
+
+#define WIDE_DISPATCH(R, CALL)                                                          \
+  switch (wide_q(R)) {                                                                  \
+    case 2: return CALL(2);                                                             \
+    case 4: return CALL(4);                                                             \
+    case 8: return CALL(8);                                                             \
+    default: return CALL(16);                                                           \
+  }
+
+template <int Q>
+int launch_sgd_wide(const int* rows, const int* cols, const float* vals, long n, int chunk, int r, float* W, int ldw,
+                    float* H, int ldh, float lr, float lam, hipStream_t s) {
+  const long streams = (n + chunk - 1) / chunk;
+  const long blocks = (streams + 3) / 4;
+  mf_sgd_wide_kernel<Q><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(rows, cols, vals, n, chunk, r, W, ldw, H, ldh,
+                                                                      lr, lam);
+  return harp_launch_status();
+}
+
+template <int Q>
+int launch_sgd_xcd_wide(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
+                        int steps, int chunk, int blocks_per_xcd, int r, float* W, int ldw, float* H, int ldh,
+                        float lr, float lam, hipStream_t s) {
+  for (int step = 0; step < steps; ++step) {
+    if (chunk == 32)
+      mf_sgd_xcd_wide_kernel<Q, 32><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam);
+    else if (chunk == 128)
+      mf_sgd_xcd_wide_kernel<Q, 128><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam);
+    else
+      mf_sgd_xcd_wide_kernel<Q, 64><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam);
+    const int st = harp_launch_status();
+    if (st != HARP_OK) return st;
+  }
+  return HARP_OK;
+}
+
+template <int Q>
+int launch_rmse_wide(const int* rows, const int* cols, const float* vals, long n, int r, const float* W, int ldw,
+                     const float* H, int ldh, double* partial, int nblocks, hipStream_t s) {
+  mf_rmse_wide_kernel<Q><<<dim3(nblocks), dim3(256), 0, s>>>(rows, cols, vals, n, r, W, ldw, H, ldh, partial);
+  return harp_launch_status();
+}
+
 }  // namespace
 
 #define MF_DISPATCH(R, CALL)          \
@@ -466,6 +677,11 @@ HARP_EXPORT int harp_mf_sgd(const int* rows, const int* cols, const float* vals,
                             int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
   if (n <= 0) return HARP_OK;
   if (chunk <= 0 || ldw < r || ldh < r) return HARP_EBADARG;
+  if (wide_ok(r)) {
+#define SGDW_CALL(QQ) launch_sgd_wide<QQ>(rows, cols, vals, n, chunk, r, W, ldw, H, ldh, lr, lam, s)
+    WIDE_DISPATCH(r, SGDW_CALL)
+#undef SGDW_CALL
+  }
 #define SGD_CALL(RR) launch_sgd<RR>(rows, cols, vals, n, chunk, W, ldw, H, ldh, lr, lam, s)
   MF_DISPATCH(r, SGD_CALL)
 #undef SGD_CALL
@@ -484,6 +700,13 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
                                 float* H, int ldh, float lr, float lam, hipStream_t s) {
   if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant < 0 || variant > 4)
     return HARP_EBADARG;
+  if (wide_ok(r)) {  // wide ranks: one wave per stream, variants do not apply
+    if (chunk != 32 && chunk != 64 && chunk != 128) return HARP_EBADARG;
+#define SGDXW_CALL(QQ) \
+  launch_sgd_xcd_wide<QQ>(rows, cols, vals, off, win, steps, chunk, blocks_per_xcd, r, W, ldw, H, ldh, lr, lam, s)
+    WIDE_DISPATCH(r, SGDXW_CALL)
+#undef SGDXW_CALL
+  }
 #define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
 #define SGDX_CALL(RR)                                                                          \
   (variant == 1 ? (chunk == 64 ? launch_sgd_xcd<RR, 64, true>(SGDX_ARGS) : HARP_EBADARG)            \
@@ -505,6 +728,11 @@ HARP_EXPORT int harp_mf_rmse_blocks() { return 1024; }
 HARP_EXPORT int harp_mf_rmse(const int* rows, const int* cols, const float* vals, long n, int r, const float* W, int ldw,
                              const float* H, int ldh, double* partial, hipStream_t s) {
   if (n <= 0) return HARP_OK;
+  if (wide_ok(r)) {
+#define RMSEW_CALL(QQ) launch_rmse_wide<QQ>(rows, cols, vals, n, r, W, ldw, H, ldh, partial, 1024, s)
+    WIDE_DISPATCH(r, RMSEW_CALL)
+#undef RMSEW_CALL
+  }
 #define RMSE_CALL(RR) launch_rmse<RR>(rows, cols, vals, n, W, ldw, H, ldh, partial, 1024, s)
   MF_DISPATCH(r, RMSE_CALL)
 #undef RMSE_CALL

@@ -15,7 +15,18 @@ import torch
 
 from . import _lib
 
-SUPPORTED_RANKS = (16, 32, 48, 64, 128, 256)
+SUPPORTED_RANKS = (16, 32, 48, 64, 128, 256)  # 16-lane stream kernels
+MAX_WIDE_RANK = 4096  # wave-per-stream kernels: 256 < r <= 4096, r % 4 == 0 (BASELINE #1: rank 2000)
+
+
+def supported_rank(r: int) -> bool:
+    return r in SUPPORTED_RANKS or (256 < r <= MAX_WIDE_RANK and r % 4 == 0)
+
+
+def _require_rank(r: int) -> None:
+    if not supported_rank(r):
+        raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS} and multiples of 4 in "
+                                  f"(256, {MAX_WIDE_RANK}], got {r}")
 
 _lib.register({
     "harp_mf_sgd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
@@ -62,8 +73,7 @@ def sgd_update(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: to
         return 0
     r = W.shape[1]
     if _lib.use_native(W):
-        if r not in SUPPORTED_RANKS:
-            raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS}, got {r}")
+        _require_rank(r)
         st = _lib.kernels().harp_mf_sgd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, chunk, W.data_ptr(),
                                         W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam),
                                         _lib.stream_ptr(W.device))
@@ -120,8 +130,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     assert cell_off.numel() == nb * nb + 1 and cell_off.dtype == torch.int64
     trained = n if window is None else int(sum(window[1]))
     if _lib.use_native(W):
-        if r not in SUPPORTED_RANKS:
-            raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS}, got {r}")
+        _require_rank(r)
         assert cell_off.device == W.device and cell_off.is_contiguous()
         win = None
         if window is not None:

@@ -73,7 +73,7 @@ def main():
         n, dt = float(n_all.item()), float(t_all.item())
     tr, _ = m._eval_ring(a.warmup + a.epochs - 1)
     if comm.rank == 0:
-        print(json.dumps({"metric": "MF-SGD updates/sec (Netflix-shape synthetic, rank 128, model rotation)",
+        print(json.dumps({"metric": f"MF-SGD updates/sec (Netflix-shape synthetic, rank {a.rank}, model rotation)",
                           "value": n / dt, "unit": "updates/s", "n_gpus": comm.world_size, "epochs": a.epochs,
                           "s_per_epoch": dt / a.epochs, "train_rmse": tr, "data_gen_s": gen_s,
                           "ratings": a.ratings, "rank": a.rank, "dtype": "fp32 factors",

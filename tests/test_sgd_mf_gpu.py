@@ -118,3 +118,66 @@ def test_sgd_xcd_windows_match_cpu(cuda):
     torch.cuda.synchronize()
     assert nc == ng == sum(win[1])
     assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
+
+
+# ---- wide ranks (wave-per-stream kernels; BASELINE #1 trains rank 2000) ----
+
+@pytest.mark.parametrize("r", [260, 1000, 2000, 3000])
+def test_sse_wide_rank_matches_torch(cuda, r):
+    n, nu, ni = 20000, 500, 300
+    g = torch.Generator().manual_seed(r)
+    rows = torch.randint(0, nu, (n,), generator=g, dtype=torch.int32)
+    cols = torch.randint(0, ni, (n,), generator=g, dtype=torch.int32)
+    vals = torch.rand(n, generator=g) * 4 + 1
+    s = 0.3 * (16.0 / r) ** 0.5
+    W = torch.rand(nu, r, generator=g) * s
+    H = torch.rand(ni, r, generator=g) * s
+    ref = ((vals.double() - (W[rows.long()].double() * H[cols.long()].double()).sum(1)) ** 2).sum()
+    got = MF.sse(rows.to(cuda), cols.to(cuda), vals.to(cuda), W.to(cuda), H.to(cuda))
+    assert abs(got.item() - ref.item()) <= 1e-5 * ref.item()
+
+
+@pytest.mark.parametrize("r", [512, 2000])
+def test_sgd_wide_single_stream_matches_sequential(cuda, r):
+    n, nu, ni = 2000, 40, 30
+    g = torch.Generator().manual_seed(0)
+    rows = torch.sort(torch.randint(0, nu, (n,), generator=g, dtype=torch.int32)).values
+    cols = torch.randint(0, ni, (n,), generator=g, dtype=torch.int32)
+    vals = torch.rand(n, generator=g) * 4 + 1
+    s = 0.3 * (16.0 / r) ** 0.5
+    W0 = torch.rand(nu, r, generator=g) * s
+    H0 = torch.rand(ni, r, generator=g) * s
+    Wc, Hc = W0.clone(), H0.clone()
+    MF.sgd_update(rows, cols, vals, Wc, Hc, 0.002, 0.05)
+    Wg, Hg = W0.to(cuda), H0.to(cuda)
+    MF.sgd_update(rows.to(cuda), cols.to(cuda), vals.to(cuda), Wg, Hg, 0.002, 0.05, chunk=n)
+    assert torch.allclose(Wg.cpu(), Wc, atol=2e-5, rtol=1e-4) and torch.allclose(Hg.cpu(), Hc, atol=2e-5, rtol=1e-4)
+
+
+def test_sgd_wide_xcd_one_stream_per_cell_matches_cpu(cuda):
+    """Rank 2000 through the XCD-blocked schedule, one stream per cell: equals the CPU
+    schedule; strided rows (a view of a wider buffer) are honoured."""
+    r = 2000
+    R, C, V, off, W0, H0 = _cells(64, 48, 4000, r, 1)
+    W0 *= (16.0 / r) ** 0.5
+    H0 *= (16.0 / r) ** 0.5
+    assert int((off[1:] - off[:-1]).max()) <= 128
+    Wc, Hc = W0.clone(), H0.clone()
+    MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.002, 0.05)
+    Wbuf = torch.zeros(64, r + 48, device=cuda)
+    Wg = Wbuf[:, :r]
+    Wg.copy_(W0)
+    Hg = H0.to(cuda)
+    MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.002, 0.05, chunk=128)
+    torch.cuda.synchronize()
+    assert torch.allclose(Wg.cpu(), Wc, atol=2e-5, rtol=1e-4) and torch.allclose(Hg.cpu(), Hc, atol=2e-5, rtol=1e-4)
+    assert bool((Wbuf[:, r:] == 0).all())  # nothing written past the rank
+
+
+def test_sgd_wide_rank_model_converges(cuda):
+    nu, ni = 2000, 600
+    u, i, v = synthetic_ratings(nu, ni, 80000, seed=5)
+    cfg = SGDConfig(rank=1000, lam=0.05, lr=0.002, epochs=6, test_every=3)
+    res = run_sgd(Communicator(None, cuda), cfg, nu, ni, (u, i, v), (u[:5000], i[:5000], v[:5000]))
+    rm = [x[2] for x in res["rmse"]]
+    assert rm[-1] < rm[0], res["rmse"]
