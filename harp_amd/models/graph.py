@@ -191,22 +191,55 @@ def _neighbour_sum(comm: Communicator, adj_src_local: torch.Tensor, adj_dst: tor
     return out
 
 
+class GraphShard:
+    """One worker's share of the graph for the color-coding DP, built once per graph:
+    owned vertices v % P == rank, their (local source, global neighbour) edges and, where
+    the neighbour table is one contiguous array (P == 1, or the all-gather strategy), a
+    CSR over it for the native fp64 SpMM (``ops/graph.py``)."""
+
+    def __init__(self, comm: Communicator, src: torch.Tensor, dst: torch.Tensor, n_vertices: int,
+                 strategy: str = "allgather"):
+        from ..ops import graph as G
+
+        P, me, dev = comm.world_size, comm.rank, comm.device
+        self.own = torch.arange(me, n_vertices, P, device=dev)
+        self.n_local = self.own.numel()
+        src, dst = src.to(dev), dst.to(dev)
+        keep = (src % P) == me
+        self.s_loc, self.d_glob = src[keep] // P, dst[keep]
+        self.csr = None
+        if P == 1 or strategy == "allgather":
+            if P == 1:
+                row = self.d_glob
+            else:  # row of neighbour u in the all-gathered table (rank-major blocks)
+                counts = [len(range(r, n_vertices, P)) for r in range(P)]
+                offs = torch.tensor([0] + list(itertools.accumulate(counts))[:-1], device=dev)
+                row = offs[self.d_glob % P] + self.d_glob // P
+            self.csr = G.build_csr(self.s_loc, row, self.n_local)
+
+
 def color_count(comm: Communicator, template: Template, src: torch.Tensor, dst: torch.Tensor, n_vertices: int,
-                colors: torch.Tensor, strategy: str = "allgather") -> float:
+                colors: torch.Tensor, strategy: str = "allgather", shard: Optional[GraphShard] = None) -> float:
     """Number of colorful embeddings (maps T -> G with all k colors distinct) for the
     given coloring. Each worker owns vertices v with v % P == rank and passes the edges
-    (both directions) whose source it owns."""
-    P, me, dev = comm.world_size, comm.rank, comm.device
+    (both directions) whose source it owns (or a prebuilt ``shard``)."""
+    from ..ops import graph as G
+
+    P, dev = comm.world_size, comm.device
     k = template.k
-    own = torch.arange(me, n_vertices, P, device=dev)
-    n_local = own.numel()
-    src, dst = src.to(dev), dst.to(dev)
-    keep = (src % P) == me
-    s_loc, d_glob = src[keep] // P, dst[keep]
-    my_col = colors.to(dev)[own]
+    if shard is None:
+        shard = GraphShard(comm, src, dst, n_vertices, strategy)
+    n_local = shard.n_local
+    my_col = colors.to(dev)[shard.own]
     base = torch.zeros((n_local, k), dtype=torch.float64, device=dev)
     base[torch.arange(n_local, device=dev), my_col] = 1.0  # size-1 sets are {c} -> index c
     memo: Dict[Tuple[int, int], torch.Tensor] = {}
+
+    def neighbour_sum(Pm: torch.Tensor) -> torch.Tensor:
+        if shard.csr is not None:
+            full = Pm if P == 1 else gather_rows(comm, Pm)
+            return G.spmm(shard.csr, full.contiguous())
+        return _neighbour_sum(comm, shard.s_loc, shard.d_glob, n_local, Pm, shard.own, n_vertices, strategy)
 
     def table(v: int, j: int) -> torch.Tensor:
         key = (v, j)
@@ -219,15 +252,10 @@ def color_count(comm: Communicator, template: Template, src: torch.Tensor, dst: 
         A = table(v, j - 1)
         Pm = table(c, len(template.children[c]))
         sa, sp = template.size(v, j - 1), template.size(c)
-        Np = _neighbour_sum(comm, s_loc, d_glob, n_local, Pm, own, n_vertices, strategy)
-        tc, t1, t2 = (t.to(dev) for t in _split_index(k, sa, sp))
-        out = torch.zeros((n_local, len(_colorsets(k, sa + sp)[0])), dtype=torch.float64, device=dev)
-        step = max(1, (1 << 24) // max(1, tc.numel()))
-        for a in range(0, n_local, step):
-            b = min(n_local, a + step)
-            out[a:b].index_add_(1, tc, A[a:b, t1] * Np[a:b, t2])
-        memo[key] = out
-        return out
+        Np = neighbour_sum(Pm)
+        tc, t1, t2 = _split_index(k, sa, sp)
+        memo[key] = G.combine(A, Np, tc, t1, t2, len(_colorsets(k, sa + sp)[0]))
+        return memo[key]
 
     full = table(0, len(template.children[0]))
     tot = full.sum().reshape(1)
@@ -248,9 +276,10 @@ def count_subgraphs(comm: Communicator, template: Template, src: torch.Tensor, d
     scale = k ** k / math.factorial(k) / template.automorphisms()
     vals = []
     t0 = time.perf_counter()
+    shard = GraphShard(comm, src, dst, n_vertices, strategy)
     for _ in range(iterations):
         colors = torch.randint(0, k, (n_vertices,), generator=g)
-        vals.append(color_count(comm, template, src, dst, n_vertices, colors, strategy) * scale)
+        vals.append(color_count(comm, template, src, dst, n_vertices, colors, strategy, shard) * scale)
     return {"estimate": sum(vals) / len(vals), "samples": vals, "time_s": time.perf_counter() - t0}
 
 
