@@ -112,3 +112,24 @@ def test_lda_large_k_cpu_rotation(corpus):
     assert m.doc_index is not None
     assert torch.equal(m.doc_index.zdoc[m.doc_index.tpos].int(), m.tz)
     assert int(m.nk.sum()) == m.tz.numel()
+
+
+def _large_k_job(comm, cfg, nd, V, toks):
+    from harp_amd.models.lda import LDACollectiveMapper
+    from harp_amd.runtime.mapper import KeyValReader
+
+    m = LDACollectiveMapper(comm, cfg, nd, V, toks)
+    m.run(KeyValReader([]))
+    ok = bool(torch.equal(m.doc_index.zdoc[m.doc_index.tpos].int(), m.tz))
+    return m.result, ok, int(m.nk.sum()), m.sparse
+
+
+def test_lda_large_k_rotation_two_workers(corpus):
+    """K > 1024 under model rotation on 2 workers: the sparse-sampler bookkeeping (doc-order
+    view per worker, chunk orders per slice) stays consistent across slice rotations."""
+    cfg = LDAConfig(num_topics=1100, alpha=0.05, beta=0.01, iterations=4, print_interval=2)
+    res = launch(_large_k_job, 2, args=(cfg, 300, 400, corpus), timeout=300)
+    for r, ok, tot, sparse in res:
+        assert ok and sparse and tot == corpus[0].numel()
+    ll = [v for _, v in res[0][0]["loglik"]]
+    assert ll[-1] > ll[0] and res[1][0]["loglik"] == res[0][0]["loglik"]
