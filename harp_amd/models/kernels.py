@@ -64,7 +64,18 @@ def rbf_kernel(X, Y, sigma: float = 1.0) -> torch.Tensor:
 
 # ---------------------------------------------------------------- kNN
 def knn_search(train: torch.Tensor, queries: torch.Tensor, k: int, tile: int = 8192) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Exact k nearest training rows of each query: (sq distances [M, k], indices [M, k])."""
+    """Exact k nearest training rows of each query: (sq distances [M, k], indices [M, k]).
+
+    Dense fp32 rows on a HIP device go through the fused GEMM + top-k selection kernel
+    (``ops/knn.py``, ``csrc/knn.hip``); sparse / other-dtype / CPU inputs use the torch
+    expression below."""
+    from ..ops import knn as knn_ops
+
+    dense = not (train.is_sparse or queries.is_sparse or train.layout == torch.sparse_csr
+                 or queries.layout == torch.sparse_csr)
+    if (dense and queries.device.type == "cuda" and train.dtype == torch.float32
+            and queries.dtype == torch.float32 and min(k, train.shape[0]) <= knn_ops.MAX_NATIVE_K):
+        return knn_ops.knn_search(train, queries, k)
     n = train.shape[0]
     k = min(k, n)
     tn = _sqnorm(train)
