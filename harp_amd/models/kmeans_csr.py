@@ -91,6 +91,19 @@ def kmeans_sparse(X, C0: torch.Tensor, iterations: int = 10, comm: Optional[Comm
     C = C0.to(device=X.device, dtype=torch.float64, copy=True)
     K, d = C.shape
     obj = []
+    if _is_sparse(X) and X.device.type == "cuda":
+        # fused HIP E-step + accumulate (csrc/kmeans_csr.hip): no [n, K] tensors
+        from ..ops import kmeans_csr as KC
+
+        A = KC.to_device_csr(X)
+        for _ in range(iterations):
+            lab, m, S, cnt = KC.assign_accumulate(A, C)
+            r = reduce_partials(comm, {"S": S, "n": cnt, "o": m.sum().reshape(1)})
+            cnt = r["n"].to(C.device)
+            nz = cnt > 0
+            C[nz] = r["S"].to(C.device)[nz] / cnt[nz, None]
+            obj.append(float(r["o"][0]))
+        return {"centroids": C, "objective": obj, "labels": lab}
     for _ in range(iterations):
         D = sq_dist(X, C)
         m, lab = D.min(1)
