@@ -75,8 +75,34 @@ class CSRRows:
         return CSRRows(self.crow.to(device), self.col.to(device), self.val.to(device), self.ncols)
 
 
+    def kernel_operands(self):
+        """(crow int64, col int32, val fp64) for ``csrc/mlr.hip``, built once per device."""
+        ops = getattr(self, "_kops", None)
+        if ops is None:
+            ops = (self.crow.contiguous(), self.col.to(torch.int32).contiguous(),
+                   self.val.to(torch.float64).contiguous())
+            self._kops = ops
+        return ops
+
+
 def _sgd_pass(W: torch.Tensor, X: CSRRows, Y: torch.Tensor, alpha: float, batch: int) -> None:
-    """One pass of the GDtask update over the local rows; W [T, D+1], bias in column 0."""
+    """One pass of the GDtask update over the local rows; W [T, D+1], bias in column 0.
+
+    HIP tensors: the whole pass is one launch of ``csrc/mlr.hip`` (one workgroup per
+    topic chain); CPU: the mini-batch torch expression below (its numerics oracle)."""
+    from ..ops import _lib
+
+    if W.device.type == "cuda" and W.dtype == torch.float64 and batch <= 1024:
+        from ..ops import mlr as mlr_ops
+
+        mlr_ops.sgd_pass(W, *X.kernel_operands(), X.nrows, Y, alpha, batch)
+        return
+    if W.device.type == "cuda":
+        _lib.kernels()
+    _sgd_pass_torch(W, X, Y, alpha, batch)
+
+
+def _sgd_pass_torch(W: torch.Tensor, X: CSRRows, Y: torch.Tensor, alpha: float, batch: int) -> None:
     n = X.nrows
     for a in range(0, n, batch):
         b = min(n, a + batch)
