@@ -16,7 +16,10 @@ MI355X design: every per-row-block kernel is GEMM-shaped — pairwise distances 
 local row block against all of X are one GEMM with the norm epilogue, B(Z) X is one
 GEMM, V p is one GEMM (V = diag(W 1) - W built on the fly from the resident weight
 block; no V file needed); X / p all-gathers and scalar allreduces are the only
-communication, exactly the reference's pattern but with bulk collectives.
+communication, exactly the reference's pattern but with bulk collectives. On a HIP
+device B(Z) X and the stress are single fused passes over the fp64 row blocks
+(``csrc/mds.hip``: the embedding dimension is 2..4, so distances come straight from the
+coordinates and B is never materialised).
 """
 from __future__ import annotations
 
@@ -62,8 +65,19 @@ class _Rows:
             return v
         return reduce_partials(self.comm, {"v": v.reshape(-1)})["v"].reshape(v.shape).to(v.dtype)
 
+    def _native(self, X) -> bool:
+        if self.D.device.type != "cuda":
+            return False
+        from ..ops import mds as mds_ops
+
+        return X.shape[1] <= mds_ops.MAX_DIM and self.D.stride() == self.W.stride() and self.D.stride(1) == 1
+
     def stress(self, X, T, d):
         diff = math.sqrt(2.0 * d) * T if T > 1e-9 else 0.0
+        if self._native(X):  # one fused pass (csrc/mds.hip)
+            from ..ops import mds as mds_ops
+
+            return mds_ops.stress_rows(self.D, self.W, self.row0, X, diff).sum()
         Dz = _dist_block(X[self.row0:self.row0 + self.n_r], X)
         Dz[torch.arange(self.n_r), self.diag] = 0
         m = (self.W != 0) & (self.D >= diff)
@@ -72,6 +86,10 @@ class _Rows:
 
     def bc(self, X, T, d):
         diff = math.sqrt(2.0 * d) * T if T > 1e-9 else 0.0
+        if self._native(X):  # B(Z) X without materialising B (csrc/mds.hip)
+            from ..ops import mds as mds_ops
+
+            return mds_ops.bc_rows(self.D, self.W, self.row0, X, diff)
         Dz = _dist_block(X[self.row0:self.row0 + self.n_r], X)
         ok = (self.W != 0) & (Dz >= 1e-10) & (self.D > diff)
         B = torch.where(ok, -self.W * (self.D - diff) / Dz.clamp_min(1e-10), torch.zeros_like(Dz))
