@@ -76,6 +76,46 @@ __global__ __launch_bounds__(256) void colorset_combine_kernel(const double* __r
   }
 }
 
+
+// PageRank pull step (contrib simplepagerank: PageRankMapper.java accumulates
+// pr(u) / outdeg(u) into every out-neighbour; here the edges are grouped by target once,
+// so an iteration is a CSR gather with no atomics):
+//   out[v] = alpha * sum_{u in in(v)} x[u] + b0 + b1 * (*dm)
+//   xnext[v] = out[v] * invdeg[v]   (v < nx; optional: fuses the next iteration's x)
+// G lanes per row (G = in-degree rounded to a power of two, 4..64), 64 / G rows per
+// wave, so short web-graph rows do not leave most of a wave idle.
+template <int G>
+__global__ __launch_bounds__(256) void pagerank_pull_kernel(const long* __restrict__ rowptr,
+                                                            const int* __restrict__ col,
+                                                            const double* __restrict__ x, double alpha, double b0,
+                                                            double b1, const double* __restrict__ dm,
+                                                            double* __restrict__ out,
+                                                            const double* __restrict__ invdeg,
+                                                            double* __restrict__ xnext, long nx, long n) {
+  const int sub = threadIdx.x & (G - 1);
+  const double beta = b0 + (dm ? b1 * dm[0] : 0.0);
+  const long ng = ((long)gridDim.x * blockDim.x) / G;
+  for (long v = ((long)blockIdx.x * blockDim.x + threadIdx.x) / G; v < n; v += ng) {
+    const long a = rowptr[v], b = rowptr[v + 1];
+    double acc = 0.0, acc1 = 0.0;
+    long j = a + sub;
+    for (; j + G < b; j += 2 * G) {
+      const int u0 = col[j], u1 = col[j + G];
+      acc += x[u0];
+      acc1 += x[u1];
+    }
+    if (j < b) acc += x[col[j]];
+    acc += acc1;
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (sub == 0) {
+      const double r = alpha * acc + beta;
+      out[v] = r;
+      if (xnext && v < nx) xnext[v] = r * invdeg[v];
+    }
+  }
+}
+
 }  // namespace
 
 // out[v, :] = sum of M[col[j], :] over j in [rowptr[v], rowptr[v+1]); M and out are
@@ -108,5 +148,27 @@ HARP_EXPORT int harp_colorset_combine_f64(const double* A, int ca, const double*
   long blocks = (n * co + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   colorset_combine_kernel<<<dim3((unsigned)blocks), dim3(256), lds, s>>>(A, ca, Nn, cn, toff, t1, t2, co, nt, out, n);
+  return harp_launch_status();
+}
+
+// one PageRank pull step over a by-target CSR (see pagerank_pull_kernel); dm, invdeg and
+// xnext may be null
+HARP_EXPORT int harp_pagerank_pull_f64(const long* rowptr, const int* col, const double* x, double alpha, double b0,
+                                       double b1, const double* dm, double* out, const double* invdeg, double* xnext,
+                                       long nx, long n, long nnz, hipStream_t s) {
+  if (n <= 0) return HARP_OK;
+  if (xnext && !invdeg) return HARP_EBADARG;
+  const long avg = nnz / n;
+  const dim3 b(256);
+  auto grid = [&](int G) {
+    long blocks = (n * G + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    return dim3((unsigned)blocks);
+  };
+  if (avg <= 4) pagerank_pull_kernel<4><<<grid(4), b, 0, s>>>(rowptr, col, x, alpha, b0, b1, dm, out, invdeg, xnext, nx, n);
+  else if (avg <= 8) pagerank_pull_kernel<8><<<grid(8), b, 0, s>>>(rowptr, col, x, alpha, b0, b1, dm, out, invdeg, xnext, nx, n);
+  else if (avg <= 16) pagerank_pull_kernel<16><<<grid(16), b, 0, s>>>(rowptr, col, x, alpha, b0, b1, dm, out, invdeg, xnext, nx, n);
+  else if (avg <= 32) pagerank_pull_kernel<32><<<grid(32), b, 0, s>>>(rowptr, col, x, alpha, b0, b1, dm, out, invdeg, xnext, nx, n);
+  else pagerank_pull_kernel<64><<<grid(64), b, 0, s>>>(rowptr, col, x, alpha, b0, b1, dm, out, invdeg, xnext, nx, n);
   return harp_launch_status();
 }

@@ -14,8 +14,11 @@ References:
     rotate around the ring instead).
 
 MI355X design:
-  * PageRank: edges stay source-partitioned; a step is one scatter-add SpMV into a dense
-    length-N vector plus the dangling mass, then ONE reduce-scatter (each worker
+  * PageRank: edges stay source-partitioned but are grouped by target once into a CSR,
+    so a step is one gather SpMV (``csrc/graph.hip`` pagerank_pull_kernel: a power-of-two
+    lane group per target row, no fp64 atomics; on one worker it also applies damping,
+    the dangling mass and the next step's PR / outdeg in the same pass) into a dense
+    length-N vector, then ONE reduce-scatter (each worker
     finalises its slice of pages) and ONE all-gather — half the bytes of the
     reference's allreduce of a KV table, and no hashing.
   * Color coding: count tables are dense [n_vertices, C(k, s)] fp64 matrices (color sets
@@ -38,6 +41,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..parallel.comm import Communicator
+from ..ops import graph as GO
 from .common import gather_rows
 
 
@@ -65,26 +69,31 @@ def pagerank(comm: Communicator, src: torch.Tensor, dst: torch.Tensor, nodes: to
     on every worker."""
     P, me, dev = comm.world_size, comm.rank, comm.device
     N = num_urls
-    src, dst, nodes = src.to(dev), dst.to(dev), nodes.to(dev)
-    outdeg = torch.zeros(N, dtype=torch.float64, device=dev)
-    outdeg.index_add_(0, src, torch.ones(src.numel(), dtype=torch.float64, device=dev))
-    dangling = nodes[outdeg[nodes] == 0]
-    pr = torch.full((N,), 1.0 / N, dtype=torch.float64, device=dev)
+    src, dst, nodes = src.to(dev).long(), dst.to(dev).long(), nodes.to(dev).long()
     chunk = math.ceil(N / P)
     Np = chunk * P
+    # a page's out-edges all live on one worker, so the local out-degree is the global one
+    outdeg = torch.bincount(src, minlength=N)[:N].to(torch.float64)
+    invdeg = torch.where(outdeg > 0, 1.0 / outdeg.clamp_min(1.0), torch.zeros_like(outdeg))
+    dvec = torch.zeros(N, dtype=torch.float64, device=dev)
+    dvec[nodes[outdeg[nodes] == 0]] = 1.0  # this worker's dangling pages
+    # edges grouped by target once: every iteration is a gather (no fp64 atomics)
+    csr = GO.build_csr(dst, src, Np)
+    pr = torch.full((N,), 1.0 / N, dtype=torch.float64, device=dev)
+    x = pr * invdeg
     for _ in range(iterations):
-        contrib = torch.zeros(Np, dtype=torch.float64, device=dev)
-        contrib.index_add_(0, dst, pr[src] / outdeg[src])
-        contrib[:N] += pr[dangling].sum() / N
-        if P > 1:
-            mine = torch.empty(chunk, dtype=torch.float64, device=dev)
-            comm.reduce_scatter(mine, contrib)
-            mine = damping * mine + (1 - damping) / N
-            full = torch.empty(Np, dtype=torch.float64, device=dev)
-            comm.all_gather_into(full, mine)
-            pr = full[:N]
-        else:
-            pr = damping * contrib[:N] + (1 - damping) / N
+        dm = torch.dot(pr, dvec).reshape(1)  # dangling mass, kept on the device
+        if P == 1:
+            pr, x = GO.pagerank_pull(csr, x, damping, (1 - damping) / N, damping / N, dm, invdeg, want_xnext=True)
+            continue
+        contrib, _ = GO.pagerank_pull(csr, x, 1.0, 0.0, 1.0 / N, dm)
+        mine = torch.empty(chunk, dtype=torch.float64, device=dev)
+        comm.reduce_scatter(mine, contrib)
+        mine = damping * mine + (1 - damping) / N
+        full = torch.empty(Np, dtype=torch.float64, device=dev)
+        comm.all_gather_into(full, mine)
+        pr = full[:N]
+        x = pr * invdeg
     return pr
 
 

@@ -13,6 +13,9 @@ from . import _lib
 _lib.register({
     "harp_csr_spmm_f64": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_long,
                           _lib.c_void_p],
+    "harp_pagerank_pull_f64": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_double, _lib.c_double,
+                               _lib.c_double, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long,
+                               _lib.c_long, _lib.c_long, _lib.c_void_p],
     "harp_colorset_combine_f64": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
                                   _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_long, _lib.c_void_p],
 })
@@ -48,6 +51,38 @@ def spmm(csr: CSR, M: torch.Tensor) -> torch.Tensor:
     out.zero_()
     out.index_add_(0, rows, M[csr.col.long()])
     return out
+
+
+def pagerank_pull(csr: CSR, x: torch.Tensor, alpha: float, b0: float, b1: float, dm: torch.Tensor = None,
+                  invdeg: torch.Tensor = None, want_xnext: bool = False):
+    """One PageRank pull step over a by-target CSR (``csrc/graph.hip`` pagerank_pull_kernel):
+    ``out[v] = alpha * sum_{u in in(v)} x[u] + b0 + b1 * dm`` (``dm`` a 1-element device
+    tensor, read on the device: no host sync), and with ``want_xnext`` also
+    ``xnext[v] = out[v] * invdeg[v]`` for v < len(invdeg). Returns (out, xnext or None)."""
+    assert x.dtype == torch.float64 and x.is_contiguous()
+    n = csr.n
+    out = torch.empty(n, dtype=torch.float64, device=x.device)
+    xnext = torch.empty(invdeg.numel(), dtype=torch.float64, device=x.device) if want_xnext else None
+    if _lib.use_native(x):
+        assert dm is None or (dm.dtype == torch.float64 and dm.device == x.device)
+        assert not want_xnext or (invdeg.dtype == torch.float64 and invdeg.is_contiguous() and invdeg.numel() <= n)
+        assert csr.col.numel() == 0 or int(csr.rowptr[-1]) == csr.col.numel()
+        st = _lib.kernels().harp_pagerank_pull_f64(
+            csr.rowptr.data_ptr(), csr.col.data_ptr(), x.data_ptr(), float(alpha), float(b0), float(b1),
+            dm.data_ptr() if dm is not None else None, out.data_ptr(),
+            invdeg.data_ptr() if want_xnext else None, xnext.data_ptr() if want_xnext else None,
+            invdeg.numel() if want_xnext else 0, n, csr.col.numel(), _lib.stream_ptr(x.device))
+        _lib.check(st, "pagerank_pull_f64")
+        return out, xnext
+    rows = torch.repeat_interleave(torch.arange(n, device=x.device), csr.rowptr[1:] - csr.rowptr[:-1])
+    out.zero_()
+    out.index_add_(0, rows, x[csr.col.long()])
+    out.mul_(alpha).add_(b0)
+    if dm is not None:
+        out.add_(b1 * dm)
+    if want_xnext:
+        xnext.copy_(out[:invdeg.numel()] * invdeg)
+    return out, xnext
 
 
 @lru_cache(maxsize=None)
