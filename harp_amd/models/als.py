@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from ..parallel.comm import Communicator
+from ..ops import als as OA
 from .mf_common import gather_factors, rmse, shuffle_coo
 
 
@@ -62,8 +63,24 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
     G = F.t() @ F if cfg.implicit else None
     out = torch.empty((n_rows, f), dtype=dt, device=dev)
     blk = max(1, int(cfg.block_bytes // (f * f * dt.itemsize * 2)))
+    # native path: per-row normal equations in one HIP pass (csrc/als.hip), no per-rating
+    # f x f outer products in HBM
+    native = OA.available(F) and f <= OA.MAX_F and dt in (torch.float32, torch.float64)
+    if native:
+        F = F.contiguous()
+        cols64 = cols.to(torch.int64).contiguous()
+        vals_dt = vals.to(dt).contiguous()
+        crow = crow.to(torch.int64).contiguous()
+        blk = max(blk, 1)
     for a in range(0, n_rows, blk):
         b = min(n_rows, a + blk)
+        if native:
+            A = torch.empty((b - a, f, f), dtype=dt, device=dev)
+            rhs = torch.empty((b - a, f), dtype=dt, device=dev)
+            OA.normal_equations(crow, cols64, vals_dt, F, G, cfg.implicit, cfg.alpha, cfg.lam,
+                                cfg.weighted_lambda or not cfg.implicit, A, rhs, a)
+            out[a:b] = _solve(A, rhs)
+            continue
         s, e = int(crow[a]), int(crow[b])
         r = rows[s:e] - a
         Fc = F[cols[s:e]]
@@ -85,13 +102,17 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
         else:
             lam = torch.full((b - a,), cfg.lam, dtype=dt, device=dev)
         A += lam[:, None, None] * eye
-        L, info = torch.linalg.cholesky_ex(A)
-        x = torch.cholesky_solve(rhs[:, :, None], L)[:, :, 0]
-        bad = info != 0
-        if bool(bad.any()):
-            x[bad] = torch.linalg.lstsq(A[bad], rhs[bad][:, :, None]).solution[:, :, 0]
-        out[a:b] = x
+        out[a:b] = _solve(A, rhs)
     return out
+
+
+def _solve(A: torch.Tensor, rhs: torch.Tensor) -> torch.Tensor:
+    L, info = torch.linalg.cholesky_ex(A)
+    x = torch.cholesky_solve(rhs[:, :, None], L)[:, :, 0]
+    bad = info != 0
+    if bool(bad.any()):
+        x[bad] = torch.linalg.lstsq(A[bad], rhs[bad][:, :, None]).solution[:, :, 0]
+    return x
 
 
 def implicit_loss(u, i, v, X, Y, cfg: ALSConfig) -> float:

@@ -1,0 +1,40 @@
+"""ALS per-row normal equations (``csrc/als.hip``): A_r = sum_j a_j F_j F_j^T + G +
+lam_r I and rhs_r = sum_j b_j F_j for a block of CSR rows, fp32 / fp64, f <= 64."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+MAX_F = 64
+
+_lib.register({
+    name: [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, ct, ct,
+           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_void_p]
+    for name, ct in (("harp_als_normal_f32", _lib.c_float), ("harp_als_normal_f64", _lib.c_double))
+})
+
+
+def available(t: torch.Tensor) -> bool:
+    return _lib.use_native(t)
+
+
+def normal_equations(crow: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, F: torch.Tensor, G, implicit: bool,
+                     alpha: float, lam: float, scale_lam: bool, A: torch.Tensor, rhs: torch.Tensor, row0: int) -> None:
+    """Fill ``A`` [m, f, f] and ``rhs`` [m, f] for rows row0 .. row0 + m of the CSR
+    (``crow`` int64 over all rows, ``cols`` int64 row ids into ``F`` [*, f])."""
+    m, f = rhs.shape
+    dt = F.dtype
+    assert f <= MAX_F and A.shape == (m, f, f) and dt in (torch.float32, torch.float64)
+    for t in (crow, cols, vals, F, A, rhs):
+        assert t.is_contiguous() and t.device == F.device
+    assert crow.dtype == torch.int64 and cols.dtype == torch.int64 and vals.dtype == dt and A.dtype == dt
+    assert row0 + m < crow.numel() and int(crow[-1]) <= cols.numel() == vals.numel()
+    if G is not None:
+        G = G.to(dt).contiguous()
+        assert G.shape == (f, f)
+    fn = _lib.kernels().harp_als_normal_f32 if dt == torch.float32 else _lib.kernels().harp_als_normal_f64
+    st = fn(crow.data_ptr(), cols.data_ptr(), vals.data_ptr(), F.data_ptr(), f,
+            G.data_ptr() if G is not None else None, int(bool(implicit)), float(alpha), float(lam),
+            int(bool(scale_lam)), A.data_ptr(), rhs.data_ptr(), int(row0), m, _lib.stream_ptr(F.device))
+    _lib.check(st, "als_normal")

@@ -1,0 +1,51 @@
+"""ALS normal-equation kernel (``csrc/als.hip``) against the plain PyTorch formulation of
+the same per-row systems (outer products + index_add, fp64 on the CPU), explicit and
+implicit, fp32 and fp64, f up to the kernel's 64, rows with 0 .. 100 ratings."""
+import pytest
+import torch
+
+from harp_amd.models import als as A
+from harp_amd.ops import als as OA
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(n_rows, n_cols, nnz, f, seed):
+    g = torch.Generator().manual_seed(seed)
+    rows = torch.sort(torch.randint(0, n_rows - 3, (nnz,), generator=g)).values  # last rows empty
+    rows[:100] = 0  # one row longer than the kernel's 32-row LDS chunk
+    rows = torch.sort(rows).values
+    cols = torch.randint(0, n_cols, (nnz,), generator=g)
+    vals = torch.rand(nnz, generator=g, dtype=torch.float64) * 5
+    vals[::7] = 0.0
+    F = torch.randn(n_cols, f, generator=g, dtype=torch.float64) * 0.3
+    return rows, cols, vals, F
+
+
+@pytest.mark.parametrize("implicit", [False, True])
+@pytest.mark.parametrize("f,dt", [(8, torch.float64), (50, torch.float32), (64, torch.float64)])
+def test_solve_rows_native_matches_torch(cuda, implicit, f, dt):
+    rows, cols, vals, F = _problem(700, 300, 6000, f, f)
+    cfg = A.ALSConfig(factors=f, implicit=implicit, alpha=2.0, lam=0.1, block_bytes=1 << 22)
+    want = A.solve_rows(rows, cols, vals, 700, F, cfg)  # CPU: torch path, fp64
+    got = A.solve_rows(rows.to(cuda), cols.to(cuda), vals.to(cuda), 700, F.to(cuda, dt), cfg)
+    tol = 1e-9 if dt == torch.float64 else 2e-3
+    assert torch.allclose(got.cpu().double(), want, rtol=tol, atol=tol)
+
+
+def test_normal_equations_direct(cuda):
+    rows, cols, vals, F = _problem(64, 40, 900, 16, 3)
+    crow = torch.zeros(65, dtype=torch.int64)
+    crow[1:] = torch.cumsum(torch.bincount(rows, minlength=64), 0)
+    G = F.t() @ F
+    Am = torch.empty(64, 16, 16, dtype=torch.float64, device=cuda)
+    rhs = torch.empty(64, 16, dtype=torch.float64, device=cuda)
+    OA.normal_equations(crow.to(cuda), cols.to(cuda), vals.to(cuda), F.to(cuda), G.to(cuda), True, 1.5, 0.2, False,
+                        Am, rhs, 0)
+    for r in (0, 5, 63):
+        sl = slice(int(crow[r]), int(crow[r + 1]))
+        Fc, v = F[cols[sl]], vals[sl]
+        want = G + Fc.t() @ (1.5 * v[:, None] * Fc) + 0.2 * torch.eye(16, dtype=torch.float64)
+        wr = Fc.t() @ ((1 + 1.5 * v) * (v > 0))
+        assert torch.allclose(Am[r].cpu(), want, rtol=1e-12, atol=1e-12)
+        assert torch.allclose(rhs[r].cpu(), wr, rtol=1e-12, atol=1e-12)
