@@ -71,15 +71,21 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
         cols64 = cols.to(torch.int64).contiguous()
         vals_dt = vals.to(dt).contiguous()
         crow = crow.to(torch.int64).contiguous()
-        blk = max(blk, 1)
+        blk = max(blk, 1 << 17)  # no per-rating intermediates: big blocks, fewer solver launches
     for a in range(0, n_rows, blk):
         b = min(n_rows, a + blk)
         if native:
-            A = torch.empty((b - a, f, f), dtype=dt, device=dev)
-            rhs = torch.empty((b - a, f), dtype=dt, device=dev)
-            OA.normal_equations(crow, cols64, vals_dt, F, G, cfg.implicit, cfg.alpha, cfg.lam,
-                                cfg.weighted_lambda or not cfg.implicit, A, rhs, a)
-            out[a:b] = _solve(A, rhs)
+            # build + Cholesky-solve every row's system in one kernel; rows whose system is
+            # not SPD (info) send the block through rocSOLVER with the lstsq fallback
+            scale = cfg.weighted_lambda or not cfg.implicit
+            info = torch.empty(b - a, dtype=torch.int32, device=dev)
+            OA.normal_equations(crow, cols64, vals_dt, F, G, cfg.implicit, cfg.alpha, cfg.lam, scale, None, None, a,
+                                X=out[a:b], info=info)
+            if bool(info.any()):
+                A = torch.empty((b - a, f, f), dtype=dt, device=dev)
+                rhs = torch.empty((b - a, f), dtype=dt, device=dev)
+                OA.normal_equations(crow, cols64, vals_dt, F, G, cfg.implicit, cfg.alpha, cfg.lam, scale, A, rhs, a)
+                out[a:b] = _solve(A, rhs)
             continue
         s, e = int(crow[a]), int(crow[b])
         r = rows[s:e] - a

@@ -10,7 +10,8 @@ MAX_F = 64
 
 _lib.register({
     name: [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, ct, ct,
-           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_void_p]
+           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
+           _lib.c_void_p]
     for name, ct in (("harp_als_normal_f32", _lib.c_float), ("harp_als_normal_f64", _lib.c_double))
 })
 
@@ -20,15 +21,23 @@ def available(t: torch.Tensor) -> bool:
 
 
 def normal_equations(crow: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, F: torch.Tensor, G, implicit: bool,
-                     alpha: float, lam: float, scale_lam: bool, A: torch.Tensor, rhs: torch.Tensor, row0: int) -> None:
+                     alpha: float, lam: float, scale_lam: bool, A, rhs, row0: int, X=None, info=None) -> None:
     """Fill ``A`` [m, f, f] and ``rhs`` [m, f] for rows row0 .. row0 + m of the CSR
-    (``crow`` int64 over all rows, ``cols`` int64 row ids into ``F`` [*, f])."""
-    m, f = rhs.shape
+    (``crow`` int64 over all rows, ``cols`` int64 row ids into ``F`` [*, f]); or, with
+    ``X`` [m, f] and ``info`` [m] int32 given (A, rhs None), solve each system in the
+    kernel (Cholesky in LDS): info[r] = 1 marks a row whose system was not SPD."""
+    solve = X is not None
+    m, f = (X if solve else rhs).shape
     dt = F.dtype
-    assert f <= MAX_F and A.shape == (m, f, f) and dt in (torch.float32, torch.float64)
-    for t in (crow, cols, vals, F, A, rhs):
+    assert f <= MAX_F and dt in (torch.float32, torch.float64)
+    outs = (X, info) if solve else (A, rhs)
+    if solve:
+        assert info is not None and info.dtype == torch.int32 and info.shape == (m,) and X.dtype == dt
+    else:
+        assert A.shape == (m, f, f) and A.dtype == dt and rhs.dtype == dt
+    for t in (crow, cols, vals, F) + outs:
         assert t.is_contiguous() and t.device == F.device
-    assert crow.dtype == torch.int64 and cols.dtype == torch.int64 and vals.dtype == dt and A.dtype == dt
+    assert crow.dtype == torch.int64 and cols.dtype == torch.int64 and vals.dtype == dt
     assert row0 + m < crow.numel() and int(crow[-1]) <= cols.numel() == vals.numel()
     if G is not None:
         G = G.to(dt).contiguous()
@@ -36,5 +45,6 @@ def normal_equations(crow: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     fn = _lib.kernels().harp_als_normal_f32 if dt == torch.float32 else _lib.kernels().harp_als_normal_f64
     st = fn(crow.data_ptr(), cols.data_ptr(), vals.data_ptr(), F.data_ptr(), f,
             G.data_ptr() if G is not None else None, int(bool(implicit)), float(alpha), float(lam),
-            int(bool(scale_lam)), A.data_ptr(), rhs.data_ptr(), int(row0), m, _lib.stream_ptr(F.device))
+            int(bool(scale_lam)), None if solve else A.data_ptr(), None if solve else rhs.data_ptr(), int(row0), m,
+            X.data_ptr() if solve else None, info.data_ptr() if solve else None, _lib.stream_ptr(F.device))
     _lib.check(st, "als_normal")

@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/als
+O=gpurun_out/${ALS_OUT:-als}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_als_gpu.py tests/test_apps_gpu.py -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }

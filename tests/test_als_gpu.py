@@ -49,3 +49,25 @@ def test_normal_equations_direct(cuda):
         wr = Fc.t() @ ((1 + 1.5 * v) * (v > 0))
         assert torch.allclose(Am[r].cpu(), want, rtol=1e-12, atol=1e-12)
         assert torch.allclose(rhs[r].cpu(), wr, rtol=1e-12, atol=1e-12)
+
+
+def test_fused_solve_flags_non_spd_rows(cuda):
+    rows, cols, vals, F = _problem(64, 40, 4000, 16, 4)  # rows 61..63 have no ratings
+    crow = torch.zeros(65, dtype=torch.int64)
+    crow[1:] = torch.cumsum(torch.bincount(rows, minlength=64), 0)
+    X = torch.empty(64, 16, dtype=torch.float64, device=cuda)
+    info = torch.empty(64, dtype=torch.int32, device=cuda)
+    # explicit, lam = 0: an empty row's system is the zero matrix
+    OA.normal_equations(crow.to(cuda), cols.to(cuda), vals.to(cuda), F.to(cuda), None, False, 0.0, 0.0, True,
+                        None, None, 0, X=X, info=info)
+    info = info.cpu()
+    assert info[61:].tolist() == [1, 1, 1] and int(info[:61].sum()) == 0
+    for r in (0, 10):
+        sl = slice(int(crow[r]), int(crow[r + 1]))
+        Fc, v = F[cols[sl]], vals[sl]
+        want = torch.linalg.solve(Fc.t() @ Fc, Fc.t() @ v)
+        assert torch.allclose(X[r].cpu(), want, rtol=1e-8, atol=1e-8)
+    cfg = A.ALSConfig(factors=16, implicit=False, lam=0.0)
+    got = A.solve_rows(rows.to(cuda), cols.to(cuda), vals.to(cuda), 64, F.to(cuda), cfg)
+    # the flagged block went through the rocSOLVER path; its SPD rows agree with the fused solve
+    assert torch.allclose(got[:61].cpu(), X[:61].cpu(), rtol=1e-8, atol=1e-8)
