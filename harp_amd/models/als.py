@@ -56,9 +56,8 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
     f = F.shape[1]
     dt = F.dtype
     dev = F.device
-    if crow is None:
-        crow = torch.zeros(n_rows + 1, dtype=torch.int64, device=dev)
-        crow[1:] = torch.cumsum(torch.bincount(rows, minlength=n_rows), 0)
+    if crow is None:  # rows are sorted: row starts by binary search (no histogram atomics)
+        crow = torch.searchsorted(rows, torch.arange(n_rows + 1, dtype=rows.dtype, device=dev))
     eye = torch.eye(f, dtype=dt, device=dev)
     G = F.t() @ F if cfg.implicit else None
     out = torch.empty((n_rows, f), dtype=dt, device=dev)

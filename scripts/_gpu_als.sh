@@ -8,4 +8,4 @@ timeout -k 10 200 python -u scripts/bench_als.py > $O/bench_als.log 2>&1 || { ta
 tail -1 $O/bench_als.log
 timeout -k 10 200 python -u scripts/bench_als.py --implicit 0 --factors 32 > $O/bench_als_exp32.log 2>&1 || exit 1
 tail -1 $O/bench_als_exp32.log
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python scripts/bench_als.py > $O/prof.log 2>&1 || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python scripts/bench_als.py --native-only > $O/prof.log 2>&1 || exit 1

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--nnz", type=float, default=2e7)
     ap.add_argument("--factors", type=int, default=64)
     ap.add_argument("--implicit", type=int, default=1)
+    ap.add_argument("--native-only", action="store_true", help="skip the torch comparison (profiling)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -42,6 +43,8 @@ def main():
     run()
     xn, tn = run()
     print("native %.4f s" % tn, flush=True)
+    if a.native_only:
+        return
     OA.available = lambda t: False  # torch formulation
     run()
     xt, tt = run()
