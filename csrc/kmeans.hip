@@ -328,28 +328,14 @@ int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* la
   return harp_launch_status();
 }
 
-// variant -> (G, WAVES, RG). Kp must be a multiple of 128 for every variant.
+// variant -> (G, WAVES, RG, PIPE). Kp must be a multiple of 128 for every variant.
+// Only the measured frontier ships (profiles/r1_kmeans_*): 14 is the default for
+// d <= 124, 13 its RG=2 neighbour, 4 the one-group shape wide rows (9..16 k-steps) use.
 #define KM_VARIANTS(KS)                                                                       \
   switch (variant) {                                                                        \
-    case 0: return launch_assign<KS, 2, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
-    case 1: return launch_assign<KS, 2, 8, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
-    case 2: return launch_assign<KS, 2, 4, 4>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
-    case 3: return launch_assign<KS, 3, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
     case 4: return launch_assign<KS, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 5: return launch_assign<KS, 2, 8, 4, 1>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 6: return launch_assign<KS, 2, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 7: return launch_assign<KS, 2, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 8: return launch_assign<KS, 2, 4, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 9: return launch_assign<KS, 2, 4, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 10: return launch_assign<KS, 2, 8, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 11: return launch_assign<KS, 3, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 12: return launch_assign<KS, 3, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     case 13: return launch_assign<KS, 4, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     case 14: return launch_assign<KS, 4, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 15: return launch_assign<KS, 3, 4, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 16: return launch_assign<KS, 4, 4, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 17: return launch_assign<KS, 4, 8, 8, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 18: return launch_assign<KS, 4, 8, 6, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     default: return HARP_EBADARG;                                                           \
   }
 
@@ -357,18 +343,8 @@ int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* la
 
 HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
   switch (variant) {
-    case 0: return 8 * 2 * 32;
-    case 1: return 8 * 2 * 32;
-    case 2: return 4 * 2 * 32;
-    case 3: return 8 * 3 * 32;
     case 4: return 16 * 1 * 32;
-    case 5: case 6: case 7: return 8 * 2 * 32;
-    case 8: case 9: return 4 * 2 * 32;
-    case 10: return 8 * 2 * 32;
-    case 11: case 12: return 8 * 3 * 32;
-    case 13: case 14: case 17: case 18: return 8 * 4 * 32;
-    case 15: return 4 * 3 * 32;
-    case 16: return 4 * 4 * 32;
+    case 13: case 14: return 8 * 4 * 32;
     default: return -1;
   }
 }
