@@ -200,6 +200,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
         if cfg.graph and not want_obj and cfg.strategy == "allreduce" and self.device.type == "cuda":
             return self._graph_step(it)
         timer = self.metrics.timer
+        self.metrics.begin_iteration()
         t_it = time.perf_counter()
         with timer.phase("compute"):
             self.sums.zero_()
@@ -215,6 +216,8 @@ class KMeansCollectiveMapper(CollectiveMapper):
                 self.comm.all_reduce(ot)
             self.objective.append(float(ot.item()))
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
+        self.metrics.end_iteration("kmeans", it, strategy=cfg.strategy,
+                                   objective=self.objective[-1] if obj is not None else None)
 
     def _sum_table(self, sums: torch.Tensor) -> PackedTable:
         """The partial-sum table of the allreduce strategy, built once over the persistent
@@ -238,6 +241,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
         if getattr(self, "_graphs", None) is None:
             self._capture_graphs()
         timer = self.metrics.timer
+        self.metrics.begin_iteration()
         t_it = time.perf_counter()
         with timer.phase("compute"):
             self._graphs[0].replay()
@@ -247,6 +251,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
         with timer.phase("prepare"):
             self._graphs[1].replay()
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
+        self.metrics.end_iteration("kmeans", it, strategy="allreduce", hip_graph=True)
 
     def _capture_graphs(self) -> None:
         cfg = self.cfg
@@ -364,9 +369,9 @@ class KMeansCollectiveMapper(CollectiveMapper):
         real = max(0, min(cfg.num_centroids - lo, self.Kb))
         blk = torch.zeros((self.Kb, cfg.dim), dtype=torch.float32, device=self.device)
         blk[:real] = self.c[lo:lo + real]
-        self.c_rot = DeviceRotator(self.comm, [blk], name="km-c")
+        self.c_rot = DeviceRotator(self.comm, [blk], name="km-c", metrics=self.metrics)
         self.s_rot = DeviceRotator(self.comm, [torch.zeros((self.Kb, self.dp), dtype=torch.float32,
-                                                           device=self.device)], name="km-s")
+                                                           device=self.device)], name="km-s", metrics=self.metrics)
         self.best_d = torch.empty(self.X.shape[0], dtype=torch.float32, device=self.device)
         self.md = torch.empty_like(self.best_d)
         self.best_l = torch.empty(self.X.shape[0], dtype=torch.int64, device=self.device)
@@ -380,6 +385,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
         ring = [(r + 1) % P for r in range(P)]
         t_it = time.perf_counter()
         timer = self.metrics.timer
+        self.metrics.begin_iteration()
         with timer.phase("compute"):
             self.best_d.fill_(float("inf"))
             self.best_l.fill_(0)
@@ -417,6 +423,8 @@ class KMeansCollectiveMapper(CollectiveMapper):
                 self.comm.all_reduce(ot)
             self.objective.append(float(ot.item()))
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
+        self.metrics.end_iteration("kmeans", it, strategy="rotation",
+                                   objective=self.objective[-1] if want_obj else None)
 
     def _rotation_gather(self) -> torch.Tensor:
         from .common import gather_rows

@@ -123,7 +123,7 @@ class LDACollectiveMapper(CollectiveMapper):
         block = self.schedule.block_at(me, 0, 0)
         slabs = [nwk_full[(block * S + k) * self.vps:(block * S + k + 1) * self.vps].clone() for k in range(S)]
         del nwk_full
-        self.rot = DeviceRotator(self.comm, slabs, name="lda-w")
+        self.rot = DeviceRotator(self.comm, slabs, name="lda-w", metrics=self.metrics)
         self.vbeta = self.vocab * cfg.beta
 
     def iterate(self, it: int) -> int:
@@ -174,12 +174,14 @@ class LDACollectiveMapper(CollectiveMapper):
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)
         for it in range(self.cfg.iterations):
+            self.metrics.begin_iteration()
             t0 = time.perf_counter()
-            self.iterate(it)
+            n = self.iterate(it)
             self.rot.wait_all()
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
             self.iter_times.append(time.perf_counter() - t0)
+            self.metrics.end_iteration("lda", it, tokens=n, iter_s=self.iter_times[-1], strategy="rotation")
             if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
         self.result = {"loglik": self.loglik, "iter_s": self.iter_times}
@@ -298,11 +300,13 @@ class LDAPushPullMapper(LDACollectiveMapper):
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)
         for it in range(self.cfg.iterations):
+            self.metrics.begin_iteration()
             t0 = time.perf_counter()
-            self.iterate(it)
+            n = self.iterate(it)
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
             self.iter_times.append(time.perf_counter() - t0)
+            self.metrics.end_iteration("lda", it, tokens=n, iter_s=self.iter_times[-1], strategy="push_pull")
             if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
         self.result = {"loglik": self.loglik, "iter_s": self.iter_times}

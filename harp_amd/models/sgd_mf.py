@@ -196,7 +196,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             gs = block * S + k
             gh = torch.Generator().manual_seed(cfg.seed * 1009 + gs)
             slabs.append((torch.rand((self.ips, r), generator=gh) * 2 * scale).to(dev))
-        self.rot = DeviceRotator(self.comm, slabs, name="sgd-h")
+        self.rot = DeviceRotator(self.comm, slabs, name="sgd-h", metrics=self.metrics)
         self.trained = 0
 
     def _all_users_of(self, me: int) -> torch.Tensor:
@@ -234,12 +234,15 @@ class SGDCollectiveMapper(CollectiveMapper):
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)
         for ep in range(self.cfg.epochs):
+            self.metrics.begin_iteration()
             t0 = time.perf_counter()
-            self.train_epoch(ep)
+            n = self.train_epoch(ep)
             self.rot.wait_all()
             if torch.cuda.is_available() and self.device.type == "cuda":
                 torch.cuda.synchronize()
             self.epoch_times.append(time.perf_counter() - t0)
+            self.metrics.end_iteration("sgd", ep, trained=n, epoch_s=self.epoch_times[-1],
+                                       updates_per_s=n / max(self.epoch_times[-1], 1e-12))
             if self.cfg.test_every and ((ep + 1) % self.cfg.test_every == 0 or ep == self.cfg.epochs - 1):
                 self.rmse_history.append((ep + 1, *self._eval_ring(ep)))
         self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained}

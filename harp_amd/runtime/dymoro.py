@@ -116,13 +116,16 @@ class DeviceRotator:
     mapping to self into a spare buffer, on slice k's private communicator; ``get(k)``
     makes the current stream wait for it (no host sync) and returns the new slab."""
 
-    def __init__(self, comm: Communicator, slabs: Sequence[torch.Tensor], name: str = "rot"):
+    def __init__(self, comm: Communicator, slabs: Sequence[torch.Tensor], name: str = "rot", metrics=None):
         self.comm = comm
+        self.name = name
         self.slabs = list(slabs)
         self.spare = [torch.empty_like(s) for s in self.slabs]
         self.channels = [comm.channel(f"{name}-{k}") for k in range(len(self.slabs))]
         self._work: Dict[int, list] = {}
+        self._nops = 0
         self.comm_time = 0.0
+        self.metrics = metrics  # records bytes per rotation + the exposed wait (see get)
 
     def start(self, k: int, rmap: Sequence[int]) -> None:
         me = self.comm.rank
@@ -136,8 +139,18 @@ class DeviceRotator:
     def get(self, k: int) -> torch.Tensor:
         works = self._work.pop(k, None)
         if works is not None:
-            for w in works:
-                w.wait()  # stream-level wait on GPU (RCCL), blocking on gloo
+            if self.metrics is not None:
+                # the wait makes the compute stream depend on the rotation; events around it
+                # time only the part of the transfer NOT hidden behind compute
+                slab = self.slabs[k]
+                with self.metrics.time_collective("rotate_wait", self.name, f"slice-{k}-{self._nops}",
+                                                  slab.numel() * slab.element_size(), self.comm.device):
+                    for w in works:
+                        w.wait()
+                self._nops += 1
+            else:
+                for w in works:
+                    w.wait()  # stream-level wait on GPU (RCCL), blocking on gloo
             self.slabs[k], self.spare[k] = self.spare[k], self.slabs[k]
         return self.slabs[k]
 

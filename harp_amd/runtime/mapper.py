@@ -26,7 +26,7 @@ from ..core.table import Table
 from ..parallel import collectives as C
 from ..parallel.comm import Communicator
 from ..parallel.events import Event, EventChannel, EventType
-from ..utils.metrics import Metrics
+from ..utils.metrics import Metrics, table_nbytes
 
 log = logging.getLogger("harp_amd.mapper")
 
@@ -82,7 +82,8 @@ class CollectiveMapper:
 
     def __init__(self, comm: Optional[Communicator] = None, metrics: Optional[Metrics] = None):
         self.comm = comm or Communicator()
-        self.metrics = metrics or Metrics(rank=self.comm.rank)
+        self.metrics = metrics or Metrics(rank=self.comm.rank, world=self.comm.world_size)
+        self.metrics.world = self.comm.world_size
         self.events = EventChannel(self.comm.rank, self.comm.world_size)
         self.result: Any = None
 
@@ -135,9 +136,11 @@ class CollectiveMapper:
 
     # -- collectives ------------------------------------------------------------------------
     def _timed(self, ctx: str, op: str, kind: str, fn, *a, **kw):
-        t0 = time.perf_counter()
-        ok = fn(self.comm, *a, **kw)
-        self.metrics.collective(kind, ctx, op, time.perf_counter() - t0)
+        """Run one collective, recording its bytes (this rank's table payload before the
+        call) and its stream time (HIP events around it on the current stream)."""
+        nbytes = table_nbytes(a[0]) if a and isinstance(a[0], Table) else 0
+        with self.metrics.time_collective(kind, ctx, op, nbytes, self.comm.device):
+            ok = fn(self.comm, *a, **kw)
         return ok
 
     def barrier(self, ctx: str, op: str) -> bool:

@@ -1,0 +1,133 @@
+"""Per-iteration metrics and the bench.py driver contract.
+
+* K-means / SGD / LDA on 2 gloo ranks write one JSONL record per iteration with phase
+  times, collective bytes (non-zero: the reference never logged bytes moved), achieved
+  GB/s and the xGMI-model efficiency (reference timing hooks:
+  KMeansCollectiveMapper.java:191-193, SGDCollectiveMapper.java:294-298,
+  RegroupCollective.java:274-295).
+* ``bench.py --gpus 2`` without a torchrun environment spawns its 2 ranks itself and
+  reports ``n_gpus: 2`` (KMeansLauncher.java:97-137 launches the multi-worker job)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from harp_amd.models.kmeans import KMeansConfig, KMeansCollectiveMapper
+from harp_amd.runtime.launcher import launch
+from harp_amd.runtime.mapper import KeyValReader
+from harp_amd.utils.metrics import Metrics, ideal_collective_s, ring_allreduce_ideal_s, table_nbytes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _km_job(comm, strategy, path):
+    m = KMeansCollectiveMapper(comm, KMeansConfig(num_points=400, num_centroids=16, dim=8, iterations=3,
+                                                  strategy=strategy),
+                               metrics=Metrics(rank=comm.rank, path=f"{path}.{comm.rank}"))
+    m.run(KeyValReader([]))
+    return m.metrics.summary()["collectives"]
+
+
+def _read(path):
+    with open(path) as f:
+        return [json.loads(line) for line in f]
+
+
+@pytest.mark.parametrize("strategy", ["allreduce", "regroup_allgather", "bcast_reduce", "push_pull", "rotation"])
+def test_kmeans_jsonl_records(tmp_path, strategy):
+    path = str(tmp_path / "m.jsonl")
+    summ = launch(_km_job, 2, args=(strategy, path), timeout=300)
+    for r in range(2):
+        recs = _read(f"{path}.{r}")
+        its = [x for x in recs if x["event"] == "iteration"]
+        assert [x["iter"] for x in its] == [0, 1, 2]
+        for x in its:
+            assert x["app"] == "kmeans" and x["world"] == 2 and x["rank"] == r
+            assert x["collective_bytes"] > 0, x
+            assert x["phases_ms"]["compute"] > 0
+            assert all(c["bytes"] >= 0 and c["ms"] >= 0 for c in x["collectives"])
+            if strategy != "rotation":
+                assert any("eff_vs_xgmi_model" in c for c in x["collectives"]), x
+        assert sum(v["bytes"] for v in summ[r].values()) > 0
+
+
+def test_allreduce_bytes_match_table(tmp_path):
+    path = str(tmp_path / "a.jsonl")
+    launch(_km_job, 2, args=("allreduce", path), timeout=300)
+    rec = _read(f"{path}.0")[0]
+    ar = [c for c in rec["collectives"] if c["kind"] == "allreduce"]
+    assert len(ar) == 1
+    kp, dp = 128, 16  # padded centroids x padded dim (fp32 partial sums)
+    assert ar[0]["bytes"] == kp * dp * 4
+    assert ar[0]["ideal_ms"] == pytest.approx(ring_allreduce_ideal_s(kp * dp * 4, 2) * 1e3, rel=1e-3)
+
+
+def test_ideal_model_and_nbytes():
+    from harp_amd.core.combiner import ArrCombiner, Operation
+    from harp_amd.core.table import PackedTable, Table
+
+    t = PackedTable(list(range(4)), torch.zeros(4, 10), combiner=ArrCombiner(Operation.SUM))
+    assert table_nbytes(t) == 160
+    g = Table(1, ArrCombiner(Operation.SUM))
+    g.add(3, torch.zeros(5, dtype=torch.float64))
+    g.add(7, torch.zeros(2, dtype=torch.int32))
+    assert table_nbytes(g) == 48
+    assert ideal_collective_s("allreduce", 0, 8) == 0.0
+    assert ideal_collective_s("allgather", 153_000_000, 2) == pytest.approx(0.5e-3)
+    assert ideal_collective_s("rotate", 153_000_000, 4) == pytest.approx(1e-3)
+    assert ideal_collective_s("allreduce", 10, 1) == 0.0
+
+
+def _sgd_job(comm, path):
+    from harp_amd.models.sgd_mf import SGDCollectiveMapper, SGDConfig, synthetic_ratings
+
+    tr = synthetic_ratings(300, 80, 4000, seed=2)
+    m = SGDCollectiveMapper(comm, SGDConfig(rank=8, epochs=2, test_every=0, xcd_blocks=False), 300, 80, tr,
+                            metrics=Metrics(rank=comm.rank, path=f"{path}.{comm.rank}"))
+    m.run(KeyValReader([]))
+    return True
+
+
+def test_sgd_jsonl_rotation_bytes(tmp_path):
+    path = str(tmp_path / "s.jsonl")
+    launch(_sgd_job, 2, args=(path,), timeout=300)
+    recs = _read(f"{path}.0")
+    assert [x["iter"] for x in recs] == [0, 1]
+    for x in recs:
+        rot = [c for c in x["collectives"] if c["kind"] == "rotate_wait"]
+        assert rot and all(c["bytes"] > 0 for c in rot)
+        assert x["trained"] > 0 and x["updates_per_s"] > 0
+
+
+def _run_bench(args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=600, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_spawns_ranks():
+    rec = _run_bench(["--gpus", "2", "--points", "2e4", "--centroids", "128", "--backend", "gloo", "--steps", "2",
+                      "--warmup", "1"])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["value"] > 0
+    assert rec["sync_bytes_per_iter"] > 0
+    assert "sgd" not in rec  # auto: CPU ranks skip the SGD record
+
+
+def test_bench_single_rank_with_sgd_record():
+    rec = _run_bench(["--gpus", "1", "--points", "1e4", "--centroids", "128", "--steps", "2", "--warmup", "1",
+                      "--sgd", "on", "--sgd-users", "2000", "--sgd-items", "300", "--sgd-ratings", "20000",
+                      "--sgd-rank", "16", "--sgd-epochs", "2"])
+    assert rec["n_gpus"] == 1 and rec["metric"].startswith("sec/iteration K-means")
+    s = rec["sgd"]
+    assert s["updates_per_sec"] > 0 and s["epochs"] == 2 and 0 < s["train_rmse"] < 2
