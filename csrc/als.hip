@@ -154,7 +154,7 @@ template <typename T>
 int launch(const long* crow, const long* cols, const T* vals, const T* F, int f, const T* G, int implicit, T alpha,
            T lam, int scale_lam, T* A, T* rhs, long row0, long nrows, T* X, int* info, hipStream_t s) {
   if (nrows <= 0) return HARP_OK;
-  if (f <= 0 || f > kMaxF || nrows > 0x7fffffffL || (X && !info) || (!X && (!A || !rhs))) return HARP_EBADARG;
+  if (f <= 0 || f > kMaxF || nrows * (long)kThreads > 0xffffffffL || (X && !info) || (!X && (!A || !rhs))) return HARP_EBADARG;
   als_normal_kernel<T><<<dim3((unsigned)nrows), dim3(kThreads), 0, s>>>(crow, cols, vals, F, f, G, implicit, alpha,
                                                                        lam, scale_lam, A, rhs, row0, X, info);
   return harp_launch_status();

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void kmeans_csr_assign_kernel(const long* __re
   for (long r = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += nw) {
     const long a = rowptr[r], b = rowptr[r + 1];
     double best = __builtin_inf();
-    int besti = 0x7fffffff;
+    int besti = 0;  // a row whose distances are all NaN still lands in a valid cluster
     for (int c0 = 0; c0 < K; c0 += 64 * KPL) {
       double acc[KPL];
 #pragma unroll

@@ -27,7 +27,8 @@ import torch
 
 from ..parallel.comm import Communicator
 from ..ops import als as OA
-from .mf_common import gather_factors, rmse, shuffle_coo
+from ..runtime.mapper import inject_fault
+from .mf_common import FactorCheckpoint, gather_factors, rmse, save_factor_models, shuffle_coo
 
 
 @dataclass
@@ -40,6 +41,9 @@ class ALSConfig:
     weighted_lambda: bool = False  # lambda * n_u (ALS-WR) instead of lambda
     seed: int = 0
     block_bytes: int = 1 << 28
+    checkpoint_dir: str = ""  # .hpt checkpoints of X / Y (global row ids: any world size resumes)
+    checkpoint_every: int = 0
+    model_dir: str = ""       # final text dump W-<worker> (users), H-<worker> (items)
 
 
 def _sorted_rows(rows: torch.Tensor, n_rows: int):
@@ -71,6 +75,7 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
         vals_dt = vals.to(dt).contiguous()
         crow = crow.to(torch.int64).contiguous()
         blk = max(blk, 1 << 17)  # no per-rating intermediates: big blocks, fewer solver launches
+        blk = min(blk, (2**32 - 1) // OA.THREADS)  # one workgroup per row: grid x threads < 2^32
     for a in range(0, n_rows, blk):
         b = min(n_rows, a + blk)
         if native:
@@ -153,7 +158,9 @@ def train_als(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
     Y = Y0[my_items]
     X = torch.zeros((my_users.numel(), cfg.factors), dtype=dt, device=dev)
     hist: List[Dict[str, float]] = []
-    for it in range(cfg.iterations):
+    ck = FactorCheckpoint(comm, cfg.checkpoint_dir, cfg.checkpoint_every)
+    start, hist = ck.resume({"X": (X, my_users, n_users), "Y": (Y, my_items, n_items)}, hist)
+    for it in range(start, cfg.iterations):
         t0 = time.perf_counter()
         Yf = gather_factors(comm, my_items, Y, n_items)
         X = solve_rows(ur, uc, uv, my_users.numel(), Yf, cfg, crow_u)
@@ -169,7 +176,11 @@ def train_als(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
             pred = (Xf[tu[mine].to(dev)] * Yf[ti[mine].to(dev)]).sum(1)
             rec["test_rmse"] = rmse(comm, ((pred - tv[mine].to(dev, dt)) ** 2).sum(), int(mine.sum()))
         hist.append(rec)
-    return {"X": X, "Y": Y, "user_ids": my_users, "item_ids": my_items, "history": hist}
+        inject_fault(me, it)
+        ck.maybe_save(it, {"X": (X, my_users), "Y": (Y, my_items)}, hist)
+    if cfg.model_dir:
+        save_factor_models(comm, cfg.model_dir, {"W": (X, my_users), "H": (Y, my_items)})
+    return {"X": X, "Y": Y, "start_iteration": start, "user_ids": my_users, "item_ids": my_items, "history": hist}
 
 
 def train_als_batch(u, i, v, n_users, n_items, cfg: ALSConfig):

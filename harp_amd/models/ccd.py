@@ -27,7 +27,8 @@ import torch
 
 from ..parallel.comm import Communicator
 from ..ops import ccd as C
-from .mf_common import gather_factors, rmse, shuffle_coo
+from ..runtime.mapper import inject_fault
+from .mf_common import FactorCheckpoint, gather_factors, rmse, save_factor_models, shuffle_coo
 
 
 @dataclass
@@ -37,6 +38,9 @@ class CCDConfig:
     iterations: int = 10
     seed: int = 0
     init_scale: float = -1.0  # <= 0: uniform [0, 1/sqrt(rank)) like CCDMPCollectiveMapper.java:200-213
+    checkpoint_dir: str = ""  # .hpt checkpoints of W / H (global row ids: any world size resumes)
+    checkpoint_every: int = 0
+    model_dir: str = ""       # final text dump W-<worker>, H-<worker> (``id : v1 .. vr``)
 
 
 def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Tensor, n_users: int, n_items: int,
@@ -66,7 +70,9 @@ def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
     res_u = torch.empty_like(uval)
     res_i = torch.empty_like(ival)
     hist: List[Dict[str, float]] = []
-    for it in range(cfg.iterations):
+    ck = FactorCheckpoint(comm, cfg.checkpoint_dir, cfg.checkpoint_every)
+    start, hist = ck.resume({"W": (W, my_users, n_users), "H": (H, my_items, n_items)}, hist)
+    for it in range(start, cfg.iterations):
         t0 = time.perf_counter()
         Hf = gather_factors(comm, my_items, H, n_items).contiguous()
         C.residual(ur, uc, uval, W, Hf, res_u)  # ResTask
@@ -86,4 +92,8 @@ def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
             rec["test_rmse"] = rmse(comm, ((pred.double() - tv[mine].to(dev, torch.float64)) ** 2).sum(),
                                     int(mine.sum()))
         hist.append(rec)
-    return {"W": W, "H": H, "user_ids": my_users, "item_ids": my_items, "history": hist}
+        inject_fault(me, it)
+        ck.maybe_save(it, {"W": (W, my_users), "H": (H, my_items)}, hist)
+    if cfg.model_dir:
+        save_factor_models(comm, cfg.model_dir, {"W": (W, my_users), "H": (H, my_items)})
+    return {"W": W, "H": H, "start_iteration": start, "user_ids": my_users, "item_ids": my_items, "history": hist}

@@ -64,12 +64,16 @@ def gather_rows(comm: Communicator, rows: torch.Tensor) -> torch.Tensor:
     """All-gather variable-count row blocks [n_i, d] -> [sum n_i, d] (rank order)."""
     if comm.world_size == 1:
         return rows
-    from ..core.table import Table
-
-    t = Table(0)
-    t.add(comm.rank, rows)
-    C.allgather(comm, t)
-    return torch.cat([t[r] for r in range(comm.world_size)])
+    P = comm.world_size
+    counts = comm.all_gather_ints([rows.shape[0]])[:, 0].tolist()
+    mx = max(counts)
+    if mx == 0:
+        return rows.new_zeros((0,) + tuple(rows.shape[1:])).to(comm.device)
+    buf = torch.zeros((mx,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=comm.device)
+    buf[: rows.shape[0]] = rows.to(comm.device)
+    out = torch.empty((P * mx,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=comm.device)
+    comm.all_gather_into(out, buf)  # one padded all-gather (equal-size slabs)
+    return torch.cat([out[r * mx:r * mx + counts[r]] for r in range(P)])
 
 
 def dense_or_csr(x):

@@ -116,7 +116,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         cfg = self.cfg
         self.init_model(reader)
-        start = self.resume() if cfg.checkpoint_dir else 0
+        start = self.start_iteration = self.resume() if cfg.checkpoint_dir else 0
         for it in range(start, cfg.iterations):
             self.step(it)
             self.inject_fault(it)
@@ -125,39 +125,46 @@ class KMeansCollectiveMapper(CollectiveMapper):
         self.finish()
 
     # -- checkpoint / resume ------------------------------------------
-    def checkpoint(self, it: int) -> str:
-        """Write the centroid table after iteration ``it`` as per-rank ``.hpt`` files in
-        ``<dir>/it-<it>/`` (+ manifest with the objective history); once every rank has
-        written, rank 0 atomically points ``<dir>/LATEST`` at it."""
-        from ..utils.checkpoint import save_checkpoint
+    def _ckpt(self):
+        from ..utils.checkpoint import Checkpointer
 
+        return Checkpointer(self.cfg.checkpoint_dir, self.comm, self.cfg.checkpoint_every)
+
+    def checkpoint(self, it: int) -> str:
+        """Write the model after iteration ``it`` as ``<dir>/it-<it>/`` + ``LATEST``.
+
+        Replicated strategies save the [Kp, d] centroid table once (rank 0, replicated);
+        the model-parallel rotation strategy saves each rank's resident centroid block
+        (after P steps every block is back home) under its global centroid ids."""
+        extra = {"objective": list(self.objective), "strategy": self.cfg.strategy}
         if self.cfg.strategy == "rotation":
-            raise NotImplementedError("checkpoint of the model-parallel rotation strategy")
-        sub = os.path.join(self.cfg.checkpoint_dir, f"it-{it:06d}")
+            blk = self.c_rot.get(0)
+            lo = self.get_self_id() * self.Kb
+            t = PackedTable(list(range(lo, lo + self.Kb)), blk, table_id=0, combiner=self.sumop)
+            return self._ckpt().save(it, {"centroids": t}, extra=extra)
         t = PackedTable(self.ids, self.c, table_id=0, combiner=self.sumop)
-        save_checkpoint(sub, {"centroids": t}, self.get_self_id(), self.get_num_workers(), it,
-                        extra={"objective": list(self.objective)}, comm=self.comm)
-        if self.is_master():
-            tmp = os.path.join(self.cfg.checkpoint_dir, "LATEST.tmp")
-            with open(tmp, "w") as f:
-                json.dump({"dir": os.path.basename(sub), "iteration": it}, f)
-            os.replace(tmp, os.path.join(self.cfg.checkpoint_dir, "LATEST"))
-        return sub
+        return self._ckpt().save(it, {"centroids": t}, extra=extra, replicated=("centroids",))
 
     def resume(self) -> int:
-        """Load the latest checkpoint if one exists; returns the first iteration to run."""
-        from ..utils.checkpoint import load_checkpoint
-
-        latest = os.path.join(self.cfg.checkpoint_dir, "LATEST")
-        if not os.path.exists(latest):
+        """Load the latest checkpoint if one exists (any world size); returns the first
+        iteration to run."""
+        got = self._ckpt().load_latest(device=self.device, rng=True)
+        if got is None:
             return 0
-        with open(latest) as f:
-            sub = os.path.join(self.cfg.checkpoint_dir, json.load(f)["dir"])
-        man, tabs = load_checkpoint(sub, self.get_self_id(), self.get_num_workers(), device=self.device)
+        man, tabs = got
         c = tabs["centroids"]
-        buf = c.buffer if isinstance(c, PackedTable) else torch.stack([p.get() for p in c.get_partitions()])
-        self.c = buf.to(self.device, torch.float32).contiguous()
+        ids = c.ids if isinstance(c, PackedTable) else c.sorted_ids()
+        buf = c.buffer if isinstance(c, PackedTable) else torch.stack([c[i] for i in ids])
+        keep = [j for j, i in enumerate(ids) if i < self.cfg.num_centroids]  # padding rows carry nothing
+        full = torch.zeros_like(self.c)
+        full[torch.tensor([ids[j] for j in keep], dtype=torch.long, device=self.device)] = \
+            buf[torch.tensor(keep, dtype=torch.long, device=buf.device)].to(self.device, torch.float32)
+        self.c = full.contiguous()
         self.op = K.prepare(self.c[: self.cfg.num_centroids].contiguous(), self.dp, self.op)
+        if self.cfg.strategy == "rotation":
+            for a in ("c_rot", "s_rot"):
+                if hasattr(self, a):
+                    delattr(self, a)  # rebuilt from self.c (block me = rows [me*Kb, (me+1)*Kb))
         self.objective = list(man["extra"].get("objective", []))
         return int(man["iteration"]) + 1
 
@@ -185,6 +192,10 @@ class KMeansCollectiveMapper(CollectiveMapper):
         if not self.broadcast("main", "broadcast-centroids", cen, 0, False):
             raise IOError("Fail to bcast")
         self.c = cen.buffer  # [Kp, d]
+        if cfg.strategy == "rotation":  # room for every rank's padded block (resume / gather)
+            kb = K.padded_k(math.ceil(k / self.get_num_workers()))
+            if kb * self.get_num_workers() > Kp:
+                self.c = torch.cat([self.c, self.c.new_zeros((kb * self.get_num_workers() - Kp, d))])
         self.op = K.prepare(self.c[:k].contiguous(), self.dp)
         self.sums = torch.zeros((Kp, self.dp), dtype=torch.float32, device=dev)
         self.part = BlockPartitioner(self.get_num_workers(), Kp)
@@ -437,4 +448,5 @@ def run_kmeans(comm, cfg: KMeansConfig, points=None, init_centroids=None) -> dic
     """Launcher target: run one K-means job on this rank, return objective history."""
     m = KMeansCollectiveMapper(comm, cfg, points, init_centroids)
     m.run(KeyValReader([]))
-    return {"objective": m.objective, "centroids": m.centroids.cpu(), "phases": m.metrics.timer.flush()}
+    return {"objective": m.objective, "centroids": m.centroids.cpu(), "phases": m.metrics.timer.flush(),
+            "start_iteration": m.start_iteration}

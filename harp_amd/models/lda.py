@@ -39,6 +39,9 @@ class LDAConfig:
     seed: int = 0
     max_chunk: int = 0        # tokens per word chunk; 0 = 2048 (dense sampler) / 65536 (sparse)
     block_words: int = 4096   # push/pull strategy: words per model partition
+    checkpoint_dir: str = ""  # .hpt checkpoints (token topics, doc-topic, resident word slices)
+    checkpoint_every: int = 0  # iterations between checkpoints (0: never)
+    model_dir: str = ""       # word-model dumps every print_interval*10 iterations + at the end
 
 
 def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, seed: int = 0, device="cpu"):
@@ -125,6 +128,7 @@ class LDACollectiveMapper(CollectiveMapper):
         del nwk_full
         self.rot = DeviceRotator(self.comm, slabs, name="lda-w", metrics=self.metrics)
         self.vbeta = self.vocab * cfg.beta
+        self.word_perm = perm  # slice s holds words perm[s*vps:(s+1)*vps]
 
     def iterate(self, it: int) -> int:
         cfg = self.cfg
@@ -173,7 +177,8 @@ class LDACollectiveMapper(CollectiveMapper):
 
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)
-        for it in range(self.cfg.iterations):
+        start = self.start_iteration = self.resume()
+        for it in range(start, self.cfg.iterations):
             self.metrics.begin_iteration()
             t0 = time.perf_counter()
             n = self.iterate(it)
@@ -184,7 +189,92 @@ class LDACollectiveMapper(CollectiveMapper):
             self.metrics.end_iteration("lda", it, tokens=n, iter_s=self.iter_times[-1], strategy="rotation")
             if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
-        self.result = {"loglik": self.loglik, "iter_s": self.iter_times}
+            self._after_iteration(it)
+        self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start}
+
+    # -- checkpoint / resume / model output --------------------------------------------------
+    def _ckpt(self):
+        from ..utils.checkpoint import Checkpointer
+
+        return Checkpointer(self.cfg.checkpoint_dir, self.comm, self.cfg.checkpoint_every)
+
+    def _after_iteration(self, it: int) -> None:
+        cfg = self.cfg
+        self.inject_fault(it)
+        if self._ckpt().due(it):
+            self.checkpoint(it)
+        if cfg.model_dir and cfg.print_interval and ((it + 1) % (cfg.print_interval * 10) == 0
+                                                     or it + 1 == cfg.iterations):
+            self.print_word_model(f"{cfg.model_dir}/tmp_word_model/{it + 1}", it + 1)
+            if it + 1 == cfg.iterations and self.is_master() and self.loglik:
+                from ..utils.model_io import write_scalar
+
+                write_scalar(f"{cfg.model_dir}/evaluation", self.loglik[-1][1])
+
+    def _resident_words(self, it: int):
+        """(k, real word ids) of the word slices resident on this rank when ``it`` starts."""
+        S = self.cfg.num_slices
+        block = self.schedule.block_at(self.get_self_id(), it, 0)
+        out = []
+        for k in range(S):
+            lo = (block * S + k) * self.vps
+            hi = min(lo + self.vps, self.vocab)
+            out.append((k, self.word_perm[lo:hi] if hi > lo else self.word_perm[:0]))
+        return out
+
+    def _state_tables(self, it: int) -> dict:
+        from ..utils.checkpoint import blob_table, tensor_table
+
+        self.rot.wait_all()
+        tabs = {"tz": blob_table(self.tz), "ndk": blob_table(self.ndk), "nk": blob_table(self.nk)}
+        for k, words in self._resident_words(it + 1):
+            tabs[f"W{k}"] = tensor_table(self.rot.slabs[k][: words.numel()], words)
+        return tabs
+
+    def checkpoint(self, it: int) -> str:
+        """After iteration ``it``: this rank's token topics z, doc-topic counts, topic sums
+        and its resident word-topic slices (global word ids). Token order is a function of
+        the input split, so resume needs the same world size."""
+        return self._ckpt().save(it, self._state_tables(it), extra={"loglik": [list(x) for x in self.loglik]})
+
+    def _restore_common(self, man, tabs) -> int:
+        if man["world"] != self.get_num_workers():
+            raise ValueError(f"LDA resume needs the checkpoint's world size {man['world']} "
+                             f"(token topics are per-rank state), got {self.get_num_workers()}")
+        self.tz.copy_(tabs["tz"][0].to(self.device))
+        self.ndk.copy_(tabs["ndk"][0].to(self.device))
+        self.nk.copy_(tabs["nk"][0].to(self.device))
+        if self.doc_index is not None:
+            self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local)
+        self.loglik = [tuple(x) for x in man["extra"].get("loglik", [])]
+        return int(man["iteration"]) + 1
+
+    def resume(self) -> int:
+        got = self._ckpt().load_latest(device=self.device, rng=True)
+        if got is None:
+            return 0
+        man, tabs = got
+        it = self._restore_common(man, tabs)
+        for k, words in self._resident_words(it):
+            t = tabs[f"W{k}"]
+            assert t.ids == words.tolist(), "resident word slice does not match the checkpoint"
+            slab = self.rot.slabs[k]
+            slab.zero_()
+            slab[: words.numel()] = t.buffer.to(self.device)
+        return it
+
+    def print_word_model(self, folder: str, next_it: int) -> str:
+        """Reference printWordTableMap: ``<folder>/<worker>`` with one line per word
+        resident here when iteration ``next_it`` starts: ``wordID topic:count ...``."""
+        from ..utils.model_io import write_topic_counts
+
+        self.rot.wait_all()
+        ids, rows = [], []
+        for k, words in self._resident_words(next_it):
+            ids.append(words)
+            rows.append(self.rot.slabs[k][: words.numel()])
+        return write_topic_counts(f"{folder}/{self.get_self_id()}", torch.cat(ids), torch.cat(rows),
+                                  self.cfg.num_topics)
 
 
 def run_lda(comm, cfg: LDAConfig, n_docs: int, vocab: int, tokens) -> dict:
@@ -299,7 +389,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
 
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)
-        for it in range(self.cfg.iterations):
+        start = self.start_iteration = self.resume()
+        for it in range(start, self.cfg.iterations):
             self.metrics.begin_iteration()
             t0 = time.perf_counter()
             n = self.iterate(it)
@@ -309,7 +400,44 @@ class LDAPushPullMapper(LDACollectiveMapper):
             self.metrics.end_iteration("lda", it, tokens=n, iter_s=self.iter_times[-1], strategy="push_pull")
             if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
-        self.result = {"loglik": self.loglik, "iter_s": self.iter_times}
+            self._after_iteration(it)
+        self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start}
+
+    def _state_tables(self, it: int) -> dict:
+        from ..utils.checkpoint import blob_table, tensor_table
+
+        tabs = {"tz": blob_table(self.tz), "ndk": blob_table(self.ndk), "nk": blob_table(self.nk)}
+        ids = self.glob.sorted_ids()
+        if ids:
+            tabs["glob"] = tensor_table(torch.stack([self.glob[b] for b in ids]), ids)
+        return tabs
+
+    def resume(self) -> int:
+        got = self._ckpt().load_latest(device=self.device, rng=True)
+        if got is None:
+            return 0
+        man, tabs = got
+        it = self._restore_common(man, tabs)
+        if "glob" in tabs:
+            g = tabs["glob"]
+            for j, b in enumerate(g.ids):
+                self.glob[b].copy_(g.buffer[j].to(self.device))
+        return it
+
+    def print_word_model(self, folder: str, next_it: int = 0) -> str:
+        """Word rows of the global-table blocks this rank owns (``wordID topic:count ...``)."""
+        from ..utils.model_io import write_topic_counts
+
+        ids, rows = [], []
+        for b in self.glob.sorted_ids():
+            lo = b * self.B
+            n = max(0, min(self.B, self.vocab - lo))
+            ids.append(torch.arange(lo, lo + n))
+            rows.append(self.glob[b][:n])
+        if not ids:
+            ids, rows = [torch.zeros(0, dtype=torch.long)], [torch.zeros((0, self.Kp), dtype=torch.int32)]
+        return write_topic_counts(f"{folder}/{self.get_self_id()}", torch.cat(ids), torch.cat(rows).cpu(),
+                                  self.cfg.num_topics)
 
 
 def run_lda_push_pull(comm, cfg: LDAConfig, n_docs: int, vocab: int, tokens) -> dict:

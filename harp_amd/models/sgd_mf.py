@@ -44,6 +44,9 @@ class SGDConfig:
     test_every: int = 5        # rmseIteInterval
     seed: int = 0
     init_scale: float = -1.0   # <0: sqrt(mean_rating / r) (E[w.h] = mean rating)
+    checkpoint_dir: str = ""   # .hpt checkpoints (W rows + resident H slices); resume on restart
+    checkpoint_every: int = 0  # epochs between checkpoints (0: never)
+    model_dir: str = ""        # final text dump: W-<worker>, H-<worker>, evaluation
 
 
 def load_mm(path: str) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -233,7 +236,8 @@ class SGDCollectiveMapper(CollectiveMapper):
 
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)
-        for ep in range(self.cfg.epochs):
+        start = self.start_iteration = self.resume()
+        for ep in range(start, self.cfg.epochs):
             self.metrics.begin_iteration()
             t0 = time.perf_counter()
             n = self.train_epoch(ep)
@@ -245,7 +249,90 @@ class SGDCollectiveMapper(CollectiveMapper):
                                        updates_per_s=n / max(self.epoch_times[-1], 1e-12))
             if self.cfg.test_every and ((ep + 1) % self.cfg.test_every == 0 or ep == self.cfg.epochs - 1):
                 self.rmse_history.append((ep + 1, *self._eval_ring(ep)))
-        self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained}
+            self.inject_fault(ep)
+            if self._ckpt().due(ep):
+                self.checkpoint(ep)
+        if self.cfg.model_dir:
+            self.save_models(self.cfg.model_dir)
+        self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained,
+                       "start_epoch": start}
+
+    # -- checkpoint / resume / model output --------------------------------------------------
+    def _ckpt(self):
+        from ..utils.checkpoint import Checkpointer
+
+        return Checkpointer(self.cfg.checkpoint_dir, self.comm, self.cfg.checkpoint_every)
+
+    def _slab_items(self, gs: int) -> torch.Tensor:
+        """Real item ids of the rows of global slice ``gs`` (padding rows dropped)."""
+        lo = gs * self.ips
+        hi = min(lo + self.ips, self.n_items)
+        return self.item_perm[lo:hi] if hi > lo else self.item_perm[:0]
+
+    def _resident(self, epoch: int):
+        """(k, global slice, real item ids) of the slabs this rank holds when ``epoch`` starts."""
+        S = self.cfg.num_slices
+        block = self.schedule.block_at(self.get_self_id(), epoch, 0)
+        return [(k, block * S + k, self._slab_items(block * S + k)) for k in range(S)]
+
+    def checkpoint(self, ep: int) -> str:
+        """After epoch ``ep``: W rows (global user ids) and the H slices resident for epoch
+        ``ep + 1`` (global item ids), so any world size can resume."""
+        from ..utils.checkpoint import tensor_table
+
+        self.rot.wait_all()
+        tabs = {"W": tensor_table(self.W, self.users)}
+        for k, gs, items in self._resident(ep + 1):
+            tabs[f"H{k}"] = tensor_table(self.rot.slabs[k][: items.numel()], items)
+        extra = {"rmse": [list(x) for x in self.rmse_history], "trained": int(self.trained)}
+        return self._ckpt().save(ep, tabs, extra=extra)
+
+    def resume(self) -> int:
+        got = self._ckpt().load_latest(device=self.device, rng=True)
+        if got is None:
+            return 0
+        man, tabs = got
+        ep = int(man["iteration"]) + 1
+        r = self.cfg.rank
+
+        def scatter(tab, n_rows):
+            full = torch.zeros((n_rows, r), dtype=torch.float32, device=self.device)
+            ids = torch.tensor(tab.ids, dtype=torch.long, device=self.device)
+            full[ids] = tab.buffer.to(self.device, torch.float32)
+            return full
+
+        self.W.copy_(scatter(tabs["W"], self.n_users)[self.users.to(self.device)])
+        H = torch.zeros((self.n_items, r), dtype=torch.float32, device=self.device)
+        for name, tab in tabs.items():
+            if name.startswith("H") and len(tab):
+                ids = torch.tensor(tab.ids, dtype=torch.long, device=self.device)
+                H[ids] = tab.buffer.to(self.device, torch.float32)
+        for k, gs, items in self._resident(ep):
+            slab = self.rot.slabs[k]
+            slab.zero_()
+            slab[: items.numel()] = H[items.to(self.device)]
+        self.rmse_history = [tuple(x) for x in man["extra"].get("rmse", [])]
+        self.trained = int(man["extra"].get("trained", 0))
+        return ep
+
+    def save_models(self, folder: str) -> None:
+        """Reference saveModels (SGDCollectiveMapper.java:737-818): ``H-<worker>`` rows of
+        the resident H slices, ``W-<worker>`` rows of the local users (``id : v1 .. vr``),
+        ``evaluation`` (last test RMSE) from the master."""
+        from ..utils.model_io import write_factor_rows, write_scalar
+
+        self.rot.wait_all()
+        me = self.get_self_id()
+        ep = self.cfg.epochs
+        items, rows = [], []
+        for k, gs, it_ids in self._resident(ep):
+            items.append(it_ids)
+            rows.append(self.rot.slabs[k][: it_ids.numel()])
+        write_factor_rows(f"{folder}/H-{me}", torch.cat(items), torch.cat(rows))
+        write_factor_rows(f"{folder}/W-{me}", self.users, self.W)
+        if self.is_master():
+            last = self.rmse_history[-1][2] if self.rmse_history else float("nan")
+            write_scalar(f"{folder}/evaluation", last)
 
     def _eval_ring(self, epoch: int) -> Tuple[float, float]:
         """RMSE with a ring tour (P steps, every slice visits every worker, slices end where

@@ -7,6 +7,7 @@ import torch
 from . import _lib
 
 MAX_F = 64
+THREADS = 256  # workgroup size of the per-row kernel (csrc/als.hip kThreads)
 
 _lib.register({
     name: [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, ct, ct,

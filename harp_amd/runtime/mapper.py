@@ -195,26 +195,7 @@ class CollectiveMapper:
 
     # -- fault injection (tests) --------------------------------------------------
     def inject_fault(self, iteration: int) -> None:
-        """``HARP_FAULT="rank=R,iter=I,kind=exit|hang|raise[,attempt=A][,seconds=S]"`` makes
-        rank R fail after iteration I of job attempt A (default 0, see ``launch(retries)``):
-        ``exit`` kills the process (a dead peer), ``hang`` stops it for S seconds (a stuck
-        peer: the others' collective watchdog fires), ``raise`` fails the mapper."""
-        spec = os.environ.get("HARP_FAULT")
-        if not spec:
-            return
-        kv = dict(x.split("=", 1) for x in spec.split(",") if "=" in x)
-        if int(kv.get("rank", -1)) != self.get_self_id() or int(kv.get("iter", -1)) != iteration:
-            return
-        if int(kv.get("attempt", 0)) != int(os.environ.get("HARP_ATTEMPT", "0")):
-            return
-        kind = kv.get("kind", "exit")
-        log.error("injected fault %s on rank %d at iteration %d", kind, self.get_self_id(), iteration)
-        if kind == "exit":
-            os._exit(17)
-        if kind == "hang":
-            time.sleep(float(kv.get("seconds", 3600)))
-            return
-        raise RuntimeError(f"injected fault at iteration {iteration}")
+        inject_fault(self.get_self_id(), iteration)
 
     # -- memory / logging ------------------------------------------------------------------
     def free_memory(self) -> None:
@@ -236,3 +217,26 @@ class CollectiveMapper:
         import gc
 
         log.info("gc counts %s", gc.get_count())
+
+
+def inject_fault(rank: int, iteration: int) -> None:
+    """``HARP_FAULT="rank=R,iter=I,kind=exit|hang|raise[,attempt=A][,seconds=S]"`` makes
+    rank R fail after iteration I of job attempt A (default 0, see ``launch(retries)``):
+    ``exit`` kills the process (a dead peer), ``hang`` stops it for S seconds (a stuck
+    peer: the others' collective watchdog fires), ``raise`` fails the mapper."""
+    spec = os.environ.get("HARP_FAULT")
+    if not spec:
+        return
+    kv = dict(x.split("=", 1) for x in spec.split(",") if "=" in x)
+    if int(kv.get("rank", -1)) != rank or int(kv.get("iter", -1)) != iteration:
+        return
+    if int(kv.get("attempt", 0)) != int(os.environ.get("HARP_ATTEMPT", "0")):
+        return
+    kind = kv.get("kind", "exit")
+    log.error("injected fault %s on rank %d at iteration %d", kind, rank, iteration)
+    if kind == "exit":
+        os._exit(17)
+    if kind == "hang":
+        time.sleep(float(kv.get("seconds", 3600)))
+        return
+    raise RuntimeError(f"injected fault at iteration {iteration}")

@@ -17,19 +17,23 @@ JSON manifest tying ranks together:
             u8 ndim, i64 shape[ndim], i64 offset, i64 nbytes, u32 crc32; writables add
             u16 len + class name
 
-``manifest-<name>.json``: iteration, world size, per-rank files, RNG state, user extras.
+``manifest.json``: iteration, world size, per-rank files (replicated tables: one file
+written by rank 0), full CPU + GPU RNG state, user extras.
 
 Resume loads a rank's partitions back (onto any device); loading with a different world
-size returns all partitions of the listed files, which the caller re-shards with a
-regroup under the table's partitioner.
+size returns all partitions of the listed files (first copy of an id wins, sorted by
+id), from which the caller keeps the ids its partitioner assigns to it.
+:class:`Checkpointer` adds the periodic ``it-<n>/`` + atomic ``LATEST`` protocol every
+iterative app uses.
 """
 from __future__ import annotations
 
+import base64
 import json
 import os
 import struct
 import zlib
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -141,19 +145,46 @@ def load_table(path: str, device: str | torch.device = "cpu", combiner=None, ver
     return t
 
 
+def _rng_state() -> dict:
+    st = {"torch": base64.b64encode(torch.random.get_rng_state().numpy().tobytes()).decode()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        st["cuda"] = [base64.b64encode(t.numpy().tobytes()).decode() for t in torch.cuda.get_rng_state_all()]
+    return st
+
+
+def restore_rng(man: dict) -> None:
+    """Restore the CPU (and, when recorded and visible, per-device GPU) RNG state saved
+    in a manifest, so a resumed randomized app continues the uninterrupted stream."""
+    st = man.get("rng") or {}
+    if isinstance(st.get("torch"), str):
+        torch.random.set_rng_state(torch.frombuffer(bytearray(base64.b64decode(st["torch"])), dtype=torch.uint8))
+    if st.get("cuda") and torch.cuda.is_available():
+        states = [torch.frombuffer(bytearray(base64.b64decode(x)), dtype=torch.uint8) for x in st["cuda"]]
+        if len(states) == torch.cuda.device_count():
+            torch.cuda.set_rng_state_all(states)
+
+
 def save_checkpoint(directory: str, tables: Dict[str, Table], rank: int, world: int, iteration: int,
-                    extra: Optional[dict] = None, comm=None) -> str:
+                    extra: Optional[dict] = None, comm=None, replicated: Sequence[str] = ()) -> str:
     """Every rank writes its tables; rank 0 writes the manifest (after a barrier when a
-    communicator is given, so the manifest only appears once all shards exist)."""
+    communicator is given, so the manifest only appears once all shards exist).
+
+    Tables named in ``replicated`` hold the same partitions on every rank (e.g. the
+    K-means centroids after an allreduce): only rank 0 writes them, and any world size
+    loads that single file back unchanged."""
     os.makedirs(directory, exist_ok=True)
+    rep = set(replicated)
     for name, t in tables.items():
+        if name in rep and rank != 0:
+            continue
         save_table(t, os.path.join(directory, f"table-{name}-r{rank}.hpt"), rank, world)
     if comm is not None:
         comm.barrier()
     if rank == 0:
         man = {"version": VERSION, "iteration": iteration, "world": world,
-               "tables": {n: [f"table-{n}-r{r}.hpt" for r in range(world)] for n in tables},
-               "rng": {"torch": torch.random.get_rng_state().tolist()[:16]}, "extra": extra or {}}
+               "tables": {n: ([f"table-{n}-r0.hpt"] if n in rep else [f"table-{n}-r{r}.hpt" for r in range(world)])
+                          for n in tables},
+               "replicated": sorted(rep & set(tables)), "rng": _rng_state(), "extra": extra or {}}
         tmp = os.path.join(directory, "manifest.json.tmp")
         with open(tmp, "w") as f:
             json.dump(man, f)
@@ -161,20 +192,96 @@ def save_checkpoint(directory: str, tables: Dict[str, Table], rank: int, world: 
     return directory
 
 
-def load_checkpoint(directory: str, rank: int, world: int, device="cpu") -> tuple:
+def load_checkpoint(directory: str, rank: int, world: int, device="cpu", rng: bool = False) -> tuple:
+    """Load this rank's view of a checkpoint: its own shard when the world size matches;
+    otherwise every shard, merged by partition id with the FIRST copy of a duplicated id
+    kept (a checkpoint never holds two different values of one id, so nothing may be
+    combined — combining would multiply replicated partitions), partitions sorted by id;
+    the caller keeps the ids it owns under its partitioner. ``rng`` restores the saved RNG
+    state."""
     with open(os.path.join(directory, "manifest.json")) as f:
         man = json.load(f)
+    rep = set(man.get("replicated", []))
     out = {}
     for name, files in man["tables"].items():
-        if man["world"] == world:
+        if name in rep:
+            out[name] = load_table(os.path.join(directory, files[0]), device)
+        elif man["world"] == world:
             out[name] = load_table(os.path.join(directory, files[rank]), device)
-        else:  # re-shard: every rank loads all shards; caller regroups with its partitioner
-            merged = None
+        else:  # re-shard: every rank loads all shards
+            parts: Dict[int, Partition] = {}
+            first = None
             for fn in files:
                 t = load_table(os.path.join(directory, fn), device)
-                if merged is None:
-                    merged = Table(t.table_id, t.combiner)
+                first = first or t
                 for p in t.get_partitions():
-                    merged.add_partition(p)
-            out[name] = merged
+                    parts.setdefault(p.id(), p)
+            ids = sorted(parts)
+            if isinstance(first, PackedTable) and ids:
+                out[name] = PackedTable(ids, torch.stack([parts[i].get() for i in ids]), table_id=first.table_id,
+                                        combiner=first.combiner)
+            else:
+                merged = Table(first.table_id if first is not None else 0, first.combiner if first is not None else None)
+                for i in ids:
+                    merged.insert_partition(parts[i])
+                out[name] = merged
+    if rng:
+        restore_rng(man)
     return man, out
+
+
+class Checkpointer:
+    """Periodic application checkpoints: ``<dir>/it-<iter>/`` (per-rank ``.hpt`` files +
+    manifest) and a ``<dir>/LATEST`` pointer that rank 0 replaces atomically once every
+    rank's shard is on disk, so a restart never sees a half-written step."""
+
+    def __init__(self, directory: str, comm, every: int = 0):
+        self.directory = directory
+        self.comm = comm
+        self.every = int(every or 0)
+
+    @property
+    def enabled(self) -> bool:
+        return bool(self.directory)
+
+    def due(self, it: int) -> bool:
+        return self.enabled and self.every > 0 and (it + 1) % self.every == 0
+
+    def save(self, it: int, tables: Dict[str, Table], extra: Optional[dict] = None,
+             replicated: Sequence[str] = ()) -> str:
+        sub = os.path.join(self.directory, f"it-{it:06d}")
+        save_checkpoint(sub, tables, self.comm.rank, self.comm.world_size, it, extra=extra, comm=self.comm,
+                        replicated=replicated)
+        if self.comm.rank == 0:
+            tmp = os.path.join(self.directory, "LATEST.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"dir": os.path.basename(sub), "iteration": it}, f)
+            os.replace(tmp, os.path.join(self.directory, "LATEST"))
+        self.comm.barrier()  # no rank runs ahead of a LATEST that may still point back
+        return sub
+
+    def load_latest(self, device="cpu", rng: bool = False):
+        """``(manifest, tables)`` of the newest complete checkpoint, or None."""
+        if not self.enabled:
+            return None
+        latest = os.path.join(self.directory, "LATEST")
+        if not os.path.exists(latest):
+            return None
+        with open(latest) as f:
+            sub = os.path.join(self.directory, json.load(f)["dir"])
+        return load_checkpoint(sub, self.comm.rank, self.comm.world_size, device=device, rng=rng)
+
+
+def tensor_table(t: torch.Tensor, ids=None, table_id: int = 0) -> PackedTable:
+    """Wrap a tensor as a packed table (row i = partition ``ids[i]``, default 0..n-1)."""
+    if t.dim() == 0:
+        t = t.reshape(1)
+    ids = list(range(t.shape[0])) if ids is None else [int(i) for i in (ids.tolist() if torch.is_tensor(ids) else ids)]
+    return PackedTable(ids, t, table_id=table_id, combiner=ArrCombiner(Operation.SUM))
+
+
+def blob_table(t: torch.Tensor, table_id: int = 0) -> Table:
+    """A whole tensor as ONE partition (id 0) — for per-rank state such as token topics."""
+    tab = Table(table_id, ArrCombiner(Operation.SUM))
+    tab.add(0, t)
+    return tab

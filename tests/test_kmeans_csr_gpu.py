@@ -44,3 +44,16 @@ def test_kmeans_sparse_gpu_equals_cpu(cuda):
     assert all(abs(a - b) <= 1e-9 * abs(b) for a, b in zip(out["objective"], ref["objective"]))
     coo = M.kmeans_sparse(X.to_sparse().to(cuda), C0, 6)  # COO input takes the same kernel
     assert torch.allclose(coo["centroids"].cpu(), ref["centroids"], atol=1e-10)
+
+
+def test_nan_row_gets_a_valid_label(cuda):
+    """a row whose every distance is NaN must not scatter to cluster INT_MAX."""
+    X = _sparse(300, 40, 0.3, 3)
+    X[7, 3] = float("nan")
+    C = torch.rand(9, 40, dtype=torch.float64, generator=torch.Generator().manual_seed(2))
+    A = KC.to_device_csr(X.to_sparse_csr().to(cuda))
+    lab, m, S, cnt = KC.assign_accumulate(A, C.to(cuda))
+    torch.cuda.synchronize()
+    lab = lab.cpu()
+    assert int(lab.min()) >= 0 and int(lab.max()) < 9
+    assert float(cnt.sum()) == 300.0
