@@ -125,6 +125,8 @@ def bench_kmeans(args, comm, torch):
     elapsed = reduce_max(comm, torch, elapsed)
     sec_per_iter = elapsed / args.steps
     # objective after timing (one extra assign pass, outside the timed region) as a sanity value
+    if args.strategy == "rotation":  # the model lives in rotating blocks: gather it first
+        m.op = K.prepare(m._rotation_gather().contiguous(), m.dp)
     _, obj = K.assign(m.X, m.op, sums=None, want_objective=True, variant=cfg.variant)
     o = obj.reshape(1).to(comm.device, torch.float64)
     if P > 1:

@@ -133,6 +133,8 @@ class PackedTable(Table):
         self.buffer = buffer
         self._ids = ids_l
         self._row = {pid: i for i, pid in enumerate(ids_l)}
+        self.version = 0  # bumped on every id-layout change (cached comm plans key on it)
+        self._ids_hash = None
         self._rebuild_parts()
 
     # construction helpers
@@ -167,6 +169,18 @@ class PackedTable(Table):
 
     def _rebuild_parts(self) -> None:
         self._parts_cache = None
+        self.version = getattr(self, "version", 0) + 1
+        self._ids_hash = None
+
+    def ids_hash(self) -> int:
+        """crc32 of the id list (int64 little-endian), cached per layout version."""
+        if self._ids_hash is None:
+            import zlib
+
+            import numpy as np
+
+            self._ids_hash = zlib.crc32(np.asarray(self._ids, dtype=np.int64).tobytes()) & 0x7FFFFFFF
+        return self._ids_hash
 
     def __len__(self) -> int:
         return len(self._ids)

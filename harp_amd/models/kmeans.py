@@ -333,36 +333,40 @@ class KMeansCollectiveMapper(CollectiveMapper):
                 raise IOError("broadcast failed")
             return ct.buffer
         if s == "push_pull":
-            # global table: each worker owns a block of centroid ids (zeros each iteration)
-            P, me = self.get_num_workers(), self.get_self_id()
-            mine = [i for i in ids if part.get_worker_id(i) == me]
-            glob = Table(1, sumop)
-            for i in mine:
-                glob.add(i, torch.zeros(sums.shape[1], dtype=sums.dtype, device=sums.device))
-            local = Table(2, sumop)
-            for i in range(k):
-                local.add(i, sums[i])
-            if not self.push("main", f"push-{it}", local, glob, part):
+            # parameter-server sync (KMeansDaalCollectiveMapper.java:504-530): push the partial
+            # sums to the owners of a distributed global table, average there, pull every
+            # centroid back. Packed tables + cached comm plans: push = one all-to-all-v into
+            # the owner slabs, pull = one all-gather (every worker wants every id).
+            st = self._pp_tables(sums, c, part, ids)
+            st["glob"].buffer.zero_()
+            if not self.push("main", f"push-{it}", st["local"], st["glob"], part):
                 raise IOError("push failed")
-            for p in glob.get_partitions():
-                row = p.get()
-                cnt = row[d]
-                if float(cnt) > 0:
-                    row[:d] /= cnt
-                    row[d] = 1.0
-                else:
-                    row[:d] = c[p.id()]
-                    row[d] = 1.0
-            pulled = Table(3, sumop)
-            for i in range(k):
-                pulled.add(i, torch.zeros(sums.shape[1], dtype=sums.dtype, device=sums.device))
-            if not self.pull("main", f"pull-{it}", pulled, glob, True):
+            K.normalize(st["glob"].buffer, st["cglob"].buffer, d)  # average at the owner
+            st["pulled"].buffer.zero_()  # pull combines into the local rows (callers zero them)
+            if not self.pull("main", f"pull-{it}", st["pulled"], st["cglob"], True):
                 raise IOError("pull failed")
-            newc = c.clone()
-            for i in range(k):
-                newc[i] = pulled[i][:d]
-            return newc
+            c.copy_(st["pulled"].buffer)
+            return c
         raise ValueError(s)
+
+    def _pp_tables(self, sums, c, part, ids) -> dict:
+        """Persistent packed tables of the push_pull strategy (static layouts)."""
+        st = getattr(self, "_pp", None)
+        if st is not None and st["sums"] is sums and st["c"] is c:
+            return st
+        me = self.get_self_id()
+        mine = [i for i in ids if part.get_worker_id(i) == me]
+        lo = mine[0] if mine else 0
+        st = {"sums": sums, "c": c,
+              "local": PackedTable(ids, sums, combiner=self.sumop),
+              "glob": PackedTable(mine, torch.zeros((len(mine), sums.shape[1]), dtype=sums.dtype, device=sums.device),
+                                  combiner=self.sumop),
+              "cglob": PackedTable(mine, c[lo:lo + len(mine)], combiner=self.sumop),
+              "pulled": PackedTable(ids, torch.zeros_like(c), combiner=self.sumop)}
+        for t in ("local", "glob", "cglob", "pulled"):
+            st[t].static_layout = True
+        self._pp = st
+        return st
 
     # -- model rotation (ml/java kmeans/rotation) ------------------------------------------
     def _rotation_init(self) -> None:

@@ -31,6 +31,10 @@ Implementation (not a translation of the reference's socket algorithms):
   the reference's S*log2 P full-table exchange), regroup -> ``ncclReduceScatter`` over the
   owner-sorted slab, allgather -> ``ncclAllGather``, reduce -> ``ncclReduce``,
   broadcast -> ``ncclBroadcast``, rotate -> grouped ``ncclSend/ncclRecv``.
+* **Planned dense push / pull / regroup** — :mod:`.plans` keeps the routing of a
+  (local, global, partitioner) layout as device index tensors: push = index_select + one
+  all-to-all-v + index_add; pull = a padded all-gather of the ids every worker wants
+  (the reference's broadcast case) + one all-to-all-v for the rest.
 * **Generic path** — heterogeneous partitions (different ids/shapes, Writables, KV maps,
   non-RCCL combiners such as MINUS) are encoded with :mod:`.codec` into one uint8 device
   buffer and moved with a single variable-size all-gather / all-to-all-v / p2p exchange
@@ -51,6 +55,7 @@ import torch
 from ..core.combiner import PartitionCombiner
 from ..core.partition import UNKNOWN_WORKER_ID, Partition, PartitionFunction, Partitioner
 from ..core.table import PackedTable, Table
+from . import plans
 from .codec import encode_partitions, pack_message, unpack_message
 from .comm import Communicator
 
@@ -289,23 +294,18 @@ def regroup(comm: Communicator, table: Table, partitioner: Optional[Partitioner]
     partitioner = partitioner or Partitioner(P)
     if same_layout(comm, table) and _is_dense_combiner(table.combiner):
         ids = table.ids
-        owners = _owners(partitioner, ids)
-        if all(0 <= o < P for o in owners):
-            per = [[i for i, o in enumerate(owners) if o == r] for r in range(P)]
-            mx = max(len(x) for x in per)
+        plan = plans.regroup_plan(table, partitioner, P)  # cached per layout version
+        if plan is not None:
+            per, mx = plan.per, plan.mx
             buf = table.buffer
             if buf.device != comm.device:
                 buf = buf.to(comm.device)
             if mx == 0:
                 return True
-            order = []
-            for r in range(P):
-                order += per[r] + [-1] * (mx - len(per[r]))
-            if order == list(range(len(ids))) and mx * P == len(ids):
+            if plan.idx is None:
                 slab = buf.contiguous()
             else:
-                idx = torch.tensor([max(i, 0) for i in order], dtype=torch.long, device=buf.device)
-                slab = buf.index_select(0, idx)
+                slab = buf.index_select(0, plan.idx.to(buf.device))
             out = torch.empty((mx,) + table.part_shape, dtype=buf.dtype, device=buf.device)
             comm.reduce_scatter(out, slab, table.combiner.operation.rccl_op)
             mine = per[comm.rank]
@@ -381,6 +381,9 @@ def push(comm: Communicator, local: Table, global_table: Table, partitioner: Opt
     owner when no worker holds the id yet. The local table is unchanged."""
     P = comm.world_size
     partitioner = partitioner or Partitioner(P)
+    if plans.dense_pair(comm, local, global_table):
+        plans.push_dense(comm, local, global_table, partitioner)
+        return True
     owner: Dict[int, int] = {}
     for r, ids in enumerate(_id_sets(comm, global_table)):
         for i in ids:
@@ -416,6 +419,9 @@ def pull(comm: Communicator, local: Table, global_table: Table, use_bcast: bool 
     table is unchanged (callers zero the local partitions first, as the reference's
     K-means does at KMeansDaalCollectiveMapper.java:527-529)."""
     P = comm.world_size
+    if plans.dense_pair(comm, local, global_table):
+        plans.pull_dense(comm, local, global_table, use_bcast)
+        return True
     owner: Dict[int, int] = {}
     for r, ids in enumerate(_id_sets(comm, global_table)):
         for i in ids:

@@ -137,8 +137,9 @@ class CollectiveMapper:
     # -- collectives ------------------------------------------------------------------------
     def _timed(self, ctx: str, op: str, kind: str, fn, *a, **kw):
         """Run one collective, recording its bytes (this rank's table payload before the
-        call) and its stream time (HIP events around it on the current stream)."""
-        nbytes = table_nbytes(a[0]) if a and isinstance(a[0], Table) else 0
+        call; 0 on a 1-worker job, where nothing moves) and its stream time (HIP events
+        around it on the current stream)."""
+        nbytes = table_nbytes(a[0]) if a and isinstance(a[0], Table) and self.comm.world_size > 1 else 0
         with self.metrics.time_collective(kind, ctx, op, nbytes, self.comm.device):
             ok = fn(self.comm, *a, **kw)
         return ok

@@ -1,0 +1,157 @@
+"""Multi-GPU RCCL tests: self-activate when >= 2 HIP devices are visible (skip otherwise).
+
+One process per GPU (``launch(..., backend="nccl")``), P = 2, 3 (odd) and
+min(device_count, 8). Covers what the gloo tests cannot: device tensors through RCCL, a
+``dist.new_group`` per rotation channel whose first op is a grouped send/recv, the
+device-side stream wait of ``DeviceRotator.get``, K-means / MF-SGD P-invariance on the
+GPU path, the RCCL watchdog turning a hung peer into a failed collective + gang restart,
+and ``bench.py --gpus P`` spawning its own RCCL ranks.
+
+Reference concurrency contract: ml/java/.../dymoro/Rotator.java:43-71 (one rotation
+thread per slice = one communicator per slice here)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from harp_amd.runtime.launcher import launch
+
+pytestmark = pytest.mark.gpu
+
+NGPU = torch.cuda.device_count() if torch.cuda.is_available() else 0
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P_LIST = sorted({p for p in (2, 3, min(NGPU, 8)) if 2 <= p <= NGPU}) or [2]
+need2 = pytest.mark.skipif(NGPU < 2, reason=f"needs >= 2 GPUs ({NGPU} visible)")
+
+
+def _battery(comm):
+    from tests.mp_checks import collective_battery
+
+    assert comm.backend == "nccl" and comm.device.type == "cuda"
+    return collective_battery(comm)
+
+
+@need2
+@pytest.mark.parametrize("P", P_LIST)
+def test_collective_battery_over_rccl(P):
+    res = launch(_battery, P, backend="nccl", timeout=300)
+    for r, checks in enumerate(res):
+        bad = {k: v for k, v in checks.items() if v is not True}
+        assert not bad, f"rank {r}: {bad}"
+
+
+def _rotator(comm, rounds):
+    from harp_amd.runtime.dymoro import DeviceRotator
+
+    P, me = comm.world_size, comm.rank
+    slabs = [torch.full((1000, 64), float(me * 10 + k), device=comm.device) for k in range(2)]
+    rot = DeviceRotator(comm, slabs, name="t")
+    ring = [(r + 1) % P for r in range(P)]
+    seen = []
+    for s in range(rounds):
+        for k in range(2):
+            x = rot.get(k)
+            seen.append(float(x[0, 0]))
+            x.add_(1000.0)  # compute on the resident slab before it moves on
+            rot.start(k, ring)
+    rot.wait_all()
+    return seen, [float(rot.get(k)[5, 7]) for k in range(2)]
+
+
+@need2
+@pytest.mark.parametrize("P", P_LIST)
+def test_device_rotator_ring_round_trip(P):
+    res = launch(_rotator, P, args=(P,), backend="nccl", timeout=300)
+    for me, (seen, final) in enumerate(res):
+        for s in range(P):
+            src = (me - s) % P  # slab resident at step s came from rank me - s
+            for k in range(2):
+                assert seen[2 * s + k] == src * 10 + k + 1000.0 * s
+        # after P hops every slab is home, touched once by every rank
+        assert final == [me * 10 + k + 1000.0 * P for k in range(2)]
+
+
+def _kmeans(comm, strategy, x, c0):
+    from harp_amd.models.kmeans import KMeansConfig, run_kmeans
+
+    P, r = comm.world_size, comm.rank
+    n = x.shape[0]
+    cfg = KMeansConfig(num_points=n // P, num_centroids=c0.shape[0], dim=x.shape[1], iterations=3, strategy=strategy)
+    return run_kmeans(comm, cfg, points=x[r * n // P:(r + 1) * n // P], init_centroids=c0)
+
+
+@need2
+@pytest.mark.parametrize("strategy", ["allreduce", "regroup_allgather", "bcast_reduce", "push_pull", "rotation"])
+def test_kmeans_strategies_match_one_rank(strategy):
+    P = P_LIST[-1]
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand((P * 4096, 32), generator=g) * 100
+    c0 = x[:300].clone()
+    one = launch(_kmeans, 1, args=("allreduce", x, c0), backend="nccl", timeout=300)[0]
+    res = launch(_kmeans, P, args=(strategy, x, c0), backend="nccl", timeout=300)
+    assert res[0]["objective"] == pytest.approx(one["objective"], rel=2e-4)
+    assert torch.allclose(res[0]["centroids"], one["centroids"], rtol=1e-3, atol=0.05)
+
+
+def _sgd(comm, tr):
+    from harp_amd.models.sgd_mf import SGDConfig, SGDCollectiveMapper
+    from harp_amd.runtime.mapper import KeyValReader
+
+    m = SGDCollectiveMapper(comm, SGDConfig(rank=32, epochs=4, test_every=2), 5000, 900, tr, None)
+    m.run(KeyValReader([]))
+    return m.rmse_history, m.trained
+
+
+@need2
+@pytest.mark.parametrize("P", P_LIST)
+def test_sgd_rotation_trained_count_and_rmse(P):
+    from harp_amd.models.sgd_mf import synthetic_ratings
+
+    tr = synthetic_ratings(5000, 900, 200_000, seed=1)
+    one = launch(_sgd, 1, args=(tr,), backend="nccl", timeout=300)[0]
+    res = launch(_sgd, P, args=(tr,), backend="nccl", timeout=300)
+    assert sum(t for _, t in res) == one[1] == 4 * 200_000
+    rm_p, rm_1 = res[0][0][-1][1], one[0][-1][1]
+    assert rm_p == pytest.approx(rm_1, rel=0.05)  # Hogwild order differs; the fit must not
+    assert rm_p < res[0][0][0][1]
+
+
+def _hang_then_resume(comm, d):
+    from harp_amd.models.kmeans import KMeansConfig, run_kmeans
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand((4096, 16), generator=g)
+    P, r = comm.world_size, comm.rank
+    cfg = KMeansConfig(num_points=4096 // P, num_centroids=64, dim=16, iterations=6, strategy="allreduce",
+                       checkpoint_dir=str(d), checkpoint_every=1)
+    return run_kmeans(comm, cfg, points=x[r * 4096 // P:(r + 1) * 4096 // P], init_centroids=x[:64].clone())
+
+
+@need2
+def test_rccl_watchdog_fails_the_gang_and_restart_resumes(tmp_path):
+    """A rank stuck past HARP_DATA_MAX_WAIT_TIME: the survivors' RCCL collective times out
+    (torch's NCCL watchdog aborts the communicator), the gang is stopped, and the job is
+    restarted in FRESH processes that resume from the last checkpoint."""
+    env = {"HARP_FAULT": "rank=1,iter=2,kind=hang,seconds=90", "HARP_DATA_MAX_WAIT_TIME": "10",
+           "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1"}
+    res = launch(_hang_then_resume, 2, args=(tmp_path,), backend="nccl", timeout=240, retries=1, env=env, grace_s=5)
+    assert res[0]["start_iteration"] == 2
+    ref = launch(_hang_then_resume, 2, args=(tmp_path / "ref",), backend="nccl", timeout=240)
+    assert torch.allclose(res[0]["centroids"], ref[0]["centroids"], atol=1e-5)
+
+
+@need2
+def test_bench_spawns_rccl_ranks():
+    P = P_LIST[-1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(P), "--points", "4e6",
+                        "--steps", "3", "--warmup", "1", "--sgd-ratings", "4000000", "--sgd-epochs", "2"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == P and rec["config"]["parallelism"] == f"dp{P}"
+    assert rec["collectives"]["allreduce"]["bytes"] > 0
+    assert rec["sgd"]["updates_per_sec"] > 0

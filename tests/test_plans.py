@@ -1,0 +1,114 @@
+"""Planned dense push / pull / regroup (harp_amd/parallel/plans.py) vs the generic
+per-partition path, on 1..4 gloo ranks. Semantics (LocalGlobalSyncCollective.java:
+456-698): push combines local rows into the owner's global row (ids nobody owns go to the
+partitioner's owner as new partitions), local unchanged; pull combines the owner's global
+row into every requesting local row, global unchanged; ids every worker requests take
+the broadcast (all-gather) route."""
+import pytest
+import torch
+
+from harp_amd.core import ArrCombiner, Operation, PackedTable, Partitioner, Table
+from harp_amd.parallel import collectives as C
+from harp_amd.parallel import plans
+from harp_amd.runtime.launcher import launch
+
+
+def _tables(r, P, op, packed):
+    comb = ArrCombiner(op)
+    # global: rank r owns ids r, r+P, ... < 12 (ids 12..14 owned by nobody)
+    gids = list(range(r, 12, P))
+    gbuf = torch.stack([torch.full((3,), float(10 * i + 1)) for i in gids]) if gids else torch.zeros(0, 3)
+    # local: every rank wants 0..5 (all-wanted) + a rank-specific sparse set incl. unowned ids
+    lids = list(range(6)) + [6 + r, 9 + (r % 2), 12 + (r % 3)]
+    lids = sorted(set(lids))
+    lbuf = torch.stack([torch.full((3,), float(r + 1) * (1 + (i % 3))) for i in lids])
+    if packed:
+        g = PackedTable(gids, gbuf.clone(), combiner=comb)
+        l = PackedTable(lids, lbuf.clone(), combiner=comb)
+    else:
+        g, l = Table(1, comb), Table(2, comb)
+        for i, row in zip(gids, gbuf):
+            g.add(i, row.clone())
+        for i, row in zip(lids, lbuf):
+            l.add(i, row.clone())
+    return l, g
+
+
+def _dump(t):
+    return {i: t[i].clone() for i in t.sorted_ids()}
+
+
+def _job(comm, op_name, repeat):
+    op = Operation[op_name]
+    P, r = comm.world_size, comm.rank
+    out = {}
+    for packed in (True, False):
+        l, g = _tables(r, P, op, packed)
+        lbefore = _dump(l)
+        for _ in range(repeat):  # second call reuses the cached plan
+            assert C.push(comm, l, g, Partitioner(P))
+        pushed = _dump(g)
+        assert all(torch.equal(lbefore[i], l[i]) for i in lbefore), "push changed the local table"
+        want = PackedTable(l.ids, torch.zeros_like(l.buffer), combiner=ArrCombiner(op)) if packed else Table(3, ArrCombiner(op))
+        if not packed:
+            for i in l.sorted_ids():
+                want.add(i, torch.zeros(3))
+        gbefore = _dump(g)
+        assert C.pull(comm, want, g, True)
+        assert all(torch.equal(gbefore[i], g[i]) for i in gbefore), "pull changed the global table"
+        out[packed] = (pushed, _dump(want))
+    return out
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4])
+@pytest.mark.parametrize("op_name", ["SUM", "MAX"])
+def test_dense_push_pull_match_generic(P, op_name):
+    res = launch(_job, P, args=(op_name, 2 if op_name == "MAX" else 1), timeout=300)
+    for r, out in enumerate(res):
+        (pd, ld), (pg, lg) = out[True], out[False]
+        assert sorted(pd) == sorted(pg), (r, sorted(pd), sorted(pg))
+        for i in pd:
+            assert torch.allclose(pd[i], pg[i]), (r, i, pd[i], pg[i])
+        assert sorted(ld) == sorted(lg)
+        for i in ld:
+            assert torch.allclose(ld[i], lg[i]), (r, i, ld[i], lg[i])
+
+
+def _plan_reuse(comm):
+    P, r = comm.world_size, comm.rank
+    comb = ArrCombiner(Operation.SUM)
+    g = PackedTable(list(range(r, 20, P)), torch.zeros(len(range(r, 20, P)), 4), combiner=comb)
+    l = PackedTable(list(range(20)), torch.ones(20, 4), combiner=comb)
+    g.static_layout = l.static_layout = True
+    calls = []
+    orig = comm.all_gather_ints
+
+    def spy(v):
+        calls.append(len(v))
+        return orig(v)
+
+    comm.all_gather_ints = spy
+    for _ in range(3):
+        g.buffer.zero_()
+        C.push(comm, l, g, Partitioner(P))
+    n_first = len(calls)
+    for _ in range(5):
+        g.buffer.zero_()
+        C.push(comm, l, g, Partitioner(P))
+    return n_first, len(calls), g.buffer.sum().item()
+
+
+def test_static_plan_has_no_per_call_metadata_exchange():
+    res = launch(_plan_reuse, 2, timeout=120)
+    for n_first, n_all, s in res:
+        assert n_all == n_first  # 5 more pushes: zero extra metadata collectives
+    assert sum(s for _, _, s in res) == 2 * 20 * 4
+
+
+def test_combine_rows_ops():
+    d = torch.zeros(3, 2)
+    plans.combine_rows(d, torch.tensor([0, 0, 2]), torch.tensor([[1., 2], [3, 4], [5, 6]]), "SUM")
+    assert d.tolist() == [[4, 6], [0, 0], [5, 6]]
+    m = torch.full((2, 2), -float("inf"))
+    plans.combine_rows(m, torch.tensor([1, 1]), torch.tensor([[1., 7], [3, 4]]), "MAX")
+    assert m[1].tolist() == [3, 7]
