@@ -52,13 +52,14 @@ _lib.register({
 
 MT = 128  # SYRK macro tile (features)
 KT = 64   # samples per SYRK stage
+LD_ALIGN = 192  # sample padding: a multiple of every SYRK stage length (64, 48)
 
 
 class FeatureMajor:
     """Feature-major bf16 copy of a data block for the MFMA SYRK: ``XT [d_pad, ld]`` with
     samples contiguous, a row of ones at index ``d`` (so G[:, d] = column sums and
     G[d, d] = n), zero padding to ``d_pad = round_up(d + 1, 128)`` features and
-    ``ld = round_up(n, 64)`` samples."""
+    ``ld = round_up(n, 192)`` samples (whole 64- and 48-sample kernel stages)."""
 
     def __init__(self, XT: torch.Tensor, n: int, d: int):
         self.XT, self.n, self.d = XT, n, d
@@ -73,7 +74,7 @@ class FeatureMajor:
 
     @staticmethod
     def dims(n: int, d: int):
-        return (d + 1 + MT - 1) // MT * MT, (n + KT - 1) // KT * KT
+        return (d + 1 + MT - 1) // MT * MT, (n + LD_ALIGN - 1) // LD_ALIGN * LD_ALIGN
 
     @classmethod
     def from_rows(cls, X: torch.Tensor) -> "FeatureMajor":

@@ -21,7 +21,7 @@ def test_gram_stats_matches_fp64(cuda, n, d):
 
 def test_feature_major_uniform_and_cov(cuda):
     fm = LA.FeatureMajor.uniform(50000, 64, 0.0, 1.0, seed=3, device=cuda)
-    assert fm.XT.shape == (128, 50048)
+    assert fm.XT.shape == (128, 50112)  # samples padded to a multiple of 192
     cnt, s, G = LA.gram_stats(fm)
     n = cnt.item()
     mean = s.double() / n
