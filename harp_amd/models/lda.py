@@ -42,6 +42,8 @@ class LDAConfig:
     checkpoint_dir: str = ""  # .hpt checkpoints (token topics, doc-topic, resident word slices)
     checkpoint_every: int = 0  # iterations between checkpoints (0: never)
     model_dir: str = ""       # word-model dumps every print_interval*10 iterations + at the end
+    time_budget_ms: float = 0.0  # >0: time-bounded rotation steps (LDAMPCollectiveMapper timer); 0: full sweeps
+    budget_pieces: int = 8    # launches a step's word chunks are cut into
 
 
 def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, seed: int = 0, device="cpu"):
@@ -142,7 +144,11 @@ class LDACollectiveMapper(CollectiveMapper):
                 slab = self.rot.get(k)
                 gs = block * S + k
                 a, b = self.offsets[gs], self.offsets[gs + 1]
-                if b > a:
+                if b > a and cfg.time_budget_ms > 0:
+                    m, delta_total = self._budget_step(gs, slab, delta_total, it, s, k)
+                    nk_view = self.nk + delta_total
+                    n += m
+                elif b > a:
                     d = L.cgs_sample(self.tdoc[a:b], self.tword[a:b], self.tz[a:b], self.chunks[gs], self.ndk, slab,
                                      nk_view, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
                                      (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ k, self.doc_index,
@@ -159,6 +165,43 @@ class LDACollectiveMapper(CollectiveMapper):
             dt = delta_total
         self.nk += dt
         return n
+
+    def _budget_step(self, gs: int, slab, delta_total, it: int, s: int, k: int):
+        """Sample slice ``gs`` for at most the step budget, in pieces of consecutive word
+        chunks; a per-slice chunk cursor makes the next visit continue where the budget
+        cut this one (tokens not reached keep their topic for this iteration)."""
+        from ..runtime.dymoro import StepBudget
+
+        cfg = self.cfg
+        if getattr(self, "budget", None) is None:
+            self.budget = StepBudget(cfg.time_budget_ms / 1e3, self.device)
+            self._chunk_cursor = {}
+            self._chunks_host = {}
+        ch = self.chunks[gs]
+        chh = self._chunks_host.get(gs)
+        if chh is None:
+            chh = self._chunks_host[gs] = ch.cpu().tolist()
+        nch = len(chh) - 1
+        per = max(1, math.ceil(nch / max(1, cfg.budget_pieces)))
+        a = self.offsets[gs]
+        state = {"delta": delta_total, "j": 0}
+
+        def piece():
+            c0 = self._chunk_cursor.get(gs, 0)
+            c1 = min(c0 + per, nch)
+            self._chunk_cursor[gs] = c1 % nch
+            t0, t1 = a + chh[c0], a + chh[c1]
+            sub = ch[c0:c1 + 1] - chh[c0]
+            tpos = self.doc_index.tpos[t0:t1] if self.doc_index is not None else None
+            d = L.cgs_sample(self.tdoc[t0:t1], self.tword[t0:t1], self.tz[t0:t1], sub, self.ndk, slab,
+                             self.nk + state["delta"], cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
+                             (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ (k << 4) ^ state["j"], self.doc_index, tpos)
+            state["delta"] = state["delta"] + d
+            state["j"] += 1
+            return t1 - t0
+
+        n, _ = self.budget.run(piece for _ in range(max(1, cfg.budget_pieces)) if nch)
+        return n, state["delta"]
 
     def log_likelihood(self, it: int) -> float:
         """Full joint log-likelihood (word + doc parts), each slice counted once: at step

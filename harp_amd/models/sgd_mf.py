@@ -24,7 +24,8 @@ from typing import List, Optional, Tuple
 import torch
 
 from ..ops import mf as MF
-from ..runtime.dymoro import DeviceRotator, RotationSchedule, create_rotation_order, get_rotation_sequences
+from ..runtime.dymoro import (DeviceRotator, RotationSchedule, StepBudget, create_rotation_order,
+                              get_rotation_sequences, tune_budget)
 from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
 
 
@@ -47,6 +48,9 @@ class SGDConfig:
     checkpoint_dir: str = ""   # .hpt checkpoints (W rows + resident H slices); resume on restart
     checkpoint_every: int = 0  # epochs between checkpoints (0: never)
     model_dir: str = ""        # final text dump: W-<worker>, H-<worker>, evaluation
+    time_budget_ms: float = 0.0  # >0: time-bounded rotation steps (Scheduler timer); 0: deterministic
+    budget_pieces: int = 8     # launches a step's work is cut into (budget granularity)
+    tune_ratio: float = 0.0    # >0: after epoch 0 retune the budget so an epoch trains this fraction
 
 
 def load_mm(path: str) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -219,7 +223,9 @@ class SGDCollectiveMapper(CollectiveMapper):
                 slab = self.rot.get(k)
                 gs = block * S + k
                 with timer.phase("compute"):
-                    if cfg.xcd_blocks:
+                    if cfg.time_budget_ms > 0:
+                        n += self._budget_step(gs, slab)
+                    elif cfg.xcd_blocks:
                         r_, c_, v_, off, hoff = self.train.get_cells(gs)
                         win = MF.cell_windows(hoff, cfg.train_fraction, epoch) if cfg.train_fraction < 1.0 else None
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
@@ -232,7 +238,50 @@ class SGDCollectiveMapper(CollectiveMapper):
                 with timer.phase("rotate"):
                     self.rot.start(k, self.schedule.rotation_map(epoch, s))
         self.trained += n
+        if cfg.time_budget_ms > 0 and cfg.tune_ratio > 0 and epoch == 0:
+            total = torch.tensor([float(self.train.n)], dtype=torch.float64, device=self.device)
+            if P > 1:
+                self.comm.all_reduce(total)
+            new = tune_budget(self, self.budget.compute_s, n, int(total.item()), P * S, cfg.tune_ratio, "sgd", epoch)
+            self.budget.budget_s = new
+            self.budget_history.append(new)
         return n
+
+    def _budget_step(self, gs: int, slab: torch.Tensor) -> int:
+        """Train slice ``gs`` for at most the step budget: successive windows of every
+        cell (per-cell cursors persist across visits, so later visits continue where the
+        budget cut the previous one)."""
+        cfg = self.cfg
+        if getattr(self, "budget", None) is None:
+            self.budget = StepBudget(cfg.time_budget_ms / 1e3, self.device)
+            self.budget_history = [self.budget.budget_s]
+            self._cursor = {}
+        if cfg.xcd_blocks:
+            r_, c_, v_, off, hoff = self.train.get_cells(gs)
+            sizes = [hoff[c + 1] - hoff[c] for c in range(len(hoff) - 1)]
+        else:
+            r_, c_, v_ = self.train.get(gs)
+            sizes = [r_.numel()]
+        cur = self._cursor.setdefault(gs, [0] * len(sizes))
+        P = max(1, cfg.budget_pieces)
+        lens = [math.ceil(m / P) if m else 0 for m in sizes]
+
+        def piece():
+            starts = list(cur)
+            for c, m in enumerate(sizes):
+                if m:
+                    cur[c] = (cur[c] + lens[c]) % m
+            L = [min(lens[c], sizes[c]) for c in range(len(sizes))]
+            if cfg.xcd_blocks:
+                return MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
+                                             cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
+                                             window=(starts, L))
+            a, m = starts[0], L[0]
+            idx = (torch.arange(a, a + m, device=r_.device) % max(sizes[0], 1)) if m else None
+            return MF.sgd_update(r_[idx], c_[idx], v_[idx], self.W, slab, cfg.lr, cfg.lam, cfg.chunk) if m else 0
+
+        items, _ = self.budget.run(piece for _ in range(P))
+        return items
 
     def map_collective(self, reader: KeyValReader, context: Context) -> None:
         self.init_model(reader)

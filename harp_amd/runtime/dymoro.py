@@ -212,6 +212,64 @@ class Rotator:
         self._pool.shutdown(wait=True)
 
 
+# ---------------------------------------------------------------- time-bounded steps
+class StepBudget:
+    """Time-bounded rotation step on the GPU (the reference's Scheduler timer,
+    Scheduler.java:118-137: blocks are submitted until a TimerTask fires, so every worker
+    rotates after ``time`` ms whatever its share of work).
+
+    A step's work is cut into ``pieces`` (kernel launches over successive windows of the
+    data, so the cut falls on kernel boundaries); pieces are issued one ahead of the
+    device: before issuing piece i+1 the host waits for piece i-1's completion event,
+    then stops issuing once ``budget_s`` has elapsed since the step began. The device
+    never idles between pieces, and at most one piece runs past the budget. On the CPU
+    the pieces run synchronously and the clock is checked after each one."""
+
+    def __init__(self, budget_s: float, device: torch.device):
+        self.budget_s = float(budget_s)
+        self.device = device
+        self.compute_s = 0.0  # accumulated step time (for the tuner)
+
+    def run(self, pieces) -> Tuple[int, int]:
+        """``pieces``: iterable of zero-arg callables returning items trained. Returns
+        (items, pieces run)."""
+        gpu = self.device.type == "cuda"
+        t0 = time.perf_counter()
+        items, n, prev = 0, 0, None
+        for piece in pieces:
+            if n and time.perf_counter() - t0 >= self.budget_s:
+                break
+            items += int(piece())
+            n += 1
+            if gpu:
+                ev = torch.cuda.Event()
+                ev.record()
+                if prev is not None:
+                    prev.synchronize()  # piece n-1 done; piece n is running: the device stays busy
+                prev = ev
+        if prev is not None:
+            prev.synchronize()
+        self.compute_s += time.perf_counter() - t0
+        return items, n
+
+
+def tune_budget(mapper, compute_s: float, items: int, total_items: int, steps: int, ratio: float,
+                ctx: str = "sgd", it: int = 0) -> float:
+    """Reference adjustMiniBatch (SGDCollectiveMapper.java:623-668): all-gather every
+    worker's (compute time, items trained) of the first iteration, then size the per-step
+    budget so one iteration trains ``ratio`` of all items:
+    budget = ratio / (trained fraction) * (mean per-step compute time)."""
+    P = mapper.get_num_workers()
+    t = PackedTable([mapper.get_self_id()], torch.tensor([[compute_s, float(items)]], dtype=torch.float64,
+                                                         device=mapper.device), combiner=ArrCombiner(Operation.SUM))
+    if not mapper.allgather(ctx, f"allgather-compute-status-{it}", t):
+        raise IOError("allgather of compute status failed")
+    tot = t.buffer.sum(0).cpu().tolist()
+    frac = tot[1] / max(float(total_items), 1.0)
+    avg_step = tot[0] / P / max(steps, 1)
+    return ratio / max(frac, 1e-12) * avg_step
+
+
 # ---------------------------------------------------------------- 2-D block scheduler
 class BlockScheduler:
     """Conflict-free 2-D (row split x column split) block scheduler.

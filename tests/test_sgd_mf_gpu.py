@@ -181,3 +181,21 @@ def test_sgd_wide_rank_model_converges(cuda):
     res = run_sgd(Communicator(None, cuda), cfg, nu, ni, (u, i, v), (u[:5000], i[:5000], v[:5000]))
     rm = [x[2] for x in res["rmse"]]
     assert rm[-1] < rm[0], res["rmse"]
+
+
+def test_sgd_time_budget_xcd_path(cuda):
+    """Time-bounded steps on the XCD-blocked kernel: an unbounded budget trains every
+    rating each epoch, a tiny one exactly one piece (a window of every cell) per step."""
+    from harp_amd.models.sgd_mf import SGDConfig, SGDCollectiveMapper, synthetic_ratings
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    tr = synthetic_ratings(20000, 3000, 400_000, seed=3, device=cuda)
+    out = {}
+    for name, b in (("full", 1e9), ("tiny", 1e-6)):
+        cfg = SGDConfig(rank=32, epochs=2, test_every=0, time_budget_ms=b, budget_pieces=8)
+        m = SGDCollectiveMapper(Communicator(None, cuda), cfg, 20000, 3000, tr, None)
+        m.run(KeyValReader([]))
+        out[name] = m.trained
+    assert out["full"] == 2 * 400_000
+    assert 0.1 * 800_000 < out["tiny"] < 0.16 * 800_000

@@ -1,0 +1,87 @@
+"""Time-bounded rotation steps (reference dymoro Scheduler timer, Scheduler.java:118-137)
+and first-iteration retuning (SGDCollectiveMapper.java:623-668 adjustMiniBatch), for
+MF-SGD and LDA, on 1 and 2 gloo ranks. The deterministic full-pass mode stays the
+default; with an unbounded budget the budgeted path trains exactly what it would."""
+import math
+
+import pytest
+import torch
+
+from harp_amd.models.sgd_mf import SGDConfig, SGDCollectiveMapper, synthetic_ratings
+from harp_amd.parallel.comm import Communicator
+from harp_amd.runtime.dymoro import StepBudget
+from harp_amd.runtime.launcher import launch
+from harp_amd.runtime.mapper import KeyValReader
+
+
+def _sgd(comm, **kw):
+    tr = synthetic_ratings(600, 120, 9000, seed=6)
+    cfg = SGDConfig(rank=8, epochs=3, test_every=0, xcd_blocks=False, **kw)
+    m = SGDCollectiveMapper(comm, cfg, 600, 120, tr, None)
+    m.run(KeyValReader([]))
+    return {"W": m.W.cpu(), "trained": m.trained, "budget": list(getattr(m, "budget_history", [])),
+            "n_local": m.train.n}
+
+
+def _cpu():
+    return Communicator(None, torch.device("cpu"))
+
+
+def test_unbounded_budget_equals_full_passes():
+    full = _sgd(_cpu())
+    bud = _sgd(_cpu(), time_budget_ms=1e9, budget_pieces=4)
+    assert bud["trained"] == full["trained"] == 3 * 9000
+    assert torch.allclose(bud["W"], full["W"], atol=1e-6)
+
+
+def test_tiny_budget_cuts_each_step_to_one_piece_and_cursors_advance():
+    res = _sgd(_cpu(), time_budget_ms=1e-6, budget_pieces=4)
+    # one piece (ceil(m/4) ratings of the slice) per visit: about a quarter per epoch
+    assert 0.2 * 3 * 9000 < res["trained"] < 0.3 * 3 * 9000
+
+
+def test_budget_retuned_after_first_epoch_two_workers():
+    res = launch(_sgd_tuned, 2, timeout=300)
+    for r in res:
+        b = r["budget"]
+        assert len(b) == 2 and b[1] > 0 and b[1] != b[0]
+    assert res[0]["budget"][1] == pytest.approx(res[1]["budget"][1])  # one all-gathered decision
+
+
+def _sgd_tuned(comm):
+    return _sgd(comm, time_budget_ms=0.05, budget_pieces=8, tune_ratio=0.5)
+
+
+def test_step_budget_counts_and_stops():
+    b = StepBudget(0.0, torch.device("cpu"))
+    calls = []
+    items, n = b.run((lambda i=i: calls.append(i) or 10) for i in range(5))
+    assert (items, n, calls) == (10, 1, [0])  # the first piece always runs
+    b = StepBudget(10.0, torch.device("cpu"))
+    items, n = b.run((lambda: 3) for _ in range(4))
+    assert (items, n) == (12, 4)
+
+
+def _lda(comm, budget):
+    from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, synthetic_corpus
+
+    doc, word = synthetic_corpus(150, 400, 6, 40, seed=2)
+    cfg = LDAConfig(num_topics=8, iterations=4, print_interval=1, time_budget_ms=budget, budget_pieces=4)
+    m = LDACollectiveMapper(comm, cfg, 150, 400, (doc, word))
+    m.init_model(KeyValReader([]))
+    toks = [m.iterate(it) for it in range(4)]
+    m.rot.wait_all()
+    return {"tokens": toks, "total": int(m.tz.numel()), "loglik": m.log_likelihood(3),
+            "nk": int(m.nk.sum())}
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_lda_budget(P):
+    full = launch(_lda, P, args=(0.0,), timeout=300)
+    unb = launch(_lda, P, args=(1e9,), timeout=300)
+    tiny = launch(_lda, P, args=(1e-6,), timeout=300)
+    for f, u, t in zip(full, unb, tiny):
+        assert f["tokens"] == u["tokens"] == [f["total"]] * 4
+        assert all(x < f["total"] for x in t["tokens"])
+        assert f["nk"] == u["nk"] == t["nk"]  # topic counts stay consistent under any cut
+    assert unb[0]["loglik"] == pytest.approx(full[0]["loglik"], rel=0.02)
