@@ -77,13 +77,49 @@ class MLP:
     def predict(self, X):
         return self.predict_proba(X).argmax(1)
 
+    def _native(self, X) -> bool:
+        from ..ops import nn as NO
+
+        return self.output == "softmax" and NO.available(self.flat) and X.device == self.flat.device
+
+    def _gradient_native(self, X: torch.Tensor, labels: torch.Tensor, s: float) -> torch.Tensor:
+        """GPU path: GEMMs on hipBLASLt, every epilogue one fused pass (csrc/nn.hip):
+        bias + activation, softmax-xent forward + backward + output bias gradient, and the
+        activation derivative + hidden bias gradient."""
+        from ..ops import nn as NO
+
+        L = len(self.params) // 2
+        acts = [X.to(self.flat.dtype).contiguous()]
+        for l in range(L - 1):
+            z = torch.mm(acts[-1], self.params[2 * l].t())
+            acts.append(NO.bias_act_(z, self.params[2 * l + 1], self.act))
+        logits = torch.addmm(self.params[-1], acts[-1], self.params[-2].t())
+        grad = torch.zeros_like(self.flat)  # bias slots accumulate
+        gp, o = [], 0
+        for p in self.params:
+            gp.append(grad[o:o + p.numel()].view(p.shape))
+            o += p.numel()
+        delta = torch.empty_like(logits)
+        self.last_loss = NO.softmax_xent(logits, labels, s, delta, gp[-1])
+        for l in reversed(range(L)):
+            torch.mm(delta.t(), acts[l], out=gp[2 * l])  # delta already carries the scale
+            if l:
+                delta = delta @ self.params[2 * l]
+                NO.dact_bgrad_(delta, acts[l], self.act, gp[2 * l - 1])
+        return grad
+
     def gradient(self, X: torch.Tensor, Y: torch.Tensor, scale: Optional[float] = None) -> torch.Tensor:
         """Flat gradient of the summed loss over the batch (times ``scale``, default 1/b);
-        Y is one-hot [b, C]."""
-        _, df = _ACT[self.act]
-        acts = self.forward(X)
+        Y is one-hot [b, C] (or int class labels [b])."""
         b = X.shape[0]
         s = (1.0 / b) if scale is None else scale
+        if self._native(X):
+            labels = (Y.argmax(1) if Y.dim() == 2 else Y).to(torch.int32).contiguous()
+            return self._gradient_native(X, labels, s)
+        if Y.dim() == 1:
+            Y = torch.nn.functional.one_hot(Y.long(), self.sizes[-1])
+        _, df = _ACT[self.act]
+        acts = self.forward(X)
         grad = torch.empty_like(self.flat)
         gp = []
         o = 0

@@ -109,13 +109,32 @@ def pca(X: torch.Tensor, comm: Optional[Communicator] = None, method: str = "cor
 
 
 # ------------------------------------------------------------------ TSQR / SVD (distributed)
+def _native_tsqr(X: torch.Tensor) -> bool:
+    """GPU blocks with d <= 64 take the native panel kernels (wider panels: rocSOLVER)."""
+    from ..ops import _lib
+    from ..ops.linalg import TSQR_MAX_D
+
+    return X.device.type == "cuda" and X.shape[1] <= TSQR_MAX_D and _lib.use_native(X)
+
 def tsqr(X: torch.Tensor, comm: Optional[Communicator] = None, want_q: bool = True) -> Dict[str, torch.Tensor]:
     """Distributed tall-skinny QR (daal_qr 3-step: local QR -> QR of stacked R's -> local
     Q update). The stacked R's are all-gathered so every worker runs step 2 itself."""
     comm = _local(comm)
+    d = X.shape[1]
+    if _native_tsqr(X):
+        # step 1 on the hand-written fp64 Householder panel kernels (csrc/tsqr.hip)
+        from ..ops.linalg import house_tsqr
+
+        Xd = X.double().contiguous()
+        Q1, R1 = house_tsqr(Xd, want_q)
+        Rs = gather_rows(comm, R1)  # [P*d, d]
+        Q2, R = house_tsqr(Rs.contiguous(), want_q)
+        out = {"R": R}
+        if want_q:
+            out["Q"] = Q1 @ Q2[comm.rank * d:(comm.rank + 1) * d]
+        return out
     Xd = X.double() if X.device.type == "cpu" else X.float()
     Q1, R1 = torch.linalg.qr(Xd, mode="reduced")
-    d = Xd.shape[1]
     Rs = gather_rows(comm, R1)  # [P*d, d]
     Q2, R = torch.linalg.qr(Rs.double(), mode="reduced")
     # make R's diagonal non-negative (unique QR)

@@ -141,3 +141,60 @@ def syrk(X: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     fm = FeatureMajor.from_rows(X)
     _, _, G = gram_stats(fm)
     return G if out is None else out.add_(G)
+
+
+# ------------------------------------------------------------------ TSQR panel (csrc/tsqr.hip)
+_lib.register({
+    "harp_tsqr_width": [_lib.c_int],
+    "harp_tsqr_rows_per_block": [],
+    "harp_tsqr_level": [_lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_long,
+                        _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    "harp_tsqr_apply": [_lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p,
+                        _lib.c_void_p, _lib.c_long, _lib.c_void_p],
+})
+
+TSQR_MAX_D = 64
+
+
+def house_tsqr(A: torch.Tensor, want_q: bool = True):
+    """Householder TSQR of a tall-skinny fp64 GPU matrix (d <= 64) on the native panel
+    kernels: every 256-row block is factored by one workgroup (row per thread, registers),
+    the stacked R's are factored level by level until one block remains, and the explicit Q
+    is built top-down by applying each block's reflectors to its slice of the level above's
+    Q. Returns (Q [n, d] or None, R [d, d]) with R's diagonal made non-negative."""
+    n, d = A.shape
+    lib = _lib.kernels()
+    W = lib.harp_tsqr_width(d)
+    if W < 0:
+        raise ValueError(f"house_tsqr supports d <= {TSQR_MAX_D} (got {d})")
+    TBR = lib.harp_tsqr_rows_per_block()
+    dev = A.device
+    st = _lib.stream_ptr(dev)
+    M = torch.zeros((n, W), dtype=torch.float64, device=dev)
+    M[:, :d] = A
+    levels = []
+    while True:
+        rows = M.shape[0]
+        nb = (rows + TBR - 1) // TBR
+        V = torch.empty_like(M)
+        tau = torch.empty((nb, W), dtype=torch.float64, device=dev)
+        R = torch.empty((nb, W, W), dtype=torch.float64, device=dev)
+        _lib.check(lib.harp_tsqr_level(M.data_ptr(), W, rows, W, V.data_ptr(), W, tau.data_ptr(), R.data_ptr(), st),
+                   "tsqr_level")
+        levels.append((V, tau, rows))
+        if nb == 1:
+            Rf = R[0]
+            break
+        M = R.reshape(nb * W, W)
+    sgn = torch.sign(torch.diagonal(Rf)[:d])
+    sgn[sgn == 0] = 1
+    Rout = (Rf[:d, :d] * sgn[:, None]).contiguous()
+    if not want_q:
+        return None, Rout
+    S = None
+    for V, tau, rows in reversed(levels):
+        Q = torch.empty((rows, W), dtype=torch.float64, device=dev)
+        _lib.check(lib.harp_tsqr_apply(V.data_ptr(), W, rows, W, tau.data_ptr(), _lib.ptr(S), Q.data_ptr(), W, st),
+                   "tsqr_apply")
+        S = Q
+    return (S[:, :d] * sgn[None, :]).contiguous(), Rout

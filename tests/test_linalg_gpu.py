@@ -52,3 +52,32 @@ def test_syrk_variants_agree(cuda, variant, n, d):
     ref = Xb.t() @ Xb
     got = G[: d + 1, : d + 1].double()
     assert torch.allclose(got, ref, rtol=2e-5, atol=1e-2), (got - ref).abs().max()
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (300, 5), (4096, 16), (70000, 33), (200_000, 64), (64, 64)])
+def test_house_tsqr_matches_torch(cuda, n, d):
+    """Hand-written fp64 Householder TSQR (csrc/tsqr.hip) vs torch / rocSOLVER QR."""
+    g = torch.Generator().manual_seed(n + d)
+    A = torch.randn(n, d, generator=g, dtype=torch.float64).to(cuda)
+    Q, R = LA.house_tsqr(A)
+    assert Q.shape == (n, d) and R.shape == (d, d)
+    assert torch.allclose(Q @ R, A, atol=1e-10 * max(1.0, float(A.abs().max())))
+    k = min(n, d)
+    assert torch.allclose(Q[:, :k].t() @ Q[:, :k], torch.eye(k, dtype=torch.float64, device=cuda), atol=1e-10)
+    assert torch.all(torch.diagonal(R) >= 0) and torch.allclose(torch.triu(R), R)
+    if n >= d:
+        _, Rt = torch.linalg.qr(A)
+        Rt = Rt * torch.sign(torch.diagonal(Rt))[:, None]
+        assert torch.allclose(R, Rt, atol=1e-9, rtol=1e-9)
+
+
+def test_distributed_svd_uses_native_tsqr(cuda):
+    from harp_amd.models import stats as ST
+
+    A = torch.randn(50_000, 24, dtype=torch.float64, device=cuda)
+    out = ST.svd(A)
+    s_ref = torch.linalg.svdvals(A)
+    assert torch.allclose(out["singularValues"], s_ref, rtol=1e-10)
+    U = out["leftSingularMatrix"]
+    rec = U @ torch.diag(out["singularValues"]) @ out["rightSingularMatrix"]
+    assert torch.allclose(rec, A, atol=1e-9)
