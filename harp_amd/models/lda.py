@@ -182,14 +182,18 @@ class LDACollectiveMapper(CollectiveMapper):
         if chh is None:
             chh = self._chunks_host[gs] = ch.cpu().tolist()
         nch = len(chh) - 1
-        per = max(1, math.ceil(nch / max(1, cfg.budget_pieces)))
+        NP = max(1, cfg.budget_pieces)
         a = self.offsets[gs]
         state = {"delta": delta_total, "j": 0}
 
         def piece():
-            c0 = self._chunk_cursor.get(gs, 0)
-            c1 = min(c0 + per, nch)
-            self._chunk_cursor[gs] = c1 % nch
+            # piece q = chunks [q*nch/NP, (q+1)*nch/NP): an exact partition of the slice;
+            # the next piece index persists per slice
+            q = self._chunk_cursor.get(gs, 0)
+            self._chunk_cursor[gs] = (q + 1) % NP
+            c0, c1 = (q * nch) // NP, ((q + 1) * nch) // NP
+            if c1 == c0:
+                return 0
             t0, t1 = a + chh[c0], a + chh[c1]
             sub = ch[c0:c1 + 1] - chh[c0]
             tpos = self.doc_index.tpos[t0:t1] if self.doc_index is not None else None

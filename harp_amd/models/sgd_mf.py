@@ -248,9 +248,8 @@ class SGDCollectiveMapper(CollectiveMapper):
         return n
 
     def _budget_step(self, gs: int, slab: torch.Tensor) -> int:
-        """Train slice ``gs`` for at most the step budget: successive windows of every
-        cell (per-cell cursors persist across visits, so later visits continue where the
-        budget cut the previous one)."""
+        """Train slice ``gs`` for at most the step budget, in ``budget_pieces`` pieces
+        that each train one window of every cell (see below)."""
         cfg = self.cfg
         if getattr(self, "budget", None) is None:
             self.budget = StepBudget(cfg.time_budget_ms / 1e3, self.device)
@@ -262,23 +261,21 @@ class SGDCollectiveMapper(CollectiveMapper):
         else:
             r_, c_, v_ = self.train.get(gs)
             sizes = [r_.numel()]
-        cur = self._cursor.setdefault(gs, [0] * len(sizes))
         P = max(1, cfg.budget_pieces)
-        lens = [math.ceil(m / P) if m else 0 for m in sizes]
-
+        # piece q covers [q*m/P, (q+1)*m/P) of every cell (an exact partition); the next
+        # piece index persists per slice, so a cut visit resumes where it stopped
         def piece():
-            starts = list(cur)
-            for c, m in enumerate(sizes):
-                if m:
-                    cur[c] = (cur[c] + lens[c]) % m
-            L = [min(lens[c], sizes[c]) for c in range(len(sizes))]
+            q = self._cursor.get(gs, 0)
+            self._cursor[gs] = (q + 1) % P
+            starts = [(q * m) // P for m in sizes]
+            L = [((q + 1) * m) // P - (q * m) // P for m in sizes]
             if cfg.xcd_blocks:
                 return MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
                                              cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
                                              window=(starts, L))
             a, m = starts[0], L[0]
-            idx = (torch.arange(a, a + m, device=r_.device) % max(sizes[0], 1)) if m else None
-            return MF.sgd_update(r_[idx], c_[idx], v_[idx], self.W, slab, cfg.lr, cfg.lam, cfg.chunk) if m else 0
+            return MF.sgd_update(r_[a:a + m], c_[a:a + m], v_[a:a + m], self.W, slab, cfg.lr, cfg.lam,
+                                 cfg.chunk) if m else 0
 
         items, _ = self.budget.run(piece for _ in range(P))
         return items
