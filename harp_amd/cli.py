@@ -46,7 +46,8 @@ SPECS: Dict[str, List[Tuple[str, type, Any]]] = {
             ("iterations", int, 10), ("train_ratio", int, 100), ("maps", int, 2), ("threads", int, 1),
             ("sched_ratio", float, 1.0), ("mem", int, 0), ("work_dir", str, "harp-work/sgd"), ("test", str, "")],
     "ccd": [("input", str, ""), ("rank", int, 16), ("lam", float, 0.1), ("iterations", int, 10), ("maps", int, 2),
-            ("threads", int, 1), ("num_model_slices", int, 2), ("work_dir", str, "harp-work/ccd"), ("test", str, "")],
+            ("threads", int, 1), ("num_model_slices", int, 2), ("work_dir", str, "harp-work/ccd"), ("test", str, ""),
+            ("mode", str, "allgather")],
     "lda": [("doc_dir", str, ""), ("num_topics", int, 100), ("alpha", float, 0.01), ("beta", float, 0.01),
             ("iterations", int, 10), ("min_bound", int, 0), ("max_bound", int, 0), ("maps", int, 2), ("threads", int, 1),
             ("sched_ratio", float, 1.0), ("mem", int, 0), ("work_dir", str, "harp-work/lda"), ("print_model", str, "false")],
@@ -205,8 +206,10 @@ def _run_ccd(comm, cfg):
     from .models.ccd import CCDConfig, train_ccd
 
     u, i, v, nu, ni, test = _mf_data(comm, cfg)
-    res = train_ccd(comm, u, i, v, nu, ni, CCDConfig(rank=cfg["rank"], lam=cfg["lam"], iterations=cfg["iterations"]),
-                    test=test)
+    res = train_ccd(comm, u, i, v, nu, ni, CCDConfig(rank=cfg["rank"], lam=cfg["lam"], iterations=cfg["iterations"],
+                                                     mode=cfg.get("mode", "allgather"),
+                                                     slices_per_rank=max(1, cfg["num_model_slices"]),
+                                                     model_dir=cfg["work_dir"]), test=test)
     return {"history": res["history"]}
 
 

@@ -1,5 +1,6 @@
 """ALS (implicit + explicit) and MF-CCD: batched solvers vs per-row dense references,
 and P=2 gloo runs vs the single-worker result (the algorithms are P-invariant)."""
+import pytest
 import torch
 
 from harp_amd.models import als as A
@@ -134,3 +135,41 @@ def test_ccd_distributed_equals_single():
     for W, ids, hist in res:
         assert torch.allclose(W, single["W"][ids], atol=1e-10)
         assert abs(hist[-1]["train_rmse"] - single["history"][-1]["train_rmse"]) < 1e-10
+
+
+def _ccd_modes(comm, mode, S):
+    from harp_amd.models.ccd import CCDConfig, train_ccd
+
+    g = torch.Generator().manual_seed(9)
+    n = 4000
+    u = torch.randint(0, 150, (n,), generator=g)
+    i = torch.randint(0, 60, (n,), generator=g)
+    v = torch.rand(n, generator=g) * 4 + 1
+    P, r = comm.world_size, comm.rank
+    sl = slice(r * n // P, (r + 1) * n // P)
+    res = train_ccd(comm, u[sl], i[sl], v[sl], 150, 60, CCDConfig(rank=7, iterations=6, mode=mode, slices_per_rank=S))
+    return {"W": res["W"].cpu(), "uid": res["user_ids"].cpu(), "rmse": [h["train_rmse"] for h in res["history"]],
+            "slab": res.get("slab_floats_per_rank")}
+
+
+@pytest.mark.parametrize("S", [1, 2])
+def test_ccd_rotation_mode_one_rank_equals_allgather(S):
+    from harp_amd.parallel.comm import Communicator
+
+    c = Communicator(None, torch.device("cpu"))
+    a = _ccd_modes(c, "allgather", S)
+    b = _ccd_modes(c, "rotation", S)
+    assert torch.allclose(a["W"], b["W"], atol=1e-10)
+    assert a["rmse"] == pytest.approx(b["rmse"], rel=1e-10)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_ccd_rotation_mode_multi_rank(P):
+    rot = launch(_ccd_modes, P, args=("rotation", 2), timeout=300)
+    ag = launch(_ccd_modes, P, args=("allgather", 2), timeout=300)
+    # both descend; different (valid) dimension orders give close fits
+    assert rot[0]["rmse"][-1] < rot[0]["rmse"][0]
+    assert rot[0]["rmse"][-1] == pytest.approx(ag[0]["rmse"][-1], rel=0.05)
+    # memory: a rank holds S slices of (m + n) x ceil(r / (S P)) floats, not a full factor
+    rs = -(-7 // (2 * P))
+    assert rot[0]["slab"] == 2 * (P * -(-150 // P) + P * -(-60 // P)) * rs

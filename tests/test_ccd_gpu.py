@@ -53,3 +53,21 @@ def test_ccd_model_gpu_matches_cpu(cuda):
     b = train_ccd(Communicator(device=cuda), u, i, v, 400, 300, cfg)
     ra, rb = a["history"][-1]["train_rmse"], b["history"][-1]["train_rmse"]
     assert abs(ra - rb) < 1e-3 * max(1.0, ra), (ra, rb)
+
+
+def test_ccd_rotation_mode_matches_allgather_on_gpu(cuda):
+    """Rotation mode (dimension slices rotated, csrc/ccd.hip phase kernels on slices) on
+    one GPU follows the same per-row update order as the allgather mode."""
+    from harp_amd.models.ccd import CCDConfig, train_ccd
+    from harp_amd.parallel.comm import Communicator
+
+    g = torch.Generator().manual_seed(2)
+    n = 200_000
+    u = torch.randint(0, 5000, (n,), generator=g)
+    i = torch.randint(0, 800, (n,), generator=g)
+    v = torch.rand(n, generator=g) * 4 + 1
+    c = Communicator(None, cuda)
+    a = train_ccd(c, u, i, v, 5000, 800, CCDConfig(rank=24, iterations=3))
+    b = train_ccd(c, u, i, v, 5000, 800, CCDConfig(rank=24, iterations=3, mode="rotation", slices_per_rank=2))
+    assert torch.allclose(a["W"], b["W"], rtol=1e-3, atol=1e-4)
+    assert a["history"][-1]["train_rmse"] == pytest.approx(b["history"][-1]["train_rmse"], rel=1e-4)
