@@ -335,7 +335,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
     "push-pull parameter server collective"; the pattern of contrib LDAMapperDyn.java:
     push :380 / pull :429, applied to the collapsed Gibbs sampler).
 
-    The model is a distributed global :class:`Table` of word blocks (``block_words`` rows
+    The model is a distributed global packed table of word blocks (``block_words`` rows
     x K_pad int32 counts; owner = block id % P, the default Partitioner). Per iteration a
     worker pulls the blocks its tokens touch into one contiguous device slab, runs the
     ``lda_cgs`` kernel over all of its tokens against that snapshot (bulk-synchronous
@@ -344,7 +344,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
 
     def init_model(self, reader: KeyValReader) -> None:
         from ..core.combiner import ArrCombiner, Operation
-        from ..core.table import Table
+        from ..core.table import PackedTable
 
         cfg = self.cfg
         P, me, dev = self.get_num_workers(), self.get_self_id(), self.device
@@ -377,37 +377,37 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self.nk = nk
         self.sum = ArrCombiner(Operation.SUM)
         nblocks = math.ceil(self.vocab / B)
-        self.glob = Table(1, self.sum)
-        for b in range(me, nblocks, P):
-            self.glob.add(b, torch.zeros((B, self.Kp), dtype=torch.int32, device=dev))
-        self._push(slab)
+        owned = list(range(me, nblocks, P))
+        # distributed global table: owned word blocks, one packed [n_owned, B, K_pad] slab
+        self.glob = PackedTable(owned, torch.zeros((len(owned), B, self.Kp), dtype=torch.int32, device=dev),
+                                table_id=1, combiner=self.sum)
+        # one persistent buffer of the blocks this worker's tokens touch: pulled into, sampled
+        # on in place, turned into the count delta and pushed back (cached comm plans)
+        nneed = len(self.need)
+        self.pull_buf = slab.view(nneed, B, self.Kp) if nneed else torch.zeros((0, B, self.Kp), dtype=torch.int32,
+                                                                              device=dev)
+        self.before = torch.empty_like(self.pull_buf)
+        self.want_pt = PackedTable(self.need, self.pull_buf, table_id=3, combiner=self.sum)
+        for t in (self.glob, self.want_pt):
+            t.static_layout = True
+        self._push_delta()  # initial counts = a delta against an all-zero model
         self.vbeta = self.vocab * cfg.beta
 
-    def _push(self, slab: torch.Tensor) -> None:
-        from ..core.table import Table
-
-        local = Table(2, self.sum)
-        for k, b in enumerate(self.need):
-            local.add(b, slab[k * self.B:(k + 1) * self.B])
-        if not self.push("lda", "push-model", local, self.glob, None):
+    def _push_delta(self) -> None:
+        if not self.push("lda", "push-model", self.want_pt, self.glob, None):
             raise IOError("push failed")
 
     def _pull(self) -> torch.Tensor:
-        from ..core.table import Table
-
-        want = Table(3, self.sum)
-        for b in self.need:
-            want.add(b, torch.zeros((self.B, self.Kp), dtype=torch.int32, device=self.device))
-        if not self.pull("lda", "pull-model", want, self.glob, True):
+        self.pull_buf.zero_()  # pull combines into the local rows
+        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True):
             raise IOError("pull failed")
-        if not self.need:
-            return torch.zeros((0, self.Kp), dtype=torch.int32, device=self.device)
-        return torch.cat([want[b] for b in self.need]).contiguous()
+        return self.pull_buf.view(-1, self.Kp)
 
     def iterate(self, it: int) -> int:
         cfg = self.cfg
         slab = self._pull()
-        before = slab.clone()
+        self.before.copy_(self.pull_buf)
+        before = self.before.view(-1, self.Kp)
         n = self.tz.numel()
         if n:
             d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, slab, self.nk,
@@ -416,7 +416,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         else:
             d = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
         slab -= before
-        self._push(slab)
+        self._push_delta()
         if self.get_num_workers() > 1:
             d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
         self.nk += d

@@ -156,3 +156,35 @@ def test_em_gmm_file():
     m = KF.em_gmm(X, 2, n_iterations=200, accuracy_threshold=1e-10)
     sk = GaussianMixture(2, reg_covar=1e-6, tol=1e-10, max_iter=200, n_init=5, random_state=0).fit(X.numpy())
     assert float(m["loglik"]) >= sk.score(X.numpy()) - 0.05
+
+
+def _airline(split):
+    import numpy as np
+
+    a = np.loadtxt(P("tutorial", "airline", f"{split}.csv"), dtype=np.float32, ndmin=2)
+    return torch.from_numpy(a[:, :-1]), torch.from_numpy(a[:, -1]).long()
+
+
+def _rf_airline(comm, Xtr, ytr):
+    f = T.DecisionForest(n_trees=16, max_depth=8, seed=3)
+    P, r = comm.world_size, comm.rank
+    n = Xtr.shape[0]
+    sl = slice(r * n // P, (r + 1) * n // P)  # each mapper grows its trees on its own file split
+    f.fit_distributed(Xtr[sl], ytr[sl], comm, num_classes=2)
+    return f
+
+
+def test_random_forest_airline_fixture():
+    """contrib RF on datasets/tutorial/airline (RFMapCollective 32 trees, 2 mappers; the
+    reference prints test accuracy only, so parity is unpinned: the gate is the task's
+    easy separability — CLASS is ARR_DELAY_GROUP >= 1 and ARR_DELAY is a feature)."""
+    from harp_amd.runtime.launcher import launch
+
+    Xtr, ytr = _airline("train")
+    Xte, yte = _airline("test")
+    assert Xtr.shape[1] == 9 and Xte.shape[0] == 14995
+    Xtr, ytr = Xtr[:40000], ytr[:40000]
+    forests = launch(_rf_airline, 2, args=(Xtr, ytr), timeout=600)
+    assert len(forests[0].trees) == len(forests[1].trees) == 16
+    acc = float((forests[0].predict(Xte) == yte).float().mean())
+    assert acc > 0.97, acc
