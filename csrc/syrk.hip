@@ -52,7 +52,10 @@ __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long 
   }
 }
 
-template <int MT_, int BA_, int BB_>
+// DIAG (timing diagnostics only, results are garbage): 1 = no global loads after the first
+// stage (MFMA + LDS + barriers), 2 = no MFMA (loads + LDS reads + a VALU use of the
+// fragments), 3 = loads + barriers only
+template <int MT_, int BA_, int BB_, int DIAG = 0>
 __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void syrk_kernel(
     const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg) {
   using C = SyrkCfg<MT_, BA_, BB_>;
@@ -92,14 +95,14 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
   __syncthreads();
   int cur = 0;
   for (long k0 = kbeg; k0 < kend; k0 += KT) {
-    if (k0 + KT < kend) {
+    if (DIAG != 1 && k0 + KT < kend) {
       stage_panel<C>(XT, ld, ti * MT, k0 + KT, smem + (cur ^ 1) * PANEL, wave, lane);
       if (!diag) stage_panel<C>(XT, ld, tj * MT, k0 + KT, smem + (2 + (cur ^ 1)) * PANEL, wave, lane);
     }
     const char* A = smem + cur * PANEL;
     const char* B = diag ? A : smem + (2 + cur) * PANEL;
 #pragma unroll
-    for (int s = 0; s < KT / 16; ++s) {
+    for (int s = 0; s < KT / 16 && DIAG != 3; ++s) {
       bf16x8 af[BA], bfr[BB];
 #pragma unroll
       for (int a = 0; a < BA; ++a) {
@@ -114,8 +117,10 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
 #pragma unroll
       for (int a = 0; a < BA; ++a)
 #pragma unroll
-        for (int bb = 0; bb < BB; ++bb)
-          acc[a][bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[bb], acc[a][bb], 0, 0, 0);
+        for (int bb = 0; bb < BB; ++bb) {
+          if constexpr (DIAG == 2) acc[a][bb][0] += (float)af[a][0] * (float)bfr[bb][7];
+          else acc[a][bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[bb], acc[a][bb], 0, 0, 0);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -296,7 +301,7 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
 
 }  // namespace
 
-template <int MT, int BA, int BB, int NS = 0>
+template <int MT, int BA, int BB, int NS = 0, int DIAG = 0>
 static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits, int target_wg,
                        hipStream_t s) {
   using C = SyrkCfg<MT, BA, BB>;
@@ -333,7 +338,7 @@ static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int
     syrk_ms_kernel<MT, BA, BB, NS><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
         (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
   } else {
-    syrk_kernel<MT, BA, BB><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
+    syrk_kernel<MT, BA, BB, DIAG><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
         (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
   }
   return harp_launch_status();
@@ -363,4 +368,17 @@ HARP_EXPORT int harp_to_feature_major_bf16(const void* X, long n, int d, long ld
   dim3 grid((unsigned)((ld + 31) / 32), (unsigned)((d_pad + 31) / 32));
   to_feature_major_kernel<<<grid, dim3(256), 0, s>>>((const __bf16*)X, n, d, ldx, (__bf16*)XT, ld, ones_row);
   return harp_launch_status();
+}
+
+// Timing diagnostics of the default kernel (see DIAG above; G receives garbage).
+HARP_EXPORT int harp_syrk_diag(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits, int mode,
+                               hipStream_t s) {
+  if (d_pad % 256 || d_pad < 512 || n % KT || ld < n || ldg < d_pad) return HARP_EBADARG;
+  switch (mode) {
+    case 0: return launch_syrk<256, 2, 4, 0, 0>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 1: return launch_syrk<256, 2, 4, 0, 1>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 2: return launch_syrk<256, 2, 4, 0, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 3: return launch_syrk<256, 2, 4, 0, 3>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    default: return HARP_EBADARG;
+  }
 }

@@ -9,3 +9,5 @@ run ccd_ag python scripts/bench_ccd.py --mode allgather
 run ccd_rot python scripts/bench_ccd.py --mode rotation
 run pca python scripts/bench_pca.py --steps 2
 run tsqr python scripts/bench_tsqr.py
+run syrk_diag python scripts/syrk_diag.py
+run syrk_diag_s24 python scripts/syrk_diag.py --splits 24
