@@ -57,7 +57,8 @@ __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long 
 // fragments), 3 = loads + barriers only
 template <int MT_, int BA_, int BB_, int DIAG = 0>
 __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void syrk_kernel(
-    const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg) {
+    const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg,
+    int* __restrict__ sync, int sync_every) {
   using C = SyrkCfg<MT_, BA_, BB_>;
   constexpr int MT = C::MT, BA = C::BA, BB = C::BB, PANEL = C::PANEL_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[4 * PANEL];
@@ -95,6 +96,25 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
   __syncthreads();
   int cur = 0;
   for (long k0 = kbeg; k0 < kend; k0 += KT) {
+    if (sync) {
+      // soft lock-step of the split's tiles (they share feature panels through this XCD's
+      // L2 only while they stream the same samples): every sync_every stages, arrive on the
+      // split's counter and wait -- boundedly, so progress never depends on it -- until
+      // every tile of the split has arrived. Correctness does not depend on the wait.
+      const int st = (int)((k0 - kbeg) / KT);
+      if (st > 0 && st % sync_every == 0) {
+        if (tid == 0) {
+          int* c = sync + split;
+          atomicAdd(c, 1);
+          const int target = ntiles * (st / sync_every);
+          for (int it = 0; it < 2000; ++it) {
+            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            __builtin_amdgcn_s_sleep(4);
+          }
+        }
+        __syncthreads();
+      }
+    }
     if (DIAG != 1 && k0 + KT < kend) {
       stage_panel<C>(XT, ld, ti * MT, k0 + KT, smem + (cur ^ 1) * PANEL, wave, lane);
       if (!diag) stage_panel<C>(XT, ld, tj * MT, k0 + KT, smem + (2 + (cur ^ 1)) * PANEL, wave, lane);
@@ -168,142 +188,11 @@ __global__ void to_feature_major_kernel(const __bf16* __restrict__ X, long n, in
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Multi-stage variant: KT2 = 32 samples per stage and NS-deep LDS-DMA pipeline (the stage
-// about to be consumed was issued NS-1 stages earlier), so L2-miss latency (the operand
-// panels are re-read by every tile of a split and mostly miss L2) hides behind NS-1
-// stages of MFMA work instead of one. Swizzle for 4 chunks per 64-B row:
-// c ^ ((row >> 2) & 3) keeps every ds_read_b128 lane group on 16 distinct 16-B units.
-constexpr int KT2 = 32;
-constexpr int CPR2 = KT2 / 8;  // 4
-__device__ __forceinline__ int swz2(int row, int c) { return c ^ ((row >> 2) & 3); }
-
-template <class C>
-__device__ __forceinline__ void stage_panel2(const __bf16* __restrict__ XT, long ld, int r0, long k0, char* lds,
-                                             int wave, int lane) {
-  constexpr int DMA = C::MT * KT2 * 2 / 1024;
-#pragma unroll
-  for (int j = wave; j < DMA; j += C::WAVES) {
-    const int q = j * 64 + lane;
-    const int row = q / CPR2, cp = q % CPR2;
-    const __bf16* src = XT + (long)(r0 + row) * ld + k0 + swz2(row, cp) * 8;
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                     (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
-  }
-}
-
-// wait until at most `left` of this wave's DMA instructions are outstanding
-__device__ __forceinline__ void wait_vm(int left) {
-  switch (left) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-  }
-}
-
-template <int MT_, int BA_, int BB_, int NS>
-__global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void syrk_ms_kernel(
-    const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg) {
-  using C = SyrkCfg<MT_, BA_, BB_>;
-  constexpr int MT = C::MT, BA = C::BA, BB = C::BB;
-  constexpr int PANEL = MT * KT2 * 2;
-  constexpr int DPW = (PANEL / 1024 + C::WAVES - 1) / C::WAVES;  // DMA instructions per wave per panel
-  static_assert((PANEL / 1024) % C::WAVES == 0, "panel DMA must split evenly over the waves");
-  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * PANEL];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const unsigned nb = gridDim.x, b = blockIdx.x;
-  const unsigned q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
-  const unsigned L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-  const int ntiles = nt * (nt + 1) / 2;
-  const int tile = L % ntiles;
-  const long split = L / ntiles;
-  int ti = 0, rem = tile;
-  while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
-  const int tj = ti + rem;
-  const bool diag = ti == tj;
-  const long kbeg = split * chunk;
-  long kend = kbeg + chunk;
-  if (kend > n) kend = n;
-  if (kbeg >= kend) return;
-  const int nsteps = (int)((kend - kbeg) / KT2);
-  const int per_step = diag ? DPW : 2 * DPW;
-  const int wr = wave / C::WC, wc = wave % C::WC;
-  floatx16 acc[BA][BB];
-#pragma unroll
-  for (int a = 0; a < BA; ++a)
-#pragma unroll
-    for (int bb = 0; bb < BB; ++bb)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[a][bb][v] = 0.f;
-  auto issue = [&](int step) {
-    char* buf = smem + (step % NS) * 2 * PANEL;
-    const long k0 = kbeg + (long)step * KT2;
-    stage_panel2<C>(XT, ld, ti * MT, k0, buf, wave, lane);
-    if (!diag) stage_panel2<C>(XT, ld, tj * MT, k0, buf + PANEL, wave, lane);
-  };
-#pragma unroll
-  for (int st = 0; st < NS - 1; ++st)
-    if (st < nsteps) issue(st);
-  for (int i = 0; i < nsteps; ++i) {
-    // stages issued after step i so far: min(NS-2, nsteps-1-i)
-    int later = nsteps - 1 - i;
-    if (later > NS - 2) later = NS - 2;
-    wait_vm(later * per_step);
-    __syncthreads();  // step i landed for every wave; step i-1's buffer is free
-    if (i + NS - 1 < nsteps) issue(i + NS - 1);
-    const char* A = smem + (i % NS) * 2 * PANEL;
-    const char* B = diag ? A : A + PANEL;
-#pragma unroll
-    for (int s = 0; s < KT2 / 16; ++s) {
-      bf16x8 af[BA], bfr[BB];
-#pragma unroll
-      for (int a = 0; a < BA; ++a) {
-        const int row = wr * (32 * BA) + a * 32 + r;
-        af[a] = *(const bf16x8*)(A + row * (CPR2 * 16) + swz2(row, 2 * s + h) * 16);
-      }
-#pragma unroll
-      for (int bb = 0; bb < BB; ++bb) {
-        const int row = wc * (32 * BB) + bb * 32 + r;
-        bfr[bb] = *(const bf16x8*)(B + row * (CPR2 * 16) + swz2(row, 2 * s + h) * 16);
-      }
-#pragma unroll
-      for (int a = 0; a < BA; ++a)
-#pragma unroll
-        for (int bb = 0; bb < BB; ++bb)
-          acc[a][bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[bb], acc[a][bb], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < BA; ++a)
-#pragma unroll
-    for (int bb = 0; bb < BB; ++bb) {
-      const int i0 = ti * MT + wr * (32 * BA) + a * 32;
-      const int j0 = tj * MT + wc * (32 * BB) + bb * 32;
-      if (diag && i0 > j0 + 31) continue;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int row = (v & 3) + 8 * (v >> 2) + 4 * h;
-        atomicAdd(G + (long)(i0 + row) * ldg + j0 + r, acc[a][bb][v]);
-      }
-    }
-}
-
 }  // namespace
 
-template <int MT, int BA, int BB, int NS = 0, int DIAG = 0>
+template <int MT, int BA, int BB, int DIAG = 0>
 static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits, int target_wg,
-                       hipStream_t s) {
+                       hipStream_t s, int* sync_ws = nullptr, int sync_every = 0) {
   using C = SyrkCfg<MT, BA, BB>;
   const int nt = d_pad / MT;
   const int ntiles = nt * (nt + 1) / 2;
@@ -312,7 +201,9 @@ static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int
     // once, so the 2-4 tiles reading a feature panel share it in that XCD's L2) and every
     // workgroup starts in the first wave -- no split straddles dispatch waves. 256 x 256
     // tiles, d_pad = 1024: 24 splits x 10 tiles = 240 workgroups (one per CU, 30 per XCD),
-    // 0.143 s vs 0.150 s for the ~1030-workgroup split-K grid (profiles/r2_syrk).
+    // 0.143 s vs 0.150 s for the ~1030-workgroup split-K grid, 0.122 s with the split
+    // lock-step hint (L2 hit 49 % -> 71 %, the 75 % ceiling of 4 tiles per panel;
+    // profiles/r2_syrk).
     const int per_xcd = 32 * (MT >= 256 ? 1 : 2);  // one 256-tile / two 128-tile WGs per CU (LDS)
     if (ntiles <= per_xcd) {
       num_splits = 8 * (per_xcd / ntiles);
@@ -334,12 +225,12 @@ static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int
   long chunk = (n + num_splits - 1) / num_splits;
   chunk = (chunk + KT - 1) / KT * KT;
   const long splits = (n + chunk - 1) / chunk;
-  if constexpr (NS > 0) {
-    syrk_ms_kernel<MT, BA, BB, NS><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
-        (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
-  } else {
+  {
+    // the lock-step hint only pays when every tile of a split is resident at once
+    int* sw = (sync_ws && sync_every > 0 && ntiles * splits <= 256 && splits <= 1024) ? sync_ws : nullptr;
+    if (sw && hipMemsetAsync(sw, 0, sizeof(int) * splits, s) != hipSuccess) return HARP_ELAUNCH;
     syrk_kernel<MT, BA, BB, DIAG><<<dim3((unsigned)(ntiles * splits)), dim3(C::WAVES * 64), 0, s>>>(
-        (const __bf16*)XT, ld, n, nt, chunk, G, ldg);
+        (const __bf16*)XT, ld, n, nt, chunk, G, ldg, sw, sync_every);
   }
   return harp_launch_status();
 }
@@ -347,18 +238,17 @@ static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int
 // G[d_pad][ldg] (+)= XT XT^T over the upper tiles; XT [d_pad][ld] bf16, d_pad % 128 == 0,
 // n % 64 == 0 (zero-padded samples), ld >= n, ld % 8 == 0. 256x256 tiles (8 waves) when
 // d_pad % 256 == 0 and d_pad >= 512 (half the operand re-reads), else 128x128 (4 waves).
-// variant 0: 64-sample stages, double buffer; 1: 32-sample stages, 4-deep pipeline
+// variant 0 (the only one): 64-sample stages, double buffer. A 32-sample 4-deep LDS-DMA
+// ring (raw s_barrier, no vmcnt drain) measured 0.19-0.20 s vs 0.122 s and was removed
+// (profiles/r2_syrk). sync_ws (>= 1024 ints, may be null) + sync_every (stages, 0 = off):
+// the split lock-step hint of the 256-tile kernel (see syrk_kernel).
 HARP_EXPORT int harp_syrk_t_bf16(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits,
-                                 int variant, hipStream_t s) {
+                                 int variant, int* sync_ws, int sync_every, hipStream_t s) {
   if (d_pad % 128 || n % KT || ld < n || ld % 8 || ldg < d_pad) return HARP_EBADARG;
   if (n == 0) return HARP_OK;
   const bool big = d_pad >= 512 && d_pad % 256 == 0;
-  if (variant == 1) {
-    if (big) return launch_syrk<256, 2, 4, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
-    return launch_syrk<128, 2, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 2048, s);
-  }
   if (variant != 0) return HARP_EBADARG;
-  if (big) return launch_syrk<256, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+  if (big) return launch_syrk<256, 2, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s, sync_ws, sync_every);
   return launch_syrk<128, 2, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 2048, s);
 }
 
@@ -375,10 +265,10 @@ HARP_EXPORT int harp_syrk_diag(const void* XT, long ld, long n, int d_pad, float
                                hipStream_t s) {
   if (d_pad % 256 || d_pad < 512 || n % KT || ld < n || ldg < d_pad) return HARP_EBADARG;
   switch (mode) {
-    case 0: return launch_syrk<256, 2, 4, 0, 0>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
-    case 1: return launch_syrk<256, 2, 4, 0, 1>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
-    case 2: return launch_syrk<256, 2, 4, 0, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
-    case 3: return launch_syrk<256, 2, 4, 0, 3>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 0: return launch_syrk<256, 2, 4, 0>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 1: return launch_syrk<256, 2, 4, 1>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 2: return launch_syrk<256, 2, 4, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 3: return launch_syrk<256, 2, 4, 3>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     default: return HARP_EBADARG;
   }
 }

@@ -8,6 +8,8 @@ tiles only, fp32 accumulation, column sums fused); fp64 and sparse inputs use to
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -45,7 +47,7 @@ def gram(X: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
 
 _lib.register({
     "harp_syrk_t_bf16": [_lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_int,
-                         _lib.c_int, _lib.c_void_p],
+                         _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p],
     "harp_to_feature_major_bf16": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_long,
                                    _lib.c_int, _lib.c_int, _lib.c_void_p],
 })
@@ -104,16 +106,25 @@ class FeatureMajor:
         return cls(XT, n, d)
 
 
-SYRK_VARIANT = 0  # 0: 64-sample stages, double buffer (faster: 151 vs 201 ms at 1e8 x 1000); 1: 32-sample, 4-deep
+SYRK_VARIANT = 0  # the one shipped kernel (profiles/r2_syrk: alternatives measured slower, removed)
 
 
-def syrk_t(fm: FeatureMajor, G: torch.Tensor | None = None, num_splits: int = 0, variant: int | None = None) -> torch.Tensor:
+SYRK_SYNC_EVERY = int(os.environ.get("HARP_SYRK_SYNC", "32"))  # stages between split lock-step points (0: off)
+_SYNC_WS: dict = {}
+
+
+def syrk_t(fm: FeatureMajor, G: torch.Tensor | None = None, num_splits: int = 0, variant: int | None = None,
+           sync_every: int | None = None) -> torch.Tensor:
     """G (+)= XT XT^T over the upper 128-tiles (fp32); call :func:`symmetrize_upper` after."""
     if G is None:
         G = torch.zeros((fm.d_pad, fm.d_pad), dtype=torch.float32, device=fm.XT.device)
+    ws = _SYNC_WS.get(fm.XT.device)
+    if ws is None:
+        ws = _SYNC_WS[fm.XT.device] = torch.zeros(1024, dtype=torch.int32, device=fm.XT.device)
+    every = SYRK_SYNC_EVERY if sync_every is None else sync_every
     st = _lib.kernels().harp_syrk_t_bf16(fm.XT.data_ptr(), fm.ld, fm.ld, fm.d_pad, G.data_ptr(), G.stride(0),
                                          num_splits, SYRK_VARIANT if variant is None else variant,
-                                         _lib.stream_ptr(fm.XT.device))
+                                         ws.data_ptr(), int(every), _lib.stream_ptr(fm.XT.device))
     _lib.check(st, "syrk_t")
     return G
 

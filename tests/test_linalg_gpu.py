@@ -42,7 +42,7 @@ def test_covariance_gpu_matches_cpu(cuda):
     assert torch.allclose(g["covariance"].cpu(), c["covariance"], rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0])
 @pytest.mark.parametrize("n,d", [(4096, 100), (20032, 700), (30016, 1000)])
 def test_syrk_variants_agree(cuda, variant, n, d):
     X = torch.rand(n, d, device=cuda) * 2 - 1
