@@ -51,6 +51,7 @@ class SGDConfig:
     time_budget_ms: float = 0.0  # >0: time-bounded rotation steps (Scheduler timer); 0: deterministic
     budget_pieces: int = 8     # launches a step's work is cut into (budget granularity)
     tune_ratio: float = 0.0    # >0: after epoch 0 retune the budget so an epoch trains this fraction
+    cpu_threads: int = 1       # CPU workers: >1 runs the 8 x 8 cells through the 2-D BlockScheduler
 
 
 def load_mm(path: str) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -223,7 +224,13 @@ class SGDCollectiveMapper(CollectiveMapper):
                 slab = self.rot.get(k)
                 gs = block * S + k
                 with timer.phase("compute"):
-                    if cfg.time_budget_ms > 0:
+                    if cfg.xcd_blocks and self.device.type == "cpu" and cfg.cpu_threads > 1:
+                        # CPU worker: the reference's threaded 2-D scheduler with its timer
+                        r_, c_, v_, off, hoff = self.train.get_cells(gs)
+                        budget = cfg.time_budget_ms / 1e3 if cfg.time_budget_ms > 0 else None
+                        n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
+                                                   host_off=hoff, threads=cfg.cpu_threads, time_budget=budget)
+                    elif cfg.time_budget_ms > 0:
                         n += self._budget_step(gs, slab)
                     elif cfg.xcd_blocks:
                         r_, c_, v_, off, hoff = self.train.get_cells(gs)

@@ -110,7 +110,8 @@ def balanced_blocks(group: torch.Tensor, idx: torch.Tensor, n_groups: int, n_idx
 def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, cell_off: torch.Tensor,
                        W: torch.Tensor, H: torch.Tensor, lr: float, lam: float, chunk: int = 64,
                        blocks_per_xcd: int = 256, host_off: list | None = None, variant: int = 0,
-                       window: Optional[Tuple[List[int], List[int]]] = None) -> int:
+                       window: Optional[Tuple[List[int], List[int]]] = None, threads: int = 1,
+                       time_budget: Optional[float] = None) -> int:
     """One SGD pass over ratings laid out in nb x nb cells (cell-major, user-sorted inside a
     cell; ``cell_off`` = nb*nb+1 int64 offsets on W's device). Sub-step s trains the nb
     row- and column-disjoint cells (x, (x+s) mod nb): on the GPU one XCD per cell
@@ -120,7 +121,9 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     H stores (slower; see csrc/mf_sgd.hip).
     ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
     ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
-    Returns the number of ratings trained."""
+    CPU only: ``threads > 1`` or a ``time_budget`` (s) run the cells through the 2-D
+    conflict-free :class:`~harp_amd.runtime.dymoro.BlockScheduler` (order then depends on
+    timing, like the reference's Scheduler). Returns the number of ratings trained."""
     _check(rows, cols, vals, W, H)
     n = rows.numel()
     if n == 0:
@@ -153,17 +156,28 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
             rt.harp_mf_sgd_cpu(rows[a:].data_ptr(), cols[a:].data_ptr(), vals[a:].data_ptr(), m, r,
                                W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam))
 
+    def cell(c: int) -> int:
+        a, b = off[c], off[c + 1]
+        if window is None:
+            seg(a, b - a)
+            return b - a
+        w0, L = int(window[0][c]), int(window[1][c])
+        first = min(L, (b - a) - w0)
+        seg(a + w0, first)
+        seg(a, L - first)
+        return L
+
+    if threads > 1 or time_budget is not None:
+        # the reference's 2-D Scheduler (MJ/dymoro/Scheduler.java:95-237): row- and
+        # column-disjoint cells run concurrently on a thread pool (native calls release the
+        # GIL), refilled as cells finish, until every cell ran or the time budget expired
+        from ..runtime.dymoro import BlockScheduler
+
+        res = BlockScheduler(nb, nb, lambda x, y: cell(x * nb + y), num_threads=max(1, threads)).schedule(time_budget)
+        return int(res["items"])
     for s in range(nb):
         for x in range(nb):
-            c = x * nb + (x + s) % nb
-            a, b = off[c], off[c + 1]
-            if window is None:
-                seg(a, b - a)
-            else:
-                w0, L = int(window[0][c]), int(window[1][c])
-                first = min(L, (b - a) - w0)
-                seg(a + w0, first)
-                seg(a, L - first)
+            cell(x * nb + (x + s) % nb)
     return trained
 
 

@@ -308,8 +308,10 @@ class BlockScheduler:
 
         with ThreadPoolExecutor(max_workers=self.num_threads) as ex:
             with lock:
-                while todo or inflight[0]:
-                    timed_out = time_budget is not None and time.perf_counter() - t0 > time_budget
+                first = True  # the first round of conflict-free blocks is submitted before the
+                while todo or inflight[0]:  # timer counts (Scheduler.java:104-117 then :118-137)
+                    timed_out = (not first and time_budget is not None
+                                 and time.perf_counter() - t0 > time_budget)
                     launched = False
                     if not timed_out:
                         for (r, c) in sorted(todo):
@@ -322,6 +324,7 @@ class BlockScheduler:
                                 inflight[0] += 1
                                 ex.submit(run, r, c)
                                 launched = True
+                    first = False
                     if timed_out and not inflight[0]:
                         break
                     if not launched:

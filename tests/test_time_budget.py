@@ -85,3 +85,17 @@ def test_lda_budget(P):
         assert all(x < f["total"] for x in t["tokens"])
         assert f["nk"] == u["nk"] == t["nk"]  # topic counts stay consistent under any cut
     assert unb[0]["loglik"] == pytest.approx(full[0]["loglik"], rel=0.02)
+
+
+def test_cpu_threaded_block_scheduler_path():
+    """CPU workers run the 8 x 8 cells through the conflict-free 2-D BlockScheduler (the
+    reference's Scheduler); unbounded it trains every rating, a tiny timer stops early."""
+    tr = synthetic_ratings(600, 120, 9000, seed=6)
+    out = {}
+    for name, b in (("all", 0.0), ("timer", 1e-6)):
+        cfg = SGDConfig(rank=8, epochs=2, test_every=0, xcd_blocks=True, cpu_threads=4, time_budget_ms=b)
+        m = SGDCollectiveMapper(_cpu(), cfg, 600, 120, tr, None)
+        m.run(KeyValReader([]))
+        out[name] = m.trained
+    assert out["all"] == 2 * 9000
+    assert 0 < out["timer"] < 2 * 9000
