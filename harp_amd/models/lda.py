@@ -394,7 +394,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self.vbeta = self.vocab * cfg.beta
 
     def _push_delta(self) -> None:
-        if not self.push("lda", "push-model", self.want_pt, self.glob, None):
+        # only the nonzero count changes travel (<= 2 per resampled token, 12 B each)
+        if not self.push("lda", "push-model", self.want_pt, self.glob, None, sparse=True):
             raise IOError("push failed")
 
     def _pull(self) -> torch.Tensor:

@@ -375,14 +375,19 @@ def _id_sets(comm: Communicator, table: Table) -> List[List[int]]:
 
 
 @_guard("push")
-def push(comm: Communicator, local: Table, global_table: Table, partitioner: Optional[Partitioner] = None) -> bool:
+def push(comm: Communicator, local: Table, global_table: Table, partitioner: Optional[Partitioner] = None,
+         sparse: bool = False) -> bool:
     """Parameter-server push: local partitions are combined into the global table at
     the owner of each id (lowest rank holding it), or inserted at the partitioner's
-    owner when no worker holds the id yet. The local table is unchanged."""
+    owner when no worker holds the id yet. The local table is unchanged. ``sparse``
+    (dense packed tables, SUM): move only the nonzero elements (:func:`plans.push_sparse`)."""
     P = comm.world_size
     partitioner = partitioner or Partitioner(P)
     if plans.dense_pair(comm, local, global_table):
-        plans.push_dense(comm, local, global_table, partitioner)
+        if sparse:
+            plans.push_sparse(comm, local, global_table, partitioner)
+        else:
+            plans.push_dense(comm, local, global_table, partitioner)
         return True
     owner: Dict[int, int] = {}
     for r, ids in enumerate(_id_sets(comm, global_table)):

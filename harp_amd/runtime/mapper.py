@@ -172,7 +172,9 @@ class CollectiveMapper:
         return self._timed(ctx, op, "pull", C.pull, local, global_table, use_bcast)
 
     def push(self, ctx: str, op: str, local: Table, global_table: Table,
-             partitioner: Optional[Partitioner] = None) -> bool:
+             partitioner: Optional[Partitioner] = None, sparse: bool = False) -> bool:
+        if sparse:
+            return self._timed(ctx, op, "push", C.push, local, global_table, partitioner, sparse=True)
         return self._timed(ctx, op, "push", C.push, local, global_table, partitioner)
 
     def rotate(self, ctx: str, op: str, table: Table, rotate_map=None) -> bool:

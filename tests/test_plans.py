@@ -112,3 +112,27 @@ def test_combine_rows_ops():
     m = torch.full((2, 2), -float("inf"))
     plans.combine_rows(m, torch.tensor([1, 1]), torch.tensor([[1., 7], [3, 4]]), "MAX")
     assert m[1].tolist() == [3, 7]
+
+
+def _sparse_job(comm, op_sparse):
+    P, r = comm.world_size, comm.rank
+    comb = ArrCombiner(Operation.SUM)
+    g = PackedTable(list(range(r, 10, P)), torch.zeros(len(range(r, 10, P)), 3, 4, dtype=torch.int32), combiner=comb)
+    ids = sorted({1, 3, 4, 7, 9, 11 + r})  # 11+r: nobody owns it -> inserted at its partitioner owner
+    gen = torch.Generator().manual_seed(r)
+    buf = torch.randint(-2, 3, (len(ids), 3, 4), generator=gen, dtype=torch.int32)
+    buf[buf.abs() == 1] = 0  # sparse
+    l = PackedTable(ids, buf, combiner=comb)
+    assert C.push(comm, l, g, Partitioner(P), sparse=op_sparse)
+    assert C.push(comm, l, g, Partitioner(P), sparse=op_sparse)  # cached plan
+    return {i: g[i].clone() for i in g.sorted_ids()}
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_sparse_push_equals_dense_push(P):
+    dense = launch(_sparse_job, P, args=(False,), timeout=300)
+    sparse = launch(_sparse_job, P, args=(True,), timeout=300)
+    for a, b in zip(dense, sparse):
+        assert sorted(a) == sorted(b)
+        for i in a:
+            assert torch.equal(a[i], b[i]), (i, a[i], b[i])
