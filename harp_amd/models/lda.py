@@ -400,7 +400,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
 
     def _pull(self) -> torch.Tensor:
         self.pull_buf.zero_()  # pull combines into the local rows
-        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True):
+        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, sparse=True):
             raise IOError("pull failed")
         return self.pull_buf.view(-1, self.Kp)
 

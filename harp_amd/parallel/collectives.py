@@ -418,14 +418,17 @@ def push(comm: Communicator, local: Table, global_table: Table, partitioner: Opt
 
 
 @_guard("pull")
-def pull(comm: Communicator, local: Table, global_table: Table, use_bcast: bool = True) -> bool:
+def pull(comm: Communicator, local: Table, global_table: Table, use_bcast: bool = True, sparse: bool = False) -> bool:
     """Parameter-server pull: every local partition whose id exists in some worker's
     global table receives a copy of it, combined into the local partition. The global
     table is unchanged (callers zero the local partitions first, as the reference's
     K-means does at KMeansDaalCollectiveMapper.java:527-529)."""
     P = comm.world_size
     if plans.dense_pair(comm, local, global_table):
-        plans.pull_dense(comm, local, global_table, use_bcast)
+        if sparse:  # only nonzero elements travel (plans.pull_sparse)
+            plans.pull_sparse(comm, local, global_table, use_bcast)
+        else:
+            plans.pull_dense(comm, local, global_table, use_bcast)
         return True
     owner: Dict[int, int] = {}
     for r, ids in enumerate(_id_sets(comm, global_table)):

@@ -369,6 +369,95 @@ def pull_dense(comm: Communicator, local: PackedTable, glob: PackedTable, use_bc
     _store(local, plan, mine)
 
 
+def _gather_var(comm: Communicator, t: torch.Tensor) -> List[torch.Tensor]:
+    """Variable-length all-gather of a 1-D tensor (size exchange + one padded all-gather)."""
+    P = comm.world_size
+    if P == 1:
+        return [t]
+    sizes = comm.all_gather_ints([t.numel()])[:, 0].tolist()
+    mx = max(max(sizes), 1)
+    buf = torch.zeros(mx, dtype=t.dtype, device=comm.device)
+    buf[: t.numel()] = t.to(comm.device)
+    out = torch.empty(P * mx, dtype=t.dtype, device=comm.device)
+    comm.all_gather_into(out, buf)
+    return [out[r * mx:r * mx + sizes[r]] for r in range(P)]
+
+
+def pull_sparse(comm: Communicator, local: PackedTable, glob: PackedTable, use_bcast: bool = True) -> int:
+    """Pull moving only the NONZERO elements of the owners' rows (word-topic counts are
+    mostly zero): routing from the cached pull plan; the ids every worker wants go by a
+    variable-size all-gather of (position, value) pairs, the rest by one all-to-all-v.
+    SUM-combined into the local rows like a dense pull. Returns elements received."""
+    if _op_name(local) not in ("SUM", "PLUS"):
+        raise ValueError("sparse pull combines by addition")
+    mine = (local.ids_hash(), glob.ids_hash(), len(local), len(glob))
+    key = _plan_key(comm, "pull", local, glob, (bool(use_bcast),))
+    plan = _cached(local, key) or _build_pull(comm, local, glob, use_bcast, key)
+    _store(local, plan, mine)
+    P, dev = comm.world_size, comm.device
+    rs = 1
+    for x in local.part_shape:
+        rs *= int(x)
+    lflat = local.buffer.view(-1)
+    got = 0
+    # broadcast part: every owner's all-wanted rows, as (position in its bc block, value)
+    mx = max(plan.bc_counts) if plan.bc_counts else 0
+    if mx:
+        if plan.bc_idx.numel():
+            blk = glob.buffer.index_select(0, plan.bc_idx).reshape(-1)
+            nz = torch.nonzero(blk).reshape(-1)
+            pos, val = nz, blk[nz]
+        else:
+            pos = torch.zeros(0, dtype=torch.int64, device=glob.buffer.device)
+            val = torch.zeros(0, dtype=glob.buffer.dtype, device=glob.buffer.device)
+        lmap = getattr(plan, "bc_lmap", None)
+        if lmap is None:
+            lmap = torch.full((P * mx,), -1, dtype=torch.int64, device=local.buffer.device)
+            lmap[plan.bc_src] = plan.bc_dst
+            plan.bc_lmap = lmap
+        allp, allv = _gather_var(comm, pos), _gather_var(comm, val)
+        for o in range(P):
+            p_o, v_o = allp[o].to(local.buffer.device), allv[o].to(local.buffer.device)
+            if not p_o.numel():
+                continue
+            lrow = lmap[o * mx + p_o // rs]
+            ok = lrow >= 0
+            lflat.index_add_(0, lrow[ok] * rs + p_o[ok] % rs, v_o[ok].to(lflat.dtype))
+            got += int(ok.sum())
+    # all-to-all part: rows in each requester's request order
+    if plan.send_idx.numel():
+        rows = glob.buffer.index_select(0, plan.send_idx).reshape(-1)
+        nz = torch.nonzero(rows).reshape(-1)
+        val = rows[nz]
+        seq = nz // rs  # row position in the send sequence
+        starts = torch.tensor([0] + list(torch.tensor(plan.send_counts).cumsum(0).tolist()), dtype=torch.int64,
+                              device=seq.device)
+        dest = torch.searchsorted(starts[1:], seq, right=True)
+        rel = (seq - starts[dest]) * rs + nz % rs
+        counts = torch.bincount(dest, minlength=P).to(torch.int64)
+    else:
+        rel = torch.zeros(0, dtype=torch.int64, device=dev)
+        val = torch.zeros(0, dtype=glob.buffer.dtype, device=dev)
+        counts = torch.zeros(P, dtype=torch.int64, device=dev)
+    if P == 1:
+        r_rel, r_val, rr = rel, val, counts.tolist()
+    else:
+        rc = torch.empty(P, dtype=torch.int64, device=dev)
+        comm.all_to_all_single(rc, counts.to(dev))
+        ss, rr = counts.tolist(), rc.cpu().tolist()
+        r_rel = torch.empty(sum(rr), dtype=torch.int64, device=dev)
+        r_val = torch.empty(sum(rr), dtype=val.dtype, device=dev)
+        comm.all_to_all_single(r_rel, rel.contiguous().to(dev), rr, ss)
+        comm.all_to_all_single(r_val, val.contiguous().to(dev), rr, ss)
+    if r_rel.numel():
+        rstart = torch.tensor([0] + list(torch.tensor(plan.recv_counts).cumsum(0).tolist()), dtype=torch.int64)
+        src = torch.repeat_interleave(torch.arange(P), torch.tensor(rr)).to(r_rel.device)
+        lrow = plan.recv_dst.to(r_rel.device)[rstart.to(r_rel.device)[src] + r_rel // rs]
+        lflat.index_add_(0, (lrow * rs + r_rel % rs).to(lflat.device), r_val.to(lflat.dtype).to(lflat.device))
+        got += int(r_rel.numel())
+    return got
+
+
 # ------------------------------------------------------------------------------- regroup
 @dataclass
 class RegroupPlan:

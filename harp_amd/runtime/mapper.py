@@ -168,7 +168,10 @@ class CollectiveMapper:
     def aggregate(self, ctx: str, op: str, table: Table, partitioner, function: PartitionFunction) -> bool:
         return self._timed(ctx, op, "aggregate", C.aggregate, table, partitioner, function)
 
-    def pull(self, ctx: str, op: str, local: Table, global_table: Table, use_bcast: bool = True) -> bool:
+    def pull(self, ctx: str, op: str, local: Table, global_table: Table, use_bcast: bool = True,
+             sparse: bool = False) -> bool:
+        if sparse:
+            return self._timed(ctx, op, "pull", C.pull, local, global_table, use_bcast, sparse=True)
         return self._timed(ctx, op, "pull", C.pull, local, global_table, use_bcast)
 
     def push(self, ctx: str, op: str, local: Table, global_table: Table,

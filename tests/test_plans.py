@@ -136,3 +136,31 @@ def test_sparse_push_equals_dense_push(P):
         assert sorted(a) == sorted(b)
         for i in a:
             assert torch.equal(a[i], b[i]), (i, a[i], b[i])
+
+
+def _sparse_pull_job(comm, sparse):
+    P, r = comm.world_size, comm.rank
+    comb = ArrCombiner(Operation.SUM)
+    gids = list(range(r, 12, P))
+    gen = torch.Generator().manual_seed(10 + r)
+    gb = torch.randint(0, 4, (len(gids), 2, 5), generator=gen, dtype=torch.int32)
+    gb[gb == 1] = 0
+    g = PackedTable(gids, gb, combiner=comb)
+    lids = sorted(set(list(range(4)) + [5 + r, 8 + (r % 2), 13]))  # 0..3 all-wanted, 13 owned by nobody
+    out = []
+    for _ in range(2):  # second call: cached plan
+        l = PackedTable(lids, torch.full((len(lids), 2, 5), 7, dtype=torch.int32), combiner=comb)
+        assert C.pull(comm, l, g, True, sparse=sparse)
+        out.append({i: l[i].clone() for i in l.sorted_ids()})
+    return out
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_sparse_pull_equals_dense_pull(P):
+    dense = launch(_sparse_pull_job, P, args=(False,), timeout=300)
+    sparse = launch(_sparse_pull_job, P, args=(True,), timeout=300)
+    for a, b in zip(dense, sparse):
+        for x, y in zip(a, b):
+            assert sorted(x) == sorted(y)
+            for i in x:
+                assert torch.equal(x[i], y[i]), (i, x[i], y[i])
