@@ -39,6 +39,7 @@ class LDAConfig:
     seed: int = 0
     max_chunk: int = 0        # tokens per word chunk; 0 = 2048 (dense sampler) / 65536 (sparse)
     block_words: int = 4096   # push/pull strategy: words per model partition
+    sparse_comm: str = "auto"  # push/pull: move nonzero counts only ("on"/"off"; auto: >1 worker and K >= 4096)
     checkpoint_dir: str = ""  # .hpt checkpoints (token topics, doc-topic, resident word slices)
     checkpoint_every: int = 0  # iterations between checkpoints (0: never)
     model_dir: str = ""       # word-model dumps every print_interval*10 iterations + at the end
@@ -393,14 +394,22 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self._push_delta()  # initial counts = a delta against an all-zero model
         self.vbeta = self.vocab * cfg.beta
 
+    def _sparse(self) -> bool:
+        """Nonzero-only push / pull: the count scan costs a pass over the slab, so it pays
+        only when the dense rows would cross xGMI and are mostly zero (large K)."""
+        m = self.cfg.sparse_comm
+        if m == "auto":
+            return self.get_num_workers() > 1 and self.Kp >= 4096
+        return m == "on"
+
     def _push_delta(self) -> None:
-        # only the nonzero count changes travel (<= 2 per resampled token, 12 B each)
-        if not self.push("lda", "push-model", self.want_pt, self.glob, None, sparse=True):
+        # sparse: only the nonzero count changes travel (<= 2 per resampled token, 12 B each)
+        if not self.push("lda", "push-model", self.want_pt, self.glob, None, sparse=self._sparse()):
             raise IOError("push failed")
 
     def _pull(self) -> torch.Tensor:
         self.pull_buf.zero_()  # pull combines into the local rows
-        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, sparse=True):
+        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, sparse=self._sparse()):
             raise IOError("pull failed")
         return self.pull_buf.view(-1, self.Kp)
 

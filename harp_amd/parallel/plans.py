@@ -259,7 +259,7 @@ def push_sparse(comm: Communicator, local: PackedTable, glob: PackedTable, parti
     for x in local.part_shape:
         rs *= int(x)
     flat = local.buffer.reshape(-1)
-    nz = torch.nonzero(flat).reshape(-1)
+    nz = nonzero_flat(flat)
     vals = flat[nz]
     row = nz // rs
     dest = plan.dest_rank[row]
@@ -369,6 +369,17 @@ def pull_dense(comm: Communicator, local: PackedTable, glob: PackedTable, use_bc
     _store(local, plan, mine)
 
 
+def nonzero_flat(x: torch.Tensor, step: int = 1 << 30) -> torch.Tensor:
+    """Flat int64 indices of the nonzeros of ``x``, in chunks of ``step`` elements (one
+    nonzero call over > 2^31 elements is not supported by every backend)."""
+    flat = x.reshape(-1)
+    n = flat.numel()
+    if n <= step:
+        return torch.nonzero(flat).reshape(-1)
+    parts = [torch.nonzero(flat[a:a + step]).reshape(-1) + a for a in range(0, n, step)]
+    return torch.cat(parts)
+
+
 def _gather_var(comm: Communicator, t: torch.Tensor) -> List[torch.Tensor]:
     """Variable-length all-gather of a 1-D tensor (size exchange + one padded all-gather)."""
     P = comm.world_size
@@ -405,7 +416,7 @@ def pull_sparse(comm: Communicator, local: PackedTable, glob: PackedTable, use_b
     if mx:
         if plan.bc_idx.numel():
             blk = glob.buffer.index_select(0, plan.bc_idx).reshape(-1)
-            nz = torch.nonzero(blk).reshape(-1)
+            nz = nonzero_flat(blk)
             pos, val = nz, blk[nz]
         else:
             pos = torch.zeros(0, dtype=torch.int64, device=glob.buffer.device)
@@ -427,7 +438,7 @@ def pull_sparse(comm: Communicator, local: PackedTable, glob: PackedTable, use_b
     # all-to-all part: rows in each requester's request order
     if plan.send_idx.numel():
         rows = glob.buffer.index_select(0, plan.send_idx).reshape(-1)
-        nz = torch.nonzero(rows).reshape(-1)
+        nz = nonzero_flat(rows)
         val = rows[nz]
         seq = nz // rs  # row position in the send sequence
         starts = torch.tensor([0] + list(torch.tensor(plan.send_counts).cumsum(0).tolist()), dtype=torch.int64,

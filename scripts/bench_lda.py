@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-chunk", type=int, default=0, help="tokens per word chunk (0: LDAConfig default)")
     ap.add_argument("--strategy", default="rotation", choices=["rotation", "push_pull"])
+    ap.add_argument("--sparse-comm", default="auto", choices=["auto", "on", "off"])
     a = ap.parse_args()
     import torch
 
@@ -36,7 +37,8 @@ def main():
     t0 = time.perf_counter()
     toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
     gen = time.perf_counter() - t0
-    cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters)
+    cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters,
+                    sparse_comm=a.sparse_comm)
     if a.max_chunk:
         cfg.max_chunk = a.max_chunk
     cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper
