@@ -39,7 +39,8 @@ class LDAConfig:
     seed: int = 0
     max_chunk: int = 0        # tokens per word chunk; 0 = 2048 (dense sampler) / 65536 (sparse)
     block_words: int = 4096   # push/pull strategy: words per model partition
-    sparse_comm: str = "auto"  # push/pull: move nonzero counts only ("on"/"off"; auto: >1 worker and K >= 4096)
+    sparse_comm: str = "off"  # push/pull: "on" moves nonzero counts only (profiles/r2_apps: the torch
+                              # nonzero / index_add compaction costs 0.15-0.26 s per iteration)
     checkpoint_dir: str = ""  # .hpt checkpoints (token topics, doc-topic, resident word slices)
     checkpoint_every: int = 0  # iterations between checkpoints (0: never)
     model_dir: str = ""       # word-model dumps every print_interval*10 iterations + at the end
@@ -400,7 +401,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         m = self.cfg.sparse_comm
         if m == "auto":
             return self.get_num_workers() > 1 and self.Kp >= 4096
-        return m == "on"
+        return m == "on"  # default off: see LDAConfig.sparse_comm
 
     def _push_delta(self) -> None:
         # sparse: only the nonzero count changes travel (<= 2 per resampled token, 12 B each)

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-chunk", type=int, default=0, help="tokens per word chunk (0: LDAConfig default)")
     ap.add_argument("--strategy", default="rotation", choices=["rotation", "push_pull"])
-    ap.add_argument("--sparse-comm", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--sparse-comm", default="off", choices=["auto", "on", "off"])
     a = ap.parse_args()
     import torch
 
