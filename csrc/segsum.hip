@@ -19,8 +19,6 @@
 //               bucket skew) in fp32 registers, flushing at bucket boundaries
 #include "common.h"
 
-#include <cstdlib>
-
 namespace {
 
 constexpr int SEG = 64;  // chunks per column-scan segment
@@ -115,7 +113,7 @@ __global__ __launch_bounds__(256) void bucket_kernel(const int* __restrict__ lab
 // bucket-sorted permutation (so work is balanced whatever the bucket sizes), keeps the
 // running row sum in registers, and flushes it with one contiguous fp32 atomic row segment
 // whenever it crosses a bucket boundary (~1 flush per slot for buckets >> RUN).
-template <int LPR, int RUN, int UNR = 4>
+template <int LPR, int RUN>
 __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restrict__ X, int dp, const int* __restrict__ perm,
                                                           const int* __restrict__ start, int K, long n,
                                                           float* __restrict__ sums, int ld) {
@@ -155,21 +153,17 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restri
       kend = start[k + 1];
     }
     long stop = kend < j1 ? kend : j1;
-    // UNR rows in flight per slot inside one bucket
-    for (; j + UNR <= stop; j += UNR) {
-      bf16x8 v[UNR];
-      int pj[UNR];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) pj[u] = perm[j + u];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) v[u] = active ? *(const bf16x8*)(X + (long)pj[u] * dp + sl * 8) : bf16x8{};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float t = 0.f;
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) t += (float)v[u][e];
-        acc[e] += t;
+    // 4 rows in flight per slot inside one bucket
+    for (; j + 4 <= stop; j += 4) {
+      bf16x8 v0{}, v1{}, v2{}, v3{};
+      if (active) {
+        v0 = *(const bf16x8*)(X + (long)perm[j] * dp + sl * 8);
+        v1 = *(const bf16x8*)(X + (long)perm[j + 1] * dp + sl * 8);
+        v2 = *(const bf16x8*)(X + (long)perm[j + 2] * dp + sl * 8);
+        v3 = *(const bf16x8*)(X + (long)perm[j + 3] * dp + sl * 8);
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += ((float)v0[e] + (float)v1[e]) + ((float)v2[e] + (float)v3[e]);
     }
     for (; j < stop; ++j) {
       if (active) {
@@ -184,15 +178,6 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restri
 }
 
 }  // namespace
-
-// rows in flight per 16-lane slot in the gather-sum (HARP_ROWSUM_UNROLL=8 to try 8; default 4)
-static int rowsum_unroll() {
-  static int u = [] {
-    const char* e = getenv("HARP_ROWSUM_UNROLL");
-    return (e && atoi(e) == 8) ? 8 : 4;
-  }();
-  return u;
-}
 
 // Labels per histogram chunk: 65536 for large n; smaller for small n so the histogram and
 // scatter passes still launch >= ~1500 workgroups (6 rounds over 256 CUs); >= 4096 keeps
@@ -244,10 +229,7 @@ HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, const int* perm, 
   const __bf16* Xb = (const __bf16*)X;
   constexpr int RUN = 256;
   auto grid = [&](int lpr) { return dim3((unsigned)(((n + RUN - 1) / RUN * lpr + 255) / 256)); };
-  const int unr = rowsum_unroll();
   if (lpr_min <= 8) rowsum_bf16_kernel<8, RUN><<<grid(8), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
-  else if (lpr_min <= 16 && unr == 8)
-    rowsum_bf16_kernel<16, RUN, 8><<<grid(16), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
   else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN><<<grid(16), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
   else rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
   return harp_launch_status();
