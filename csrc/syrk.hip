@@ -54,7 +54,8 @@ __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long 
 
 // DIAG (timing diagnostics only, results are garbage): 1 = no global loads after the first
 // stage (MFMA + LDS + barriers), 2 = no MFMA (loads + LDS reads + a VALU use of the
-// fragments), 3 = loads + barriers only
+// fragments), 3 = loads + barriers only, 4 = every stage loads the first stage's (L2-hot)
+// samples (same instruction stream, no L2 misses)
 template <int MT_, int BA_, int BB_, int DIAG = 0>
 __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void syrk_kernel(
     const __bf16* __restrict__ XT, long ld, long n, int nt, long chunk, float* __restrict__ G, int ldg,
@@ -115,9 +116,11 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
         __syncthreads();
       }
     }
-    if (DIAG != 1 && k0 + KT < kend) {
-      stage_panel<C>(XT, ld, ti * MT, k0 + KT, smem + (cur ^ 1) * PANEL, wave, lane);
-      if (!diag) stage_panel<C>(XT, ld, tj * MT, k0 + KT, smem + (2 + (cur ^ 1)) * PANEL, wave, lane);
+    const bool more = DIAG != 1 && k0 + KT < kend;
+    const long kn = DIAG == 4 ? kbeg : k0 + KT;  // DIAG 4: every stage re-reads the first (L2-hot)
+    if (more) {
+      stage_panel<C>(XT, ld, ti * MT, kn, smem + (cur ^ 1) * PANEL, wave, lane);
+      if (!diag) stage_panel<C>(XT, ld, tj * MT, kn, smem + (2 + (cur ^ 1)) * PANEL, wave, lane);
     }
     const char* A = smem + cur * PANEL;
     const char* B = diag ? A : smem + (2 + cur) * PANEL;
@@ -269,6 +272,7 @@ HARP_EXPORT int harp_syrk_diag(const void* XT, long ld, long n, int d_pad, float
     case 1: return launch_syrk<256, 2, 4, 1>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     case 2: return launch_syrk<256, 2, 4, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     case 3: return launch_syrk<256, 2, 4, 3>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 4: return launch_syrk<256, 2, 4, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     default: return HARP_EBADARG;
   }
 }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """SYRK bottleneck split (csrc/syrk.hip harp_syrk_diag): time the default 256-tile kernel
 with (0) everything, (1) no global loads after the first stage, (2) no MFMA, (3) loads +
-barriers only, on the PCA shape. python scripts/syrk_diag.py [--n 1e8] [--d 1000]"""
+barriers only, (4) L2-hot loads (every stage re-reads the first), on the PCA shape. python scripts/syrk_diag.py [--n 1e8] [--d 1000]"""
 import argparse
 import json
 import os
@@ -28,7 +28,7 @@ def main():
     G = torch.zeros((fm.d_pad, fm.d_pad), dtype=torch.float32, device="cuda")
     lib = _lib.kernels()
     out = {"n": int(a.n), "d": a.d}
-    for mode in (0, 1, 2, 3):
+    for mode in (0, 1, 2, 3, 4):
         def run():
             _lib.check(lib.harp_syrk_diag(fm.XT.data_ptr(), fm.ld, fm.ld, fm.d_pad, G.data_ptr(), G.stride(0),
                                           a.splits, mode, _lib.stream_ptr(G.device)), "syrk_diag")
