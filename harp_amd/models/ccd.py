@@ -182,7 +182,22 @@ def train_ccd_rotation(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: 
         rot.wait_all()
 
     hist: List[Dict[str, float]] = []
-    for it in range(cfg.iterations):
+    # checkpoint: each rank's home slices (after every tour the slices are back home)
+    from ..utils.checkpoint import Checkpointer, tensor_table
+
+    ck = Checkpointer(cfg.checkpoint_dir, comm, cfg.checkpoint_every)
+    start = 0
+    got = ck.load_latest(device=dev, rng=True)
+    if got is not None:
+        man, tabs = got
+        if man["world"] != P:
+            raise ValueError(f"CCD rotation-mode resume needs the checkpoint's world size {man['world']}, got {P}")
+        for k in range(S):
+            rot.slabs[2 * k].copy_(tabs[f"W{k}"].buffer.to(dev))
+            rot.slabs[2 * k + 1].copy_(tabs[f"H{k}"].buffer.to(dev))
+        hist = list(man["extra"].get("history", []))
+        start = int(man["iteration"]) + 1
+    for it in range(start, cfg.iterations):
         t0 = time.perf_counter()
         res_u.copy_(uval)
         tour(lambda Ws, Hs: C.residual(ur, uc, res_u, Ws[mine_u], Hs, res_u))
@@ -196,6 +211,12 @@ def train_ccd_rotation(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: 
                "train_rmse": rmse(comm, (res_i.double() ** 2).sum(), res_i.numel())}
         hist.append(rec)
         inject_fault(me, it)
+        if ck.due(it):
+            tabs = {}
+            for k in range(S):
+                tabs[f"W{k}"] = tensor_table(rot.slabs[2 * k])
+                tabs[f"H{k}"] = tensor_table(rot.slabs[2 * k + 1])
+            ck.save(it, tabs, extra={"history": list(hist), "mode": "rotation"})
     # assemble this rank's owned rows of the full factors (one tour; for the result only)
     W = torch.zeros((n_mu, ns * rs), dtype=dt, device=dev)
     H = torch.zeros((n_mi, ns * rs), dtype=dt, device=dev)
@@ -222,5 +243,5 @@ def train_ccd_rotation(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: 
                                      int(mine.sum()))
     if cfg.model_dir:
         save_factor_models(comm, cfg.model_dir, {"W": (W, my_users), "H": (H, my_items)})
-    return {"W": W, "H": H, "start_iteration": 0, "user_ids": my_users, "item_ids": my_items, "history": hist,
+    return {"W": W, "H": H, "start_iteration": start, "user_ids": my_users, "item_ids": my_items, "history": hist,
             "slab_floats_per_rank": sum(x.numel() for x in slabs)}

@@ -241,3 +241,23 @@ def test_kmeans_resume_on_other_world_size(tmp_path, strategy):
     m.init_model(KeyValReader([]))
     assert m.resume() == 6
     assert torch.allclose(m.c[:10], two[0]["centroids"], atol=1e-6)
+
+
+def _ccd_rot_job(comm, d):
+    from harp_amd.models.ccd import CCDConfig, train_ccd
+
+    u, i, v = _mf_tr()
+    P, r = comm.world_size, comm.rank
+    sl = slice(r * u.numel() // P, (r + 1) * u.numel() // P)
+    res = train_ccd(comm, u[sl], i[sl], v[sl], 200, 70,
+                    CCDConfig(rank=6, iterations=5, mode="rotation", checkpoint_dir=str(d), checkpoint_every=1))
+    return {"W": res["W"].cpu(), "H": res["H"].cpu(), "start": res["start_iteration"], "hist": res["history"]}
+
+
+def test_ccd_rotation_mode_kill_and_resume(tmp_path):
+    ref = launch(_ccd_rot_job, 2, args=(tmp_path / "ref",), timeout=300)
+    res = launch(_ccd_rot_job, 2, args=(tmp_path / "ft",), timeout=300, retries=1, env=FAULT)
+    assert [x["start"] for x in res] == [2, 2]
+    for a, b in zip(ref, res):
+        assert torch.allclose(a["W"], b["W"], atol=1e-9) and torch.allclose(a["H"], b["H"], atol=1e-9)
+        assert len(b["hist"]) == 5
