@@ -249,6 +249,8 @@ def run(args) -> int:
         build_kernels()
     from harp_amd.runtime.launcher import init_distributed, shutdown
 
+    # bounded collective watchdog for the bench (a stuck peer fails the run in minutes, not 30)
+    os.environ.setdefault("HARP_DATA_MAX_WAIT_TIME", "600")
     comm = init_distributed(backend)
     if backend == "gloo" and torch.cuda.is_available():
         from harp_amd.parallel.comm import Communicator
@@ -263,7 +265,12 @@ def run(args) -> int:
         torch.cuda.empty_cache()
     want_sgd = args.sgd == "on" or (args.sgd == "auto" and comm.device.type == "cuda")
     if want_sgd:
-        rec["sgd"] = bench_sgd(args, comm, torch)
+        # the nested record must never cost the headline line: a failure is reported inside it
+        try:
+            rec["sgd"] = bench_sgd(args, comm, torch)
+        except Exception as e:  # noqa: BLE001
+            rec["sgd"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+            print(f"bench: MF-SGD record failed on rank {comm.rank}: {e!r}", file=sys.stderr)
     if comm.rank == 0:
         print(json.dumps(rec), flush=True)
     shutdown()

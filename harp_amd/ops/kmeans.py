@@ -18,6 +18,7 @@ Layouts (chosen for the MFMA kernel):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -65,6 +66,23 @@ def generate_points(n: int, d: int, lo: float = 0.0, hi: float = 1000.0, seed: i
     g = torch.Generator().manual_seed(seed * 1000003 + row0)
     x = torch.rand((n, d), generator=g, dtype=torch.float32) * (hi - lo) + lo
     return pack_points(x, device)
+
+
+_SIDE: dict = {}
+
+
+def pipeline_chunks(n: int, ppb: int) -> int:
+    """Chunks the bucketed assign is split into (env HARP_KMEANS_CHUNKS, default 1 = one
+    assign then one bucket + gather-sum). Small inputs always run unchunked."""
+    c = int(os.environ.get("HARP_KMEANS_CHUNKS", "1"))
+    return max(1, min(c, n // (ppb * 256)))  # every chunk still fills the chip
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
 
 
 @dataclass
@@ -129,16 +147,37 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             assert sums.device == dev
         assert X.dtype == torch.bfloat16 and X.is_contiguous() and op.Cm2.shape[1] == dp
         fused = sums if accumulate == "atomic" else None
-        st = lib.harp_kmeans_assign(X.data_ptr(), op.Cm2.data_ptr(), n, dp, op.Cm2.shape[0], op.d,
-                                    labels.data_ptr(), _lib.ptr(fused), fused.stride(0) if fused is not None else 0,
-                                    _lib.ptr(obj_partial) if want_objective else None, _lib.ptr(min_dist), variant,
-                                    _lib.stream_ptr(dev))
-        _lib.check(st, "kmeans_assign")
-        if sums is not None and fused is None:
+        bucket = sums is not None and fused is None
+        chunks = pipeline_chunks(n, ppb) if bucket else 1
+        per = (nblk + chunks - 1) // chunks * ppb  # rows per chunk, a whole number of workgroups
+        side = _side_stream(dev) if chunks > 1 else None
+        main = torch.cuda.current_stream(dev)
+        for r0 in range(0, n, per):
+            r1 = min(n, r0 + per)
+            b0 = r0 // ppb
+            st = lib.harp_kmeans_assign(X[r0].data_ptr(), op.Cm2.data_ptr(), r1 - r0, dp, op.Cm2.shape[0], op.d,
+                                        labels[r0].data_ptr(), _lib.ptr(fused),
+                                        fused.stride(0) if fused is not None else 0,
+                                        obj_partial[b0].data_ptr() if want_objective else None,
+                                        min_dist[r0].data_ptr() if min_dist is not None else None, variant,
+                                        _lib.stream_ptr(dev))
+            _lib.check(st, "kmeans_assign")
+            if not bucket:
+                continue
             from . import segment
 
-            perm, start = segment.bucket_labels(labels, op.Cm2.shape[0])
-            segment.bucket_rowsum(X, perm, start, sums)
+            if side is None:
+                perm, start = segment.bucket_labels(labels, op.Cm2.shape[0])
+                segment.bucket_rowsum(X, perm, start, sums)
+                continue
+            # bucket + gather-sum of this chunk on the side stream while the next chunk's
+            # assign runs: the memory-bound row sums fill the gaps of the MFMA-bound assign
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                perm, start = segment.bucket_labels(labels[r0:r1], op.Cm2.shape[0])
+                segment.bucket_rowsum(X[r0:r1], perm, start, sums)
+        if side is not None:
+            main.wait_stream(side)
         obj = obj_partial[:nblk].double().sum() if want_objective else None
         return labels, obj
     # CPU reference (fp32)

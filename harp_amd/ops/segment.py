@@ -40,10 +40,12 @@ def bucket_labels(labels: torch.Tensor, K: int) -> Tuple[torch.Tensor, torch.Ten
     lib = _lib.kernels()
     _lib_ret_long(lib.harp_bucket_workspace_ints)
     need = lib.harp_bucket_workspace_ints(n, K)
-    key = (labels.device, n, K)
+    stream = torch.cuda.current_stream(labels.device).cuda_stream
+    key = (labels.device, n, K, stream)
     ws = _WS.get(key)
     if ws is None:
-        _WS.clear()  # keep one workspace alive
+        for k in [k for k in _WS if k[3] == stream]:
+            del _WS[k]  # one workspace alive per stream (allocated and reused on that stream)
         ws = torch.empty(need, dtype=torch.int32, device=labels.device)
         _WS[key] = ws
     so, po = ctypes.c_long(0), ctypes.c_long(0)

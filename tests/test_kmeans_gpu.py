@@ -135,3 +135,27 @@ def test_kmeans_hip_graph_iterations_match_eager(cuda):
         torch.cuda.synchronize()
         out[graph] = m.c[:300].clone()
     assert torch.allclose(out[True], out[False], rtol=1e-5, atol=1e-3), (out[True] - out[False]).abs().max()
+
+
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_chunked_side_stream_pipeline_matches_single_pass(cuda, monkeypatch, chunks):
+    """HARP_KMEANS_CHUNKS: assign of chunk i+1 overlaps bucket + gather-sum of chunk i on a
+    side stream; labels, objective, min distances and (x, count) sums equal the one-pass run."""
+    n, d, k = 1024 * 256 * 3 + 777, 100, 500
+    torch.manual_seed(1)
+    X = K.pack_points(torch.rand(n, d, device=cuda) * 1000, cuda)
+    op = K.prepare(torch.rand(k, d, device=cuda) * 1000, X.shape[1])
+    out = {}
+    for c in (1, chunks):
+        monkeypatch.setenv("HARP_KMEANS_CHUNKS", str(c))
+        sums = torch.zeros((K.padded_k(k), X.shape[1]), dtype=torch.float32, device=cuda)
+        md = torch.empty(n, dtype=torch.float32, device=cuda)
+        lab, obj = K.assign(X, op, sums=sums, min_dist=md)
+        torch.cuda.synchronize()
+        out[c] = (lab.clone(), obj.item(), md.clone(), sums)
+    assert K.pipeline_chunks(n, 1024) == chunks
+    a, b = out[1], out[chunks]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+    assert b[1] == pytest.approx(a[1], rel=1e-9)
+    assert torch.allclose(a[3], b[3], rtol=1e-5, atol=1e-2)
+    assert int(b[3][:, d].sum().item()) == n
