@@ -70,6 +70,7 @@ EXTRA = {  # named-only flags
     "sgd": [("num_users", int, 0), ("num_items", int, 0)],
     "ccd": [("num_users", int, 0), ("num_items", int, 0)],
     "daal": [("k", int, 0), ("method", str, ""), ("label_cols", int, 1)],
+    "mds": [("work_dir", str, "harp-work/mds"), ("checkpoint_every", int, 0)],
 }
 
 
@@ -276,8 +277,24 @@ def _run_mds(comm, cfg):
         lo, hi = max(a, off), min(b, off + blk.shape[0])
         if lo < hi:
             rows[lo - a:hi - a] = blk[lo - off:hi - off, :n]
+    every = cfg["checkpoint_every"] or 0
     res = wda_mds(comm, rows, torch.ones_like(rows), a, n,
-                  MDSConfig(d=cfg["d"], alpha=cfg["alpha"], threshold=cfg["threshold"], cg_iter=cfg["cg_iter"]))
+                  MDSConfig(d=cfg["d"], alpha=cfg["alpha"], threshold=cfg["threshold"], cg_iter=cfg["cg_iter"],
+                            checkpoint_dir=os.path.join(cfg["work_dir"], "checkpoints") if every > 0 else "",
+                            checkpoint_every=every))
+    if comm.rank == 0 and cfg["work_dir"]:
+        from .utils.model_io import write_mds_points
+
+        labels = None
+        if cfg["labels_file"]:  # "<id> <label>" lines (the reference's label file)
+            lab = {}
+            with open(cfg["labels_file"]) as f:
+                for ln in f:
+                    t = ln.split()
+                    if len(t) >= 2:
+                        lab[int(t[0])] = int(t[1])
+            labels = [lab.get(i, 1) for i in range(n)]
+        write_mds_points(os.path.join(cfg["work_dir"], "X"), res["X"], labels)
     return {"stress": res["stress"], "smacof_iters": res["smacof_iters"], "X": res["X"].cpu()}
 
 

@@ -24,6 +24,7 @@ coordinates and B is never materialised).
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -42,6 +43,9 @@ class MDSConfig:
     cg_iter: int = 20
     max_iter: int = 10000
     seed: int = 0
+    checkpoint_dir: str = ""   # .hpt checkpoint after every ``checkpoint_every`` annealing stages
+    checkpoint_every: int = 1
+    model_dir: str = ""        # X written as <model_dir>/X (XFileUtil.storeXOnMaster format)
 
 
 def _dist_block(Xr: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
@@ -151,6 +155,20 @@ def wda_mds(comm: Communicator, delta_rows: torch.Tensor, weight_rows: torch.Ten
     hist: List[Dict[str, float]] = []
     t0 = time.perf_counter()
     smacof = 0
+    # checkpoint unit = one annealing stage: X is replicated (bit-identical on every
+    # worker), so it is saved once and a restart may use any number of workers
+    from ..runtime.mapper import inject_fault
+    from ..utils.checkpoint import Checkpointer, tensor_table
+
+    ck = Checkpointer(cfg.checkpoint_dir, comm, cfg.checkpoint_every)
+    stage_no, start_stage = 0, 0
+    got = ck.load_latest(device=dev)
+    if got is not None:
+        man, tabs = got
+        ex = man["extra"]
+        X = tabs["X"].buffer.to(dev, dt).reshape(n, cfg.d).clone()
+        T, smacof, hist = float(ex["T"]), int(ex["smacof"]), list(ex["history"])
+        stage_no = start_stage = int(man["iteration"]) + 1
 
     def stress(X, T):
         return float(rows.allsum(rows.stress(X, T, cfg.d).reshape(1))[0]) / sum_sq
@@ -171,13 +189,29 @@ def wda_mds(comm: Communicator, delta_rows: torch.Tensor, weight_rows: torch.Ten
                 return X, s
             pre = s
 
+    def after_stage(X, T_next):
+        nonlocal stage_no
+        inject_fault(comm.rank, stage_no)
+        if ck.due(stage_no):
+            ck.save(stage_no, {"X": tensor_table(X)}, extra={"T": T_next, "smacof": smacof, "history": hist},
+                    replicated=("X",))
+        stage_no += 1
+
+    s = hist[-1]["stress"] if hist else float("nan")
     while T > t_min:
         X, s = stage(X, T)
         hist.append({"T": T, "stress": s})
         T *= cfg.alpha
-    X, s = stage(X, 0.0)
-    hist.append({"T": 0.0, "stress": s})
-    return {"X": X, "stress": s, "history": hist, "smacof_iters": smacof, "time_s": time.perf_counter() - t0}
+        after_stage(X, T)
+    if not (hist and hist[-1]["T"] == 0.0):
+        X, s = stage(X, 0.0)
+        hist.append({"T": 0.0, "stress": s})
+    if cfg.model_dir and comm.rank == 0:
+        from ..utils.model_io import write_mds_points
+
+        write_mds_points(os.path.join(cfg.model_dir, "X"), X)
+    return {"X": X, "stress": s, "history": hist, "smacof_iters": smacof, "time_s": time.perf_counter() - t0,
+            "start_stage": start_stage}
 
 
 def _max():

@@ -261,3 +261,34 @@ def test_ccd_rotation_mode_kill_and_resume(tmp_path):
     for a, b in zip(ref, res):
         assert torch.allclose(a["W"], b["W"], atol=1e-9) and torch.allclose(a["H"], b["H"], atol=1e-9)
         assert len(b["hist"]) == 5
+
+
+def _mds_job(comm, d, model_dir=""):
+    from harp_amd.models import mds as MD
+    from tests.test_mds import _problem
+
+    D, W = _problem(30, seed=4)
+    P, r = comm.world_size, comm.rank
+    a, b = r * 30 // P, (r + 1) * 30 // P
+    cfg = MD.MDSConfig(d=3, alpha=0.8, threshold=1e-6, checkpoint_dir=str(d), checkpoint_every=1, model_dir=model_dir)
+    out = MD.wda_mds(comm, D[a:b], W[a:b], a, 30, cfg)
+    return {"X": out["X"].cpu(), "stress": out["stress"], "start": out["start_stage"], "hist": out["history"]}
+
+
+def test_mds_kill_and_resume_and_x_file(tmp_path):
+    """Annealing-stage checkpoints of the replicated embedding: a rank killed in stage 2
+    (before its checkpoint) restarts at stage 2 and ends bit-identical to the uninterrupted run; rank 0 writes X in
+    the reference's storeXOnMaster format."""
+    from harp_amd.utils.model_io import read_mds_points
+
+    ref = launch(_mds_job, 2, args=(tmp_path / "ref",), timeout=300)
+    res = launch(_mds_job, 2, args=(tmp_path / "ft", str(tmp_path / "model")), timeout=300, retries=1, env=FAULT)
+    assert [x["start"] for x in res] == [2, 2]
+    for a, b in zip(ref, res):
+        assert torch.equal(a["X"], b["X"]) and a["hist"] == b["hist"]
+    ids, X, labels = read_mds_points(str(tmp_path / "model" / "X"))
+    assert ids.tolist() == list(range(30)) and labels == [1] * 30
+    assert torch.allclose(X, res[0]["X"], atol=1e-9)
+    # the replicated X resumes on a different world size
+    one = launch(_mds_job, 1, args=(tmp_path / "ft",), timeout=300)[0]
+    assert one["start"] == len(ref[0]["hist"]) - 1  # every annealing stage was checkpointed

@@ -105,8 +105,11 @@ def test_cli_lda_ccd_subgraph_mds_daal(tmp_path):
             q[b * 12:(b + 1) * 12].tofile(str(tmp_path / "mds" / f"distance_{b}"))
             f.write(f"{b}\t12\t24\t{b}\t{b * 12}\n")
     res = _run(["mds", "2", str(tmp_path / "mds"), "distance_", "w_", "v_", str(tmp_path / "mds" / "ids"), "",
-                "1e-7", "3", "0.9", "24", "20", "1"])
+                "1e-7", "3", "0.9", "24", "20", "1", "--work-dir", str(tmp_path / "mdsout")])
     assert res["stress"] < 1e-3
+    with open(tmp_path / "mdsout" / "X") as f:
+        lines = f.read().splitlines()
+    assert len(lines) == 24 and lines[5].split("\t")[0] == "5" and lines[5].endswith("\t1")
     # daal-style pca on dense CSV files
     os.makedirs(tmp_path / "pca")
     X = torch.randn(200, 5, generator=g, dtype=torch.float64) @ torch.randn(5, 5, generator=g, dtype=torch.float64)
