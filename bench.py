@@ -57,6 +57,7 @@ def parse_args(argv=None):
     ap.add_argument("--sgd-rank", type=int, default=128)
     ap.add_argument("--sgd-epochs", type=int, default=5)
     ap.add_argument("--sgd-warmup", type=int, default=1)
+    ap.add_argument("--sgd-slices", type=int, default=2, help="H slices per rank (rotation pipeline depth)")
     ap.add_argument("--metrics-jsonl", default="", help="per-iteration phase/bytes records (JSONL)")
     return ap.parse_args(argv)
 
@@ -170,7 +171,7 @@ def bench_sgd(args, comm, torch):
     t0 = time.perf_counter()
     u, i, v = synthetic_ratings(args.sgd_users, args.sgd_items, args.sgd_ratings, seed=7, device=dev)
     cfg = SGDConfig(rank=args.sgd_rank, epochs=args.sgd_warmup + args.sgd_epochs, test_every=0,
-                    xcd_blocks=dev.type == "cuda")
+                    xcd_blocks=dev.type == "cuda", num_slices=args.sgd_slices)
     m = SGDCollectiveMapper(comm, cfg, args.sgd_users, args.sgd_items, (u, i, v), None)
     m.init_model(_Reader())
     del u, i, v

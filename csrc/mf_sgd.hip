@@ -714,6 +714,8 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
                      : variant == 2 ? launch_sgd_xcd<RR, 64, false, 6>(SGDX_ARGS)                    \
                      : variant == 3 ? launch_sgd_xcd<RR, 64, false, 7>(SGDX_ARGS)                    \
                                     : launch_sgd_xcd<RR, 64, false, 8>(SGDX_ARGS))                   \
+                : chunk == 8 ? launch_sgd_xcd<RR, 8>(SGDX_ARGS)                                     \
+                : chunk == 16 ? launch_sgd_xcd<RR, 16>(SGDX_ARGS)                                   \
                 : chunk == 32 ? launch_sgd_xcd<RR, 32>(SGDX_ARGS)                                   \
                               : chunk == 64 ? launch_sgd_xcd<RR, 64>(SGDX_ARGS)                     \
                                             : chunk == 128 ? launch_sgd_xcd<RR, 128>(SGDX_ARGS)     \

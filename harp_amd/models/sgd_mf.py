@@ -36,7 +36,7 @@ class SGDConfig:
     lr: float = 0.002          # epsilon
     epochs: int = 10
     num_slices: int = 2        # model slices per worker (numModelSlices)
-    chunk: int = 64            # ratings per GPU update stream
+    chunk: int = 0             # ratings per GPU update stream (0 = auto: ops.mf.auto_chunk)
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
     kernel_variant: int = 0    # blocked kernel variant (reserved)

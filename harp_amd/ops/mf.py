@@ -72,6 +72,7 @@ def sgd_update(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: to
     if n == 0:
         return 0
     r = W.shape[1]
+    chunk = chunk if chunk > 0 else 64
     if _lib.use_native(W):
         _require_rank(r)
         st = _lib.kernels().harp_mf_sgd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, chunk, W.data_ptr(),
@@ -107,6 +108,21 @@ def balanced_blocks(group: torch.Tensor, idx: torch.Tensor, n_groups: int, n_idx
     return blk.view(-1)[flat]
 
 
+def auto_chunk(n: int, blocks_per_xcd: int) -> int:
+    """Ratings per update stream for an XCD-blocked pass over ``n`` ratings. A stream's
+    ratings form one dependent chain (~0.6 us each: H row from L2, dot, update), so a
+    kernel lasts at least chunk x that; with the 8-GPU per-rank share (12.5M Netflix
+    ratings, 16 rotation sub-steps) chunk 64 left most of each XCD's 16 x blocks_per_xcd
+    stream slots idle and every launch took ~40 us for ~100K ratings. Halve from 64 until
+    the average cell fills the XCD's stream slots (floor 8)."""
+    cell = n / float(XCDS * XCDS)
+    slots = 16 * max(1, blocks_per_xcd)
+    ch = 64
+    while ch > 8 and cell / ch < slots:
+        ch //= 2
+    return ch
+
+
 def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, cell_off: torch.Tensor,
                        W: torch.Tensor, H: torch.Tensor, lr: float, lam: float, chunk: int = 64,
                        blocks_per_xcd: int = 256, host_off: list | None = None, variant: int = 0,
@@ -117,8 +133,8 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     row- and column-disjoint cells (x, (x+s) mod nb): on the GPU one XCD per cell
     (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
     ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path).
-    ``chunk``: ratings per stream (32, 64 or 128 on the GPU); ``variant``: 0, or 1 = non-temporal
-    H stores (slower; see csrc/mf_sgd.hip).
+    ``chunk``: ratings per stream (8, 16, 32, 64 or 128 on the GPU; <= 0 = :func:`auto_chunk`);
+    ``variant``: 0, or 1 = non-temporal H stores (slower; see csrc/mf_sgd.hip).
     ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
     ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
     CPU only: ``threads > 1`` or a ``time_budget`` (s) run the cells through the 2-D
@@ -139,6 +155,9 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
         if window is not None:
             win = torch.tensor(list(window[0]) + list(window[1]), dtype=torch.int64).pin_memory()
             win = win.to(W.device, non_blocking=True)
+        if chunk <= 0:  # wide ranks (one wave per stream) take 32 / 64 / 128 only
+            chunk = (auto_chunk(trained, blocks_per_xcd) if r <= 256 else max(32, auto_chunk(trained, blocks_per_xcd))) \
+                if variant == 0 else 64
         lib = _lib.kernels()
         st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
                                  _lib.ptr(win), r, nb, chunk,

@@ -153,3 +153,12 @@ def test_sgd_fixed_fraction_mode(small):
     n = train[0].numel()
     assert abs(sum(r["trained"] for r in res) - 12 * n) <= 2 * 64 * 2 * 24  # ceil per cell
     assert res[0]["rmse"][-1][2] < 0.6
+
+
+def test_auto_chunk_fills_the_xcd_stream_slots():
+    from harp_amd.ops.mf import auto_chunk
+
+    assert auto_chunk(50_240_253, 128) == 64   # 1 GPU, 2 slices: big cells keep long streams
+    assert auto_chunk(6_280_032, 128) == 32    # 8 GPUs, 2 slices per rank: ~98K ratings per cell
+    assert auto_chunk(785_004, 128) == 8       # 8 GPUs, 2 slices, 8 rotation steps: ~12K per cell
+    assert auto_chunk(10, 128) == 8            # floor
