@@ -409,8 +409,11 @@ class LDAPushPullMapper(LDACollectiveMapper):
             raise IOError("push failed")
 
     def _pull(self) -> torch.Tensor:
-        self.pull_buf.zero_()  # pull combines into the local rows
-        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, sparse=self._sparse()):
+        sparse = self._sparse()
+        if sparse:
+            self.pull_buf.zero_()  # a sparse pull combines nonzeros into zeroed rows
+        # dense: every needed block has an owner, so the overwrite pull rewrites all of them
+        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, sparse=sparse, overwrite=not sparse):
             raise IOError("pull failed")
         return self.pull_buf.view(-1, self.Kp)
 

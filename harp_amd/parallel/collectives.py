@@ -418,17 +418,22 @@ def push(comm: Communicator, local: Table, global_table: Table, partitioner: Opt
 
 
 @_guard("pull")
-def pull(comm: Communicator, local: Table, global_table: Table, use_bcast: bool = True, sparse: bool = False) -> bool:
+def pull(comm: Communicator, local: Table, global_table: Table, use_bcast: bool = True, sparse: bool = False,
+         overwrite: bool = False) -> bool:
     """Parameter-server pull: every local partition whose id exists in some worker's
     global table receives a copy of it, combined into the local partition. The global
     table is unchanged (callers zero the local partitions first, as the reference's
-    K-means does at KMeansDaalCollectiveMapper.java:527-529)."""
+    K-means does at KMeansDaalCollectiveMapper.java:527-529). ``overwrite`` (packed
+    tables, dense transfer): the received rows replace the local ones -- the same result
+    as zeroing them first, without the extra pass."""
     P = comm.world_size
+    if overwrite and (sparse or not plans.dense_pair(comm, local, global_table)):
+        raise ValueError("overwrite pull needs packed tables and a dense transfer")
     if plans.dense_pair(comm, local, global_table):
         if sparse:  # only nonzero elements travel (plans.pull_sparse)
             plans.pull_sparse(comm, local, global_table, use_bcast)
         else:
-            plans.pull_dense(comm, local, global_table, use_bcast)
+            plans.pull_dense(comm, local, global_table, use_bcast, overwrite=overwrite)
         return True
     owner: Dict[int, int] = {}
     for r, ids in enumerate(_id_sets(comm, global_table)):

@@ -54,9 +54,46 @@ def identity_value(op: str, dtype: torch.dtype):
     return 0
 
 
-def combine_rows(dst: torch.Tensor, idx: torch.Tensor, rows: torch.Tensor, op: str) -> None:
-    """``dst[idx[j]] (op)= rows[j]`` for every j (duplicates in ``idx`` all combine)."""
+_ELEMENTWISE = {"SUM": torch.Tensor.add_, "PLUS": torch.Tensor.add_, "MULTIPLY": torch.Tensor.mul_,
+                "PROD": torch.Tensor.mul_,
+                "MAX": lambda d, r: torch.maximum(d, r, out=d), "MIN": lambda d, r: torch.minimum(d, r, out=d)}
+
+
+def _is_identity(idx: Optional[torch.Tensor], n: int) -> bool:
+    """``idx`` == arange(n) (checked once per plan; one device sync at plan build)."""
+    if idx is None or idx.numel() != n:
+        return False
+    return n == 0 or bool(torch.equal(idx, torch.arange(n, dtype=idx.dtype, device=idx.device)))
+
+
+def _flag(plan: "_Plan", name: str, idx: Optional[torch.Tensor], n: int) -> bool:
+    v = getattr(plan, name, None)
+    if v is None:
+        v = _is_identity(idx, n)
+        setattr(plan, name, v)
+    return v
+
+
+def _take(buf: torch.Tensor, idx: torch.Tensor, ident: bool) -> torch.Tensor:
+    """Rows ``buf[idx]``; the buffer itself when ``idx`` is every row in order (no copy)."""
+    if ident:
+        return buf
+    return buf.index_select(0, idx) if idx.numel() else buf[:0]
+
+
+def combine_rows(dst: torch.Tensor, idx: torch.Tensor, rows: torch.Tensor, op: str, ident: bool = False) -> None:
+    """``dst[idx[j]] (op)= rows[j]`` for every j (duplicates in ``idx`` all combine).
+    ``ident``: ``idx`` is arange(len(dst)) -- one elementwise pass instead of an index op."""
     if rows.numel() == 0:
+        return
+    if op == "REPLACE":  # overwrite pull: each destination row receives exactly one row
+        if ident and rows.shape == dst.shape:
+            dst.copy_(rows)
+        else:
+            dst.index_copy_(0, idx, rows.to(dst.dtype))
+        return
+    if ident and rows.shape == dst.shape and op in _ELEMENTWISE:
+        _ELEMENTWISE[op](dst, rows.to(dst.dtype))
         return
     if op in ("SUM", "PLUS"):
         dst.index_add_(0, idx, rows.to(dst.dtype))
@@ -231,9 +268,9 @@ def push_dense(comm: Communicator, local: PackedTable, glob: PackedTable, partit
                           dtype=glob.buffer.dtype, device=glob.buffer.device)
         glob.set_contents(glob.ids + plan.new_ids, torch.cat([glob.buffer, fill]))
         plan.new_ids = []  # the layout now includes them; the cached plan stays valid
-    send = local.buffer.index_select(0, plan.send_idx) if plan.send_idx.numel() else local.buffer[:0]
+    send = _take(local.buffer, plan.send_idx, _flag(plan, "_send_ident", plan.send_idx, len(local)))
     recv = _alltoall_rows(comm, send, plan.send_counts, plan.recv_counts, glob.buffer)
-    combine_rows(glob.buffer, plan.recv_dst, recv, op)
+    combine_rows(glob.buffer, plan.recv_dst, recv, op, _flag(plan, "_recv_ident", plan.recv_dst, len(glob)))
     _store(local, plan, mine)
 
 
@@ -287,10 +324,10 @@ def push_sparse(comm: Communicator, local: PackedTable, glob: PackedTable, parti
 def _alltoall_rows(comm: Communicator, send: torch.Tensor, send_counts, recv_counts, like: torch.Tensor):
     dev = comm.device
     shape = tuple(like.shape[1:])
+    if comm.world_size == 1:  # the rows stay on this rank: no staging copy
+        return send if send.device == like.device else send.to(like.device)
     recv = torch.empty((sum(recv_counts),) + shape, dtype=like.dtype, device=dev)
-    if comm.world_size == 1:
-        recv.copy_(send.to(dev))
-    elif sum(send_counts) or sum(recv_counts):
+    if sum(send_counts) or sum(recv_counts):
         s = send.contiguous().to(dev)
         if s.dtype == torch.bool:
             s = s.to(torch.uint8)
@@ -345,13 +382,15 @@ def _build_pull(comm: Communicator, local: PackedTable, glob: PackedTable, use_b
                  bc_src=t(bc_src, ldev), bc_dst=t(bc_dst, ldev))
 
 
-def pull_dense(comm: Communicator, local: PackedTable, glob: PackedTable, use_bcast: bool = True) -> None:
+def pull_dense(comm: Communicator, local: PackedTable, glob: PackedTable, use_bcast: bool = True,
+               overwrite: bool = False) -> None:
     """Dense pull (see module doc): every local row whose id some global table holds
-    receives (combines) the owner's row."""
+    receives (combines) the owner's row. ``overwrite``: it is replaced instead, which
+    equals zeroing those rows first and combining by SUM, in one pass fewer."""
     mine = (local.ids_hash(), glob.ids_hash(), len(local), len(glob))
     key = _plan_key(comm, "pull", local, glob, (bool(use_bcast),))
     plan = _cached(local, key) or _build_pull(comm, local, glob, use_bcast, key)
-    op = _op_name(local)
+    op = "REPLACE" if overwrite else _op_name(local)
     mx = max(plan.bc_counts) if plan.bc_counts else 0
     if mx:
         blk = torch.zeros((mx,) + glob.part_shape, dtype=glob.buffer.dtype, device=comm.device)
@@ -363,9 +402,9 @@ def pull_dense(comm: Communicator, local: PackedTable, glob: PackedTable, use_bc
         if plan.bc_src.numel():
             rows = allb.index_select(0, plan.bc_src.to(comm.device))
             combine_rows(local.buffer, plan.bc_dst, rows.to(local.buffer.device), op)
-    send = glob.buffer.index_select(0, plan.send_idx) if plan.send_idx.numel() else glob.buffer[:0]
+    send = _take(glob.buffer, plan.send_idx, _flag(plan, "_send_ident", plan.send_idx, len(glob)))
     recv = _alltoall_rows(comm, send, plan.send_counts, plan.recv_counts, local.buffer)
-    combine_rows(local.buffer, plan.recv_dst, recv, op)
+    combine_rows(local.buffer, plan.recv_dst, recv, op, _flag(plan, "_recv_ident", plan.recv_dst, len(local)))
     _store(local, plan, mine)
 
 

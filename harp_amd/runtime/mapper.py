@@ -169,9 +169,11 @@ class CollectiveMapper:
         return self._timed(ctx, op, "aggregate", C.aggregate, table, partitioner, function)
 
     def pull(self, ctx: str, op: str, local: Table, global_table: Table, use_bcast: bool = True,
-             sparse: bool = False) -> bool:
+             sparse: bool = False, overwrite: bool = False) -> bool:
         if sparse:
             return self._timed(ctx, op, "pull", C.pull, local, global_table, use_bcast, sparse=True)
+        if overwrite:
+            return self._timed(ctx, op, "pull", C.pull, local, global_table, use_bcast, overwrite=True)
         return self._timed(ctx, op, "pull", C.pull, local, global_table, use_bcast)
 
     def push(self, ctx: str, op: str, local: Table, global_table: Table,

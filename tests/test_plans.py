@@ -164,3 +164,43 @@ def test_sparse_pull_equals_dense_pull(P):
             assert sorted(x) == sorted(y)
             for i in x:
                 assert torch.equal(x[i], y[i]), (i, x[i], y[i])
+
+
+def _overwrite_job(comm):
+    P, r = comm.world_size, comm.rank
+    comb = ArrCombiner(Operation.SUM)
+    gids = list(range(r, 12, P))
+    g = PackedTable(gids, torch.stack([torch.full((2, 3), float(10 * i + 1)) for i in gids]), combiner=comb)
+    lids = sorted(set(list(range(4)) + [5 + r, 8 + (r % 2)]))  # 0..3 wanted by all: the broadcast route
+    out = []
+    for over in (False, True):
+        for _ in range(2):  # second call: cached plan (identity flags reused)
+            l = PackedTable(lids, torch.full((len(lids), 2, 3), -7.0), combiner=comb)
+            if not over:
+                l.buffer.zero_()
+            assert C.pull(comm, l, g, True, overwrite=over)
+        out.append({i: l[i].clone() for i in l.sorted_ids()})
+    return out
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_overwrite_pull_equals_zero_then_sum(P):
+    for zeroed, over in launch(_overwrite_job, P, timeout=300):
+        assert sorted(zeroed) == sorted(over)
+        for i in zeroed:
+            assert torch.equal(zeroed[i], over[i]), (i, zeroed[i], over[i])
+            assert float(over[i][0, 0]) == 10 * i + 1
+
+
+def test_identity_fast_path_matches_index_ops():
+    d = torch.arange(12.).reshape(4, 3)
+    a, b = d.clone(), d.clone()
+    rows = torch.ones(4, 3) * 2
+    idx = torch.arange(4)
+    assert plans._is_identity(idx, 4) and not plans._is_identity(idx.flip(0), 4)
+    plans.combine_rows(a, idx, rows, "SUM", ident=True)
+    plans.combine_rows(b, idx, rows, "SUM")
+    assert torch.equal(a, b)
+    plans.combine_rows(a, idx, rows * 5, "MAX", ident=True)
+    plans.combine_rows(b, idx, rows * 5, "MAX")
+    assert torch.equal(a, b)
