@@ -21,6 +21,8 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
+from ..ops import linalg as LA
+
 from ..parallel.comm import Communicator
 from .common import reduce_partials
 
@@ -169,11 +171,11 @@ def em_gmm(X: torch.Tensor, K: int, comm: Optional[Communicator] = None, n_itera
         lse = torch.logsumexp(logp, 1)
         R = torch.exp(logp - lse[:, None])  # [n, K]
         Nk = R.sum(0)
-        S1 = R.t() @ Xd
+        S1 = LA.atb(R, Xd)
         if covariance == "full":
             S2 = torch.einsum("nk,ni,nj->kij", R, Xd, Xd)
         else:
-            S2 = R.t() @ (Xd * Xd)
+            S2 = LA.atb(R, Xd * Xd)
         st = reduce_partials(comm or _one(), {"Nk": Nk.cpu(), "S1": S1.cpu(), "S2": S2.cpu(),
                                               "ll": lse.sum().reshape(1).cpu(),
                                               "n": torch.tensor([float(n)])})

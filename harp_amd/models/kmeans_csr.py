@@ -18,6 +18,8 @@ from typing import Dict, Optional
 
 import torch
 
+from ..ops import linalg as LA
+
 from ..parallel.comm import Communicator
 from .common import gather_rows, reduce_partials
 
@@ -113,7 +115,7 @@ def kmeans_sparse(X, C0: torch.Tensor, iterations: int = 10, comm: Optional[Comm
             S = torch.sparse.mm(X.double().t() if X.layout != torch.sparse_csr else
                                 X.to_sparse_coo().double().t(), onehot).t()
         else:
-            S = onehot.t() @ X.double()
+            S = LA.atb(onehot, X.double())
         r = reduce_partials(comm, {"S": S, "n": onehot.sum(0), "o": m.sum().reshape(1)})
         cnt = r["n"].to(C.device)
         nz = cnt > 0

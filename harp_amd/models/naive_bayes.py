@@ -12,6 +12,8 @@ from typing import Dict, Optional
 
 import torch
 
+from ..ops import linalg as LA
+
 from ..parallel.comm import Communicator
 from .common import reduce_partials
 from .stats import _local
@@ -33,7 +35,7 @@ def train(X: torch.Tensor, y: torch.Tensor, num_classes: int, comm: Optional[Com
         sums.index_put_((yl[rows], cols), Xc.values().to(acc), accumulate=True)
     else:
         onehot = torch.nn.functional.one_hot(yl, num_classes).to(acc)
-        sums = onehot.t() @ X.to(acc)
+        sums = LA.atb(onehot, X.to(acc))
     counts = torch.bincount(yl, minlength=num_classes).to(acc)
     p = reduce_partials(comm, {"sums": sums, "counts": counts})
     fs = p["sums"] + alpha

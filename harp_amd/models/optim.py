@@ -19,6 +19,8 @@ from typing import Callable, Optional, Sequence
 
 import torch
 
+from ..ops import linalg as LA
+
 from ..parallel.comm import Communicator
 from .common import reduce_partials
 
@@ -115,7 +117,7 @@ class CrossEntropyLoss(Objective):
         v = torch.nn.functional.cross_entropy(Z, yl, reduction="sum")
         R = torch.softmax(Z, 1)
         R[torch.arange(Xb.shape[0], device=Xb.device), yl] -= 1
-        G = R.t() @ Xb
+        G = LA.atb(R, Xb)
         if self.intercept:
             G = torch.cat([R.sum(0)[:, None], G], 1)
         return v, G.reshape(-1), Xb.shape[0]

@@ -116,11 +116,57 @@ def _native_tsqr(X: torch.Tensor) -> bool:
 
     return X.device.type == "cuda" and X.shape[1] <= TSQR_MAX_D and _lib.use_native(X)
 
-def tsqr(X: torch.Tensor, comm: Optional[Communicator] = None, want_q: bool = True) -> Dict[str, torch.Tensor]:
+CHOLQR_MAX_DIAG_RATIO = 1e5  # max(diag R) / min(diag R) beyond which CholeskyQR2 is not trusted
+
+
+def cholesky_qr2(X: torch.Tensor, comm: Optional[Communicator] = None) -> Optional[Dict[str, torch.Tensor]]:
+    """Distributed CholeskyQR2 in fp64: G = sum_ranks X^T X (one d x d allreduce), R1 =
+    chol(G), Q1 = X R1^-1; the same again on Q1 restores orthogonality to ~1e-15, R =
+    R2 R1. Every flop is a GEMM / TRSM on the fp64 matrix cores and the data is read a
+    handful of times, against D sequential Householder steps of the panel kernels.
+
+    Stable while cond(X) is well below 1e8; returns None (the caller falls back to
+    Householder TSQR) when the Cholesky fails or the R1 diagonal spread -- a lower bound of
+    cond(X) -- exceeds ``CHOLQR_MAX_DIAG_RATIO``. The decision is taken from allreduced
+    values, so every worker takes the same branch."""
+    comm = _local(comm)
+    Xd = X.double().contiguous()
+    Q, R = Xd, None
+    for _ in range(2):
+        G = reduce_partials(comm, {"g": LA.atb(Q, Q)})["g"].to(Xd.device)
+        L, info = torch.linalg.cholesky_ex(G)
+        if int(info) != 0:
+            return None
+        Rk = L.t().contiguous()
+        dg = torch.diagonal(Rk)
+        if R is None and float(dg.max()) > CHOLQR_MAX_DIAG_RATIO * float(dg.min().clamp_min(1e-300)):
+            return None
+        # Q R^-1 as one GEMM with the d x d triangular inverse (a right-side TRSM over the
+        # tall matrix measured ~200x slower in rocBLAS and runs out of workspace)
+        eye = torch.eye(Rk.shape[0], dtype=Rk.dtype, device=Rk.device)
+        Q = Q @ torch.linalg.solve_triangular(Rk, eye, upper=True)
+        R = Rk if R is None else Rk @ R
+    return {"Q": Q, "R": R}
+
+
+def tsqr(X: torch.Tensor, comm: Optional[Communicator] = None, want_q: bool = True,
+         method: str = "auto") -> Dict[str, torch.Tensor]:
     """Distributed tall-skinny QR (daal_qr 3-step: local QR -> QR of stacked R's -> local
-    Q update). The stacked R's are all-gathered so every worker runs step 2 itself."""
+    Q update). The stacked R's are all-gathered so every worker runs step 2 itself.
+
+    ``method``: "auto" (GPU: :func:`cholesky_qr2`, falling back to Householder for
+    ill-conditioned input; CPU: Householder), "cholqr2", or "householder". The result
+    (R with a non-negative diagonal, orthonormal Q) is the same either way."""
     comm = _local(comm)
     d = X.shape[1]
+    if method == "cholqr2" or (method == "auto" and X.device.type == "cuda"):  # same branch on every rank
+        out = cholesky_qr2(X, comm)
+        if out is not None:
+            if not want_q:
+                out.pop("Q")
+            return out
+        if method == "cholqr2":
+            raise ValueError("CholeskyQR2 failed (matrix too ill-conditioned)")
     if _native_tsqr(X):
         # step 1 on the hand-written fp64 Householder panel kernels (csrc/tsqr.hip)
         from ..ops.linalg import house_tsqr
@@ -133,7 +179,7 @@ def tsqr(X: torch.Tensor, comm: Optional[Communicator] = None, want_q: bool = Tr
         if want_q:
             out["Q"] = Q1 @ Q2[comm.rank * d:(comm.rank + 1) * d]
         return out
-    Xd = X.double() if X.device.type == "cpu" else X.float()
+    Xd = X.double() if X.device.type == "cpu" or X.dtype == torch.float64 else X.float()
     Q1, R1 = torch.linalg.qr(Xd, mode="reduced")
     Rs = gather_rows(comm, R1)  # [P*d, d]
     Q2, R = torch.linalg.qr(Rs.double(), mode="reduced")

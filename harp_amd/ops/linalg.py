@@ -45,6 +45,28 @@ def gram(X: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     return G if out is None else out.add_(G)
 
 
+ATB_CHUNK = 1000  # rows per batched slice of a tall A^T B
+
+
+def atb(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """A^T B for tall A [n, m], B [n, k] (n >> m, k). On the GPU the n rows are cut into
+    slices of ``ATB_CHUNK`` rows: one batched GEMM of the slices plus a sum. A single
+    GEMM with a reduction dimension of millions of rows is pathological in the library
+    kernels, especially in fp64: X^T X of 4e6 x 16 fp64 took 0.43 s as one mm and 0.3 ms
+    as 4000 batched slices (scripts/probe_fp64_gemm.py, profiles/r2_tsqr)."""
+    n = A.shape[0]
+    if A.device.type != "cuda" or n < 8 * ATB_CHUNK:
+        return A.t() @ B
+    c = n // ATB_CHUNK
+    m = c * ATB_CHUNK
+    At = A[:m].reshape(c, ATB_CHUNK, A.shape[1])
+    Bt = B[:m].reshape(c, ATB_CHUNK, B.shape[1])
+    out = torch.bmm(At.transpose(1, 2), Bt).sum(0)
+    if m < n:
+        out += A[m:].t() @ B[m:]
+    return out
+
+
 _lib.register({
     "harp_syrk_t_bf16": [_lib.c_void_p, _lib.c_long, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_int,
                          _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p],

@@ -81,3 +81,27 @@ def test_distributed_svd_uses_native_tsqr(cuda):
     U = out["leftSingularMatrix"]
     rec = U @ torch.diag(out["singularValues"]) @ out["rightSingularMatrix"]
     assert torch.allclose(rec, A, atol=1e-9)
+
+
+@pytest.mark.parametrize("d", [16, 64, 200])
+def test_tsqr_auto_cholqr2_on_gpu(cuda, d):
+    """GPU tsqr (method auto) = CholeskyQR2 on the fp64 matrix cores: exact QR of a
+    well-conditioned tall matrix; an ill-conditioned one falls back to Householder."""
+    from harp_amd.models import stats as ST
+
+    g = torch.Generator().manual_seed(d)
+    A = (torch.randn(100_000, d, generator=g, dtype=torch.float64) *
+         torch.logspace(0, 2, d, dtype=torch.float64)).to(cuda)
+    assert ST.cholesky_qr2(A) is not None
+    out = ST.tsqr(A)
+    Q, R = out["Q"], out["R"]
+    assert torch.allclose(Q.t() @ Q, torch.eye(d, dtype=torch.float64, device=cuda), atol=1e-12)
+    assert torch.allclose(Q @ R, A, atol=1e-9 * float(A.abs().max()))
+    _, Rt = torch.linalg.qr(A)
+    Rt = Rt * torch.sign(torch.diagonal(Rt))[:, None]
+    assert torch.allclose(R, Rt, rtol=1e-9, atol=1e-8)
+    bad = A.clone()
+    bad[:, -1] = bad[:, 0] * (1 + 1e-12)  # numerically rank-deficient
+    assert ST.cholesky_qr2(bad) is None
+    fb = ST.tsqr(bad)
+    assert torch.allclose(fb["Q"] @ fb["R"], bad, atol=1e-8 * float(bad.abs().max()))

@@ -146,3 +146,40 @@ def test_quality_metrics_and_batch_ops():
     Xo = torch.cat([torch.randn(200, 3, dtype=torch.float64), torch.full((5, 3), 25.0, dtype=torch.float64)])
     w = ST.outliers_bacon(Xo)
     assert w[-5:].sum() == 0 and w[:200].mean() > 0.9
+
+
+def _cholqr_job(comm, X):
+    from harp_amd.models import stats as ST
+
+    P, r = comm.world_size, comm.rank
+    n = X.shape[0]
+    Xs = X[r * n // P:(r + 1) * n // P]
+    out = ST.tsqr(Xs, comm, method="cholqr2")
+    return out["Q"], out["R"]
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_cholesky_qr2_distributed_matches_householder(P):
+    from harp_amd.runtime.launcher import launch
+
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(900, 12, generator=g, dtype=torch.float64) @ torch.diag(torch.logspace(0, 3, 12, dtype=torch.float64))
+    res = launch(_cholqr_job, P, args=(X,), timeout=120)
+    Q = torch.cat([q for q, _ in res])
+    R = res[0][1]
+    _, Rt = torch.linalg.qr(X)
+    Rt = Rt * torch.sign(torch.diagonal(Rt))[:, None]
+    assert torch.allclose(R, Rt, rtol=1e-10, atol=1e-9)
+    assert torch.allclose(Q.t() @ Q, torch.eye(12, dtype=torch.float64), atol=1e-13)
+    assert torch.allclose(Q @ R, X, atol=1e-10)
+
+
+def test_cholesky_qr2_refuses_ill_conditioned_and_auto_falls_back():
+    from harp_amd.models import stats as ST
+
+    g = torch.Generator().manual_seed(12)
+    X = torch.randn(500, 6, generator=g, dtype=torch.float64) @ torch.diag(torch.tensor([1, 1, 1, 1, 1, 1e-9],
+                                                                                        dtype=torch.float64))
+    assert ST.cholesky_qr2(X) is None
+    out = ST.tsqr(X, method="auto")  # CPU auto = Householder anyway; result must stay exact
+    assert torch.allclose(out["Q"] @ out["R"], X, atol=1e-12)
