@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
       dr[c] = g;
       atomicAdd(&colsum[c], g);  // LDS: 4 rows per column slot
     }
-    if (lane == 0) lrow = -(zr[y] - m - __logf(s));
+    // an out-of-range label contributes no target (and is never used as an index)
+    if (lane == 0 && y >= 0 && y < C) lrow = -(zr[y] - m - __logf(s));
   }
   if (lane == 0 && row < B) atomicAdd(loss, lrow);
   __syncthreads();

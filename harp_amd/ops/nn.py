@@ -25,6 +25,7 @@ def available(t: torch.Tensor) -> bool:
 def bias_act_(z: torch.Tensor, b: torch.Tensor | None, act: str) -> torch.Tensor:
     """In place: z = act(z + b) ([rows, N] fp32, contiguous)."""
     assert z.is_contiguous() and z.dtype == torch.float32
+    assert b is None or (b.is_contiguous() and b.numel() >= z.shape[1])
     _lib.check(_lib.kernels().harp_nn_bias_act(z.data_ptr(), _lib.ptr(b), z.shape[0], z.shape[1], ACT[act],
                                                _lib.stream_ptr(z.device)), "nn_bias_act")
     return z
@@ -36,6 +37,7 @@ def softmax_xent(z: torch.Tensor, labels: torch.Tensor, scale: float, delta: tor
     returns the summed cross-entropy loss (0-dim device tensor)."""
     B, C = z.shape
     assert z.is_contiguous() and delta.is_contiguous() and labels.dtype == torch.int32
+    assert delta.shape == z.shape and labels.numel() >= B and (dbias is None or dbias.numel() >= C)
     loss = torch.zeros(1, dtype=torch.float32, device=z.device)
     _lib.check(_lib.kernels().harp_nn_softmax_xent(z.data_ptr(), B, C, labels.data_ptr(), float(scale),
                                                    delta.data_ptr(), loss.data_ptr(), _lib.ptr(dbias),
@@ -46,7 +48,8 @@ def softmax_xent(z: torch.Tensor, labels: torch.Tensor, scale: float, delta: tor
 def dact_bgrad_(delta: torch.Tensor, a: torch.Tensor, act: str, dbias: torch.Tensor | None = None) -> torch.Tensor:
     """In place: delta *= act'(a) (a = activation values); dbias += column sums."""
     B, N = delta.shape
-    assert delta.is_contiguous() and a.is_contiguous()
+    assert delta.is_contiguous() and a.is_contiguous() and a.shape == delta.shape
+    assert dbias is None or dbias.numel() >= N
     _lib.check(_lib.kernels().harp_nn_dact_bgrad(delta.data_ptr(), a.data_ptr(), B, N, ACT[act], _lib.ptr(dbias),
                                                  _lib.stream_ptr(delta.device)), "nn_dact_bgrad")
     return delta
