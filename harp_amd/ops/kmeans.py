@@ -149,7 +149,7 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
         fused = sums if accumulate == "atomic" else None
         bucket = sums is not None and fused is None
         chunks = pipeline_chunks(n, ppb) if bucket else 1
-        per = (nblk + chunks - 1) // chunks * ppb  # rows per chunk, a whole number of workgroups
+        per = max(1, (nblk + chunks - 1) // chunks) * ppb  # rows per chunk, whole workgroups
         side = _side_stream(dev) if chunks > 1 else None
         main = torch.cuda.current_stream(dev)
         for r0 in range(0, n, per):
