@@ -62,20 +62,6 @@ template <class DT>
 struct DocRow;
 template <>
 struct DocRow<int> {
-  static constexpr int RAW_PER_T = 1;  // raw dwords per topic slot: TPL dwords per lane
-  template <int TPL>
-  __device__ static __forceinline__ void load_raw(const int* drow, int k0, unsigned (&r)[TPL]) {
-#pragma unroll
-    for (int t = 0; t < TPL; t += 4) {
-      const uint4 v = *(const uint4*)(drow + k0 + t);
-      r[t] = v.x; r[t + 1] = v.y; r[t + 2] = v.z; r[t + 3] = v.w;
-    }
-  }
-  template <int TPL>
-  __device__ static __forceinline__ void unpack(const unsigned (&r)[TPL], int (&nd)[TPL]) {
-#pragma unroll
-    for (int t = 0; t < TPL; ++t) nd[t] = (int)r[t];
-  }
   template <int TPL>
   __device__ static __forceinline__ void load(const int* drow, int k0, int (&nd)[TPL]) {
 #pragma unroll
@@ -85,37 +71,9 @@ struct DocRow<int> {
     }
   }
   __device__ static __forceinline__ void add(int* drow, int k, int v) { atomicAdd(drow + k, v); }
-  template <int TPL>
-  __device__ static __forceinline__ void patch(unsigned (&r)[TPL], int lane, int z, int nz) {
-#pragma unroll
-    for (int t = 0; t < TPL; ++t)
-      r[t] += (lane * TPL + t == nz ? 1u : 0u) - (lane * TPL + t == z ? 1u : 0u);
-  }
 };
 template <>
 struct DocRow<unsigned short> {
-  template <int TPL>
-  __device__ static __forceinline__ void load_raw(const unsigned short* drow, int k0, unsigned (&r)[TPL]) {
-    // only the first TPL/2 dwords are used: two 16-bit counts per dword
-    if constexpr (TPL % 8 != 0) {
-      const uint2 v = *(const uint2*)(drow + k0);
-      r[0] = v.x; r[1] = v.y;
-    } else {
-#pragma unroll
-      for (int t = 0; t < TPL / 2; t += 4) {
-        const uint4 v = *(const uint4*)(drow + k0 + 2 * t);
-        r[t] = v.x; r[t + 1] = v.y; r[t + 2] = v.z; r[t + 3] = v.w;
-      }
-    }
-  }
-  template <int TPL>
-  __device__ static __forceinline__ void unpack(const unsigned (&r)[TPL], int (&nd)[TPL]) {
-#pragma unroll
-    for (int q = 0; q < TPL / 2; ++q) {
-      nd[2 * q] = (int)(r[q] & 0xFFFFu);
-      nd[2 * q + 1] = (int)(r[q] >> 16);
-    }
-  }
   template <int TPL>
   __device__ static __forceinline__ void load(const unsigned short* drow, int k0, int (&nd)[TPL]) {
     static_assert(TPL % 4 == 0, "TPL must be a multiple of 4");
@@ -141,15 +99,6 @@ struct DocRow<unsigned short> {
       }
     }
   }
-  template <int TPL>
-  __device__ static __forceinline__ void patch(unsigned (&r)[TPL], int lane, int z, int nz) {
-#pragma unroll
-    for (int q = 0; q < TPL / 2; ++q) {
-      const int k = lane * TPL + 2 * q;
-      r[q] += (k == nz ? 1u : 0u) + (k + 1 == nz ? 0x10000u : 0u);
-      r[q] -= (k == z ? 1u : 0u) + (k + 1 == z ? 0x10000u : 0u);
-    }
-  }
   __device__ static __forceinline__ void add(unsigned short* drow, int k, int v) {
     unsigned* word = (unsigned*)(drow + (k & ~1));
     const unsigned sh = (k & 1) ? 16u : 0u;
@@ -158,15 +107,12 @@ struct DocRow<unsigned short> {
   }
 };
 
-// PF = 1: the doc-topic row of the NEXT token is loaded (raw) while this token samples, so
-// the random HBM row fetch leaves the per-token critical path; a row of the same document
-// is patched in registers with this token's topic move (the load was issued before this
-// token's atomics: same-wave program order), other documents' rows are Hogwild as before.
-// Measured (profiles/r1_lda/ldapf): 0.90e9 vs 1.17e9 tokens/s for PF = 0 at K = 1000 —
-// the extra 16 VGPRs drop occupancy from 4 to 3 waves/SIMD, and more resident waves hide
-// the row latency better than one-token-ahead prefetch; PF = 0 stays the default.
-template <int TPL, class DT, int PF = 0, int XW = 0>  // topics per lane; K_pad = 64 * TPL; XW: +waves/SIMD
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 ? 4 - PF + XW : 5 - PF + XW) < 8 ? (TPL == 16 ? 4 - PF + XW : 5 - PF + XW) : 8, 8))) void lda_cgs_kernel(
+// XW: extra waves per SIMD over the compiler's occupancy (a few VGPRs spill; more resident
+// waves hide the random doc-row fetch). A one-token-ahead doc-row prefetch measured slower
+// (0.90e9 vs 1.17e9 tokens/s at K = 1000, profiles/r1_lda/ldapf: its extra VGPRs cost a
+// wave per SIMD) and was removed.
+template <int TPL, class DT, int XW = 0>  // topics per lane; K_pad = 64 * TPL
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 ? 4 + XW : 5 + XW) < 8 ? (TPL == 16 ? 4 + XW : 5 + XW) : 8, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
@@ -206,43 +152,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     for (int t = 0; t < TPL; ++t) qw[t] = (nwf[t] + beta) * s_inv[k0 + t];
     int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
                                            // waits on ONE memory round trip, not two
-    unsigned rn[TPL];  // PF: raw doc row of the next token (in flight)
-    int d_nn = 0, z_nn = 0, pz = -1, pnz = -1;
-    if constexpr (PF) {
-      DocRow<DT>::template load_raw<TPL>(ndk + (long)d_next * ldd, k0, rn);
-      if (a + 1 < b) {
-        d_nn = tdoc[a + 1];
-        z_nn = tz[a + 1];
-      }
-    }
     for (long i = a; i < b; ++i) {
       const int d = d_next;
       const int z = z_next;
       DT* drow = ndk + (long)d * ldd;
       float nd[TPL];
-      if constexpr (PF) {
-        unsigned rc[TPL];
-#pragma unroll
-        for (int t = 0; t < TPL; ++t) rc[t] = rn[t];
-        if (pz >= 0) DocRow<DT>::template patch<TPL>(rc, lane, pz, pnz);  // previous token, same doc
-        if (i + 1 < b) {
-          d_next = d_nn;
-          z_next = z_nn;
-          DocRow<DT>::template load_raw<TPL>(ndk + (long)d_next * ldd, k0, rn);
-          if (i + 2 < b) {
-            d_nn = tdoc[i + 2];
-            z_nn = tz[i + 2];
-          }
-        }
-        int ndi[TPL];
-        DocRow<DT>::template unpack<TPL>(rc, ndi);
-#pragma unroll
-        for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
-      } else {
-        if (i + 1 < b) {
-          d_next = tdoc[i + 1];
-          z_next = tz[i + 1];
-        }
+      if (i + 1 < b) {
+        d_next = tdoc[i + 1];
+        z_next = tz[i + 1];
+      }
+      {
         int ndi[TPL];
         DocRow<DT>::template load<TPL>(drow, k0, ndi);
 #pragma unroll
@@ -305,10 +224,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
           atomicSub(&s_delta[z], 1);
           atomicAdd(&s_delta[nz], 1);
         }
-      }
-      if constexpr (PF) {  // the prefetched next row predates this move: patch it if same doc
-        pz = (d_next == d && i + 1 < b) ? z : -1;
-        pnz = nz;
       }
     }
     // flush this chunk's word-row delta
@@ -531,7 +446,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
 }  // namespace
 
 namespace {
-template <class DT, int PF, int XW = 0>
+template <class DT, int XW = 0>
 int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
                int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
                unsigned long long seed, hipStream_t s) {
@@ -540,15 +455,15 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
   const dim3 g((unsigned)blocks), bl(256);
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
-    lda_cgs_kernel<4, DT, PF, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<4, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                            nk_delta, K, alpha, beta, seed);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
-    lda_cgs_kernel<8, DT, PF, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<8, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                            nk_delta, K, alpha, beta, seed);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
-    lda_cgs_kernel<16, DT, PF, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
+    lda_cgs_kernel<16, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
                                             nk_delta, K, alpha, beta, seed);
   }
   return harp_launch_status();
@@ -556,32 +471,26 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
 }  // namespace
 
 // ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8)
-// variant: 0 = doc row loaded per token, 1 = next token's doc row prefetched (see PF),
-// 2..5 = variant 0 held to 1..4 more waves per SIMD (fewer VGPRs, some spilled)
+// variant: 0 = compiler occupancy, 3 = two more waves per SIMD (fewer VGPRs, some spilled)
 HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
                              void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
                              int K, float alpha, float beta, unsigned long long seed, int variant, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  if (K <= 0 || K > 1024 || ldw % 4 || variant < 0 || variant > 5) return HARP_EBADARG;
+  // variant 0: compiler occupancy; 3: two more waves per SIMD (the default). The doc-row
+  // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
+  // (profiles/r1_lda/occupancy) and are no longer built.
+  if (K <= 0 || K > 1024 || ldw % 4 || (variant != 0 && variant != 3)) return HARP_EBADARG;
 #define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks
 #define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
-    return variant == 1   ? launch_cgs<int, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
-           : variant == 2 ? launch_cgs<int, 0, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
-           : variant == 3 ? launch_cgs<int, 0, 2>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
-           : variant == 4 ? launch_cgs<int, 0, 3>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
-           : variant == 5 ? launch_cgs<int, 0, 4>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
-                          : launch_cgs<int, 0>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL);
+    return variant == 3 ? launch_cgs<int, 2>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+                        : launch_cgs<int, 0>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL);
   }
   if (ndk_bits == 16) {
     if (ldd % 8) return HARP_EBADARG;
-    return variant == 1   ? launch_cgs<unsigned short, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
-           : variant == 2 ? launch_cgs<unsigned short, 0, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
-           : variant == 3 ? launch_cgs<unsigned short, 0, 2>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
-           : variant == 4 ? launch_cgs<unsigned short, 0, 3>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
-           : variant == 5 ? launch_cgs<unsigned short, 0, 4>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
-                          : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
+    return variant == 3 ? launch_cgs<unsigned short, 2>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+                        : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
   }
 #undef CGS_ARGS
 #undef CGS_TAIL

@@ -78,18 +78,6 @@ __device__ __forceinline__ void load_row_l2(const float* __restrict__ p, float (
 }
 
 template <int EPL>
-__device__ __forceinline__ void store_row_nt(float* __restrict__ p, const float (&x)[EPL]) {
-  if constexpr (EPL % 4 == 0) {
-#pragma unroll
-    for (int k = 0; k < EPL; k += 4)
-      __builtin_nontemporal_store(floatx4{x[k], x[k + 1], x[k + 2], x[k + 3]}, (floatx4*)(p + 16 * k));
-  } else {
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) __builtin_nontemporal_store(x[k], p + 16 * k);
-  }
-}
-
-template <int EPL>
 __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&x)[EPL]) {
   if constexpr (EPL % 4 == 0) {
 #pragma unroll
@@ -268,7 +256,7 @@ constexpr int XCDS = 8;
 // store waits changed nothing, while ablating the H stores (+66 %) or the H loads (+32 %)
 // and uniform instead of skewed item popularity (+30 %) did: the kernel is bound by L2
 // traffic on hot H rows.
-template <int R, bool NTS = false>
+template <int R>
 __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, const float* sV, int n, int sl,
                                                float* __restrict__ W, unsigned ldw, float* __restrict__ H,
                                                unsigned ldh, float lr, float lam) {
@@ -322,8 +310,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     const unsigned row2 = (unsigned)sR[i2], col2 = (unsigned)sC[i2];
     const float v2 = sV[i2];
     load_row_l2<EPL>(H + (col2 * ldh + lo), hl);
-    if constexpr (NTS) store_row_nt<EPL>(H + (col0 * ldh + lo), h);
-    else store_row<EPL>(H + (col0 * ldh + lo), h);
+    store_row<EPL>(H + (col0 * ldh + lo), h);
     if (last) return false;
     // row of rating i+1: just updated (same item as i), updated one rating ago (same item as
     // i-1, its store was issued after the prefetch), or the prefetched copy
@@ -355,8 +342,8 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
 // 16-lane subgroup runs one stream. `win` (optional, 2 x 64 int64): cell c trains only the
 // window of win[64 + c] ratings starting at win[c], wrapping around the cell — the
 // fixed-fraction mode standing in for the reference's timer-bounded rotation steps.
-template <int R, int CH, bool NTS = false, int MINW = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
+template <int R, int CH>
+__global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
                                                          const long* __restrict__ win, int step,
                                                          float* __restrict__ W, int ldw, float* __restrict__ H, int ldh,
@@ -389,7 +376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
     __syncthreads();
     const long mine = n - (r0 + (long)sub * CH);
     if (mine > 0)
-      sgd_stream_lds<R, NTS>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
+      sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
                              (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
 }
@@ -432,11 +419,11 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
-template <int R, int CH, bool NTS = false, int MINW = 1>
+template <int R, int CH>
 int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win, int steps,
                    int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
-    mf_sgd_xcd_kernel<R, CH, NTS, MINW><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+    mf_sgd_xcd_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
         rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
@@ -691,14 +678,14 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 
 // All `steps` (= 8) sub-steps of the XCD-blocked schedule over one resident slice: `off`
 // is a DEVICE array of 65 int64 cell offsets into rows/cols/vals (every cell < 2^31 ratings).
-// `chunk` (ratings per stream and round) is 32, 64 or 128; `variant` 1 = non-temporal H
-// stores (chunk 64 only; measured 23 % slower, kept for the record); 2 / 3 / 4 = at least
-// 6 / 7 / 8 waves per SIMD (chunk 64; VGPRs trimmed, possibly spilled).
+// `chunk` (ratings per stream and round) is 8, 16, 32, 64 or 128 (32..128 for wide ranks);
+// `variant` must be 0 (non-temporal H stores, 23 % slower, and forced 6 / 7 / 8 waves per
+// SIMD were measured in round 1 and are no longer built).
 // `win`: optional DEVICE array [2 x 64] of per-cell window starts and lengths (NULL = all).
 HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
                                 int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
                                 float* H, int ldh, float lr, float lam, hipStream_t s) {
-  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant < 0 || variant > 4)
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant != 0)
     return HARP_EBADARG;
   if (wide_ok(r)) {  // wide ranks: one wave per stream, variants do not apply
     if (chunk != 32 && chunk != 64 && chunk != 128) return HARP_EBADARG;
@@ -708,18 +695,13 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
 #undef SGDXW_CALL
   }
 #define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
-#define SGDX_CALL(RR)                                                                          \
-  (variant == 1 ? (chunk == 64 ? launch_sgd_xcd<RR, 64, true>(SGDX_ARGS) : HARP_EBADARG)            \
-   : variant >= 2 ? (chunk != 64 ? HARP_EBADARG                                                      \
-                     : variant == 2 ? launch_sgd_xcd<RR, 64, false, 6>(SGDX_ARGS)                    \
-                     : variant == 3 ? launch_sgd_xcd<RR, 64, false, 7>(SGDX_ARGS)                    \
-                                    : launch_sgd_xcd<RR, 64, false, 8>(SGDX_ARGS))                   \
-                : chunk == 8 ? launch_sgd_xcd<RR, 8>(SGDX_ARGS)                                     \
-                : chunk == 16 ? launch_sgd_xcd<RR, 16>(SGDX_ARGS)                                   \
-                : chunk == 32 ? launch_sgd_xcd<RR, 32>(SGDX_ARGS)                                   \
-                              : chunk == 64 ? launch_sgd_xcd<RR, 64>(SGDX_ARGS)                     \
-                                            : chunk == 128 ? launch_sgd_xcd<RR, 128>(SGDX_ARGS)     \
-                                                           : HARP_EBADARG)
+#define SGDX_CALL(RR)                                                             \
+  (chunk == 8 ? launch_sgd_xcd<RR, 8>(SGDX_ARGS)                                    \
+   : chunk == 16 ? launch_sgd_xcd<RR, 16>(SGDX_ARGS)                                \
+   : chunk == 32 ? launch_sgd_xcd<RR, 32>(SGDX_ARGS)                                \
+   : chunk == 64 ? launch_sgd_xcd<RR, 64>(SGDX_ARGS)                                \
+   : chunk == 128 ? launch_sgd_xcd<RR, 128>(SGDX_ARGS)                              \
+                  : HARP_EBADARG)
   MF_DISPATCH(r, SGDX_CALL)
 #undef SGDX_CALL
 #undef SGDX_ARGS

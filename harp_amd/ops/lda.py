@@ -23,9 +23,10 @@ _lib.register({
 
 
 # csrc/lda.hip harp_lda_cgs variants: 0 = compiler occupancy (4 waves/SIMD at K=1000),
-# 1 = next token's doc row prefetched, 2..5 = variant 0 forced to 1..4 more waves per SIMD.
-# Default 3 (6 waves, a few VGPRs spilled): 1.47e9 vs 1.17e9 tokens/s at 1M x 1M x 1000
-# (profiles/r1_lda/occupancy) — more resident waves hide the random doc-row fetch best.
+# 3 = two more waves per SIMD. Default 3 (6 waves, a few VGPRs spilled): 1.47e9 vs 1.17e9
+# tokens/s at 1M x 1M x 1000 (profiles/r1_lda/occupancy) — more resident waves hide the
+# random doc-row fetch best. (The doc-row prefetch and the other occupancies measured
+# there were slower and are no longer built.)
 SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "3"))
 
 

@@ -134,7 +134,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
     ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path).
     ``chunk``: ratings per stream (8, 16, 32, 64 or 128 on the GPU; <= 0 = :func:`auto_chunk`);
-    ``variant``: 0, or 1 = non-temporal H stores (slower; see csrc/mf_sgd.hip).
+    ``variant``: must be 0 (the measured alternatives are no longer built; csrc/mf_sgd.hip).
     ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
     ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
     CPU only: ``threads > 1`` or a ``time_budget`` (s) run the cells through the 2-D
@@ -156,8 +156,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
             win = torch.tensor(list(window[0]) + list(window[1]), dtype=torch.int64).pin_memory()
             win = win.to(W.device, non_blocking=True)
         if chunk <= 0:  # wide ranks (one wave per stream) take 32 / 64 / 128 only
-            chunk = (auto_chunk(trained, blocks_per_xcd) if r <= 256 else max(32, auto_chunk(trained, blocks_per_xcd))) \
-                if variant == 0 else 64
+            chunk = auto_chunk(trained, blocks_per_xcd) if r <= 256 else max(32, auto_chunk(trained, blocks_per_xcd))
         lib = _lib.kernels()
         st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
                                  _lib.ptr(win), r, nb, chunk,

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--layout", choices=("xcd", "flat"), default="xcd")
     ap.add_argument("--skew", type=float, default=2.0, help="item popularity skew (1 = uniform)")
     ap.add_argument("--blocks-per-xcd", type=int, default=128)
-    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant (only 0 is built)")
     a = ap.parse_args()
     import torch
 
