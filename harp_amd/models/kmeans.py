@@ -227,8 +227,13 @@ class KMeansCollectiveMapper(CollectiveMapper):
                 self.comm.all_reduce(ot)
             self.objective.append(float(ot.item()))
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
-        self.metrics.end_iteration("kmeans", it, strategy=cfg.strategy,
+        self.metrics.end_iteration("kmeans", it, strategy=cfg.strategy, flops=self._iter_flops(),
                                    objective=self.objective[-1] if obj is not None else None)
+
+    def _iter_flops(self) -> float:
+        """Useful distance FLOPs of one iteration on this rank: 2 n K d (the GEMM's
+        padding columns and rows excluded)."""
+        return 2.0 * self.X.shape[0] * self.cfg.num_centroids * self.cfg.dim if getattr(self, "X", None) is not None else 0.0
 
     def _sum_table(self, sums: torch.Tensor) -> PackedTable:
         """The partial-sum table of the allreduce strategy, built once over the persistent
@@ -262,7 +267,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
         with timer.phase("prepare"):
             self._graphs[1].replay()
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
-        self.metrics.end_iteration("kmeans", it, strategy="allreduce", hip_graph=True)
+        self.metrics.end_iteration("kmeans", it, strategy="allreduce", hip_graph=True, flops=self._iter_flops())
 
     def _capture_graphs(self) -> None:
         cfg = self.cfg
@@ -438,7 +443,7 @@ class KMeansCollectiveMapper(CollectiveMapper):
                 self.comm.all_reduce(ot)
             self.objective.append(float(ot.item()))
         self.history.append({"iter": it, "s": time.perf_counter() - t_it})
-        self.metrics.end_iteration("kmeans", it, strategy="rotation",
+        self.metrics.end_iteration("kmeans", it, strategy="rotation", flops=self._iter_flops(),
                                    objective=self.objective[-1] if want_obj else None)
 
     def _rotation_gather(self) -> torch.Tensor:

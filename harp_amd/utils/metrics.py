@@ -90,6 +90,10 @@ class PhaseTimer:
         self.counts.clear()
 
 
+# dense bf16 MFMA peak of one MI355X at the 2.4 GHz boost clock (no sparsity); sustained
+# clocks under MFMA load are lower (1.8-2.0 GHz measured), so ~0.8 is the practical ceiling
+MFMA_BF16_PEAK_TFLOPS = 2500.0
+
 # xGMI link model used to report achieved-vs-ideal collective bandwidth:
 XGMI_LINK_GBPS = 153.0
 XGMI_LINKS = 7
@@ -249,9 +253,12 @@ class Metrics:
         self.resolve()
         self._iter_mark = (dict(self.timer.totals), len(self.collectives))
 
-    def end_iteration(self, app: str, it: int, **extra) -> Optional[dict]:
+    def end_iteration(self, app: str, it: int, flops: float = 0.0, peak_tflops: float = MFMA_BF16_PEAK_TFLOPS,
+                      **extra) -> Optional[dict]:
         """Emit one JSONL record for the iteration since :meth:`begin_iteration` (no-op
-        unless a metrics path is set: resolving the events costs a device sync)."""
+        unless a metrics path is set: resolving the events costs a device sync).
+        ``flops``: the iteration's useful matrix FLOPs on this rank; the record then carries
+        the achieved TFLOP/s over the ``compute`` phase and its fraction of ``peak_tflops``."""
         if not self.path or self._iter_mark is None:
             return None
         totals0, c0 = self._iter_mark
@@ -267,6 +274,11 @@ class Metrics:
                "collective_ms": round(coll_ms, 4), "collective_bytes": nbytes,
                "collective_gbps": round(nbytes / (coll_ms / 1e3) / 1e9, 3) if coll_ms > 0 else None,
                "collectives": colls, **self.memory(), **extra}
+        comp_ms = phases.get("compute", 0.0)
+        if flops > 0 and comp_ms > 0:
+            tf = flops / (comp_ms / 1e3) / 1e12
+            rec["compute_tflops"] = float(f"{tf:.6g}")
+            rec["mfma_peak_frac"] = float(f"{tf / peak_tflops:.6g}") if peak_tflops > 0 else None
         return self.emit(rec)
 
     def summary(self) -> dict:

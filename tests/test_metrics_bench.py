@@ -48,6 +48,7 @@ def test_kmeans_jsonl_records(tmp_path, strategy):
             assert x["app"] == "kmeans" and x["world"] == 2 and x["rank"] == r
             assert x["collective_bytes"] > 0, x
             assert x["phases_ms"]["compute"] > 0
+            assert x["compute_tflops"] > 0 and 0 < x["mfma_peak_frac"] < 1  # 2 n K d over the compute phase
             assert all(c["bytes"] >= 0 and c["ms"] >= 0 for c in x["collectives"])
             if strategy != "rotation":
                 assert any("eff_vs_xgmi_model" in c for c in x["collectives"]), x
