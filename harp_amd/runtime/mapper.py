@@ -84,6 +84,8 @@ class CollectiveMapper:
         self.comm = comm or Communicator()
         self.metrics = metrics or Metrics(rank=self.comm.rank, world=self.comm.world_size)
         self.metrics.world = self.comm.world_size
+        if self.comm.device.type != "cuda":
+            self.metrics.timer.use_events = False  # a CPU worker on a GPU host: wall-clock phases
         self.events = EventChannel(self.comm.rank, self.comm.world_size)
         self.result: Any = None
 
