@@ -92,20 +92,39 @@ __global__ __launch_bounds__(1024) void segscan_kernel(const int* __restrict__ c
   if (threadIdx.x == 1023) start[K] = part[1023];
 }
 
+// XCD-contiguous chunk order: workgroup b runs on XCD b % 8, and the chunks of one XCD are a
+// contiguous range, so the per-bucket runs that consecutive chunks write into perm meet in
+// the SAME L2 and leave it as whole lines (round-robin chunks split every bucket's
+// ~6-entry run boundary across two XCDs' L2s, i.e. partial-line writes to HBM).
+__device__ __forceinline__ int xcd_contiguous(unsigned b, unsigned nb) {
+  const unsigned q = nb / 8, r = nb % 8, x = b % 8;
+  return (int)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8);
+}
+
 __global__ __launch_bounds__(256) void bucket_kernel(const int* __restrict__ lab, long n, int K, long chunk,
                                                      const int* __restrict__ H, const int* __restrict__ T,
                                                      const int* __restrict__ start, int* __restrict__ perm) {
   extern __shared__ __attribute__((aligned(16))) int cur[];
-  const int c = blockIdx.x, s = c / SEG;
+  const int c = xcd_contiguous(blockIdx.x, gridDim.x), s = c / SEG;
   for (int k = threadIdx.x; k < K; k += blockDim.x)
     cur[k] = start[k] + T[(long)s * K + k] + H[(long)c * K + k];
   __syncthreads();
   const long a = (long)c * chunk;
   long b = a + chunk;
   if (b > n) b = n;
-  for (long i = a + threadIdx.x; i < b; i += blockDim.x) {
-    const int pos = atomicAdd(&cur[lab[i]], 1);
-    perm[pos] = (int)i;
+  // 8 labels per thread in flight: their loads are independent, so the loop is not one
+  // dependent global-load -> LDS-atomic -> store chain per label
+  constexpr int U = 8;
+  for (long i0 = a + threadIdx.x; i0 < b; i0 += (long)U * blockDim.x) {
+    int l[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + (long)u * blockDim.x;
+      l[u] = i < b ? lab[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (l[u] >= 0) perm[atomicAdd(&cur[l[u]], 1)] = (int)(i0 + (long)u * blockDim.x);
   }
 }
 
