@@ -289,15 +289,21 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     const long* __restrict__ tpos, const long* __restrict__ doc_off, unsigned short* __restrict__ zdoc,
     DT* __restrict__ ndk, int ldd,
     int* __restrict__ nwk, int ldw, const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, int Kp,
-    float alpha, float beta, unsigned long long seed) {
+    float alpha, float beta, unsigned long long seed, int ldelta) {
   extern __shared__ float smem[];
   float* s_qw = smem;
+  // ldelta: this workgroup's topic-sum deltas accumulate in LDS (after s_qw) and are
+  // flushed once when it exits, instead of two global atomics per moved token on only K
+  // addresses shared by every workgroup of the GPU
+  int* s_nkd = ldelta ? (int*)(smem + Kp) : nullptr;
   __shared__ float s_bs[256];  // per-64-topic block sums of qw (Kp <= 16384)
   __shared__ float s_q;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int nb = Kp >> 6;
   __shared__ int s_c;
+  if (ldelta)
+    for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) s_nkd[t] = 0;
   for (;;) {
     __syncthreads();  // the previous chunk's samplers are done with the LDS rows (and s_c)
     if (threadIdx.x == 0) s_c = atomicAdd(work, 1);
@@ -426,8 +432,13 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           atomicAdd(&s_q, inv_nz - inv_z);
           atomicSub(wrow + z, 1);
           atomicAdd(wrow + nz, 1);
-          atomicSub(nk_delta + z, 1);
-          atomicAdd(nk_delta + nz, 1);
+          if (ldelta) {
+            atomicSub(&s_nkd[z], 1);
+            atomicAdd(&s_nkd[nz], 1);
+          } else {  // K > 4096: the moves spread over enough topics (per-XCD copies measured no gain)
+            atomicSub(nk_delta + z, 1);
+            atomicAdd(nk_delta + nz, 1);
+          }
         }
       }
       // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
@@ -440,6 +451,10 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       hi = hin;
       inv_z = invn;
     }
+  }
+  if (ldelta) {  // every wave left the chunk loop together (the break follows a barrier)
+    for (int t = threadIdx.x; t < K; t += 64 * WAVES)
+      if (s_nkd[t]) atomicAdd(nk_delta + t, s_nkd[t]);
   }
 }
 
@@ -504,7 +519,8 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
                   const long* doc_off, unsigned short* zdoc, DT* ndk, int ldd, int* nwk, int ldw, const float* inv_nk,
                   int* nk_delta, int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
   const int Kp = (K + 63) / 64 * 64;
-  const size_t lds = 4 * (size_t)Kp;
+  const int ldelta = Kp <= 4096;  // LDS topic-sum deltas while they cost at most 16 KB
+  const size_t lds = (ldelta ? 8 : 4) * (size_t)Kp;
   static size_t lds_set = 0;  // raise the dynamic-LDS cap past 64 KB once per instantiation
   if (lds > 65536 && lds > lds_set) {
     if (hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
@@ -520,7 +536,7 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
   if (blocks > 256 * per_cu) blocks = 256 * per_cu;
   lda_cgs_sparse_kernel<WAVES, DT><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
       tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
-      beta, seed);
+      beta, seed, ldelta);
   return harp_launch_status();
 }
 }  // namespace

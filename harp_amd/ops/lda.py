@@ -171,8 +171,8 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
     if _lib.use_native(tz):
         inv = torch.zeros(Kp, dtype=torch.float32, device=dev)
         inv[:K] = 1.0 / (nk[:K].float() + vbeta)
-        delta = torch.zeros(Kp, dtype=torch.int32, device=dev)
         if doc_index is not None:
+            delta = torch.zeros(Kp, dtype=torch.int32, device=dev)
             assert tpos.dtype == torch.int64 and tpos.numel() == tz.numel() and tpos.is_contiguous()
             if order is None:
                 order = chunk_order(chunks)
@@ -186,6 +186,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
                 _lib.stream_ptr(dev))
             _lib.check(st, "lda_cgs_sparse")
             return delta
+        delta = torch.zeros(Kp, dtype=torch.int32, device=dev)
         st = _lib.kernels().harp_lda_cgs(tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(),
                                          chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
