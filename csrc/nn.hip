@@ -74,8 +74,10 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     // an out-of-range label contributes no target (and is never used as an index)
     if (lane == 0 && y >= 0 && y < C) lrow = -(zr[y] - m - __logf(s));
   }
-  if (lane == 0 && row < B) atomicAdd(loss, lrow);
+  __shared__ float wl[4];
+  if (lane == 0) wl[w] = row < B ? lrow : 0.f;
   __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, wl[0] + wl[1] + wl[2] + wl[3]);  // one per workgroup
   if (dbias)
     for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(&dbias[c], colsum[c]);
 }
