@@ -75,7 +75,7 @@ __device__ __forceinline__ void stage_dma(const __bf16* __restrict__ cm2, int ti
 
 template <int KS, int G, int WAVES, int RG, int PIPE>
 __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
-    const __bf16* __restrict__ X, const __bf16* __restrict__ Cm2, long N, int ntiles, int dcount,
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int ntiles, int dcount,
     int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial,
     float* __restrict__ mind) {
   using C = KMCfg<KS, G, WAVES, RG>;
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
   for (int g = 0; g < G; ++g) {
     long p = pbase + g * 32 + r;
     if (p > N - 1) p = N - 1;
-    const bf16x8* row = (const bf16x8*)(X + p * C::DP);
+    const bf16x8* row = (const bf16x8*)(X + p * ldx);
 #pragma unroll
     for (int s = 0; s < KS; ++s) xf[g][s] = row[2 * s + h];
   }
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
         const long p = pbase + g * 32 + i;
         if (p >= N) break;
         const int l = __shfl(lab[g], i, 64);
-        const __bf16* xr = X + p * C::DP;
+        const __bf16* xr = X + p * ldx;
         float* sr = sums + (long)l * ld_sums;
         for (int c = lane; c <= dcount; c += 64) atomicAdd(sr + c, (float)xr[c]);
       }
@@ -318,13 +318,13 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
 }
 
 template <int KS, int G, int WAVES, int RG, int PIPE = 0>
-int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* labels, float* sums, int ld_sums,
-                  float* obj_partial, float* mind, hipStream_t stream) {
+int launch_assign(const void* X, long ldx, const void* Cm2, long N, int Kp, int d, int* labels, float* sums,
+                  int ld_sums, float* obj_partial, float* mind, hipStream_t stream) {
   using C = KMCfg<KS, G, WAVES, RG>;
   if (Kp % C::TILE) return HARP_EBADARG;
   const long nblk = (N + C::PTS - 1) / C::PTS;
   kmeans_assign_kernel<KS, G, WAVES, RG, PIPE><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
-      (const __bf16*)X, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial, mind);
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial, mind);
   return harp_launch_status();
 }
 
@@ -333,9 +333,9 @@ int launch_assign(const void* X, const void* Cm2, long N, int Kp, int d, int* la
 // d <= 124, 13 its RG=2 neighbour, 4 the one-group shape wide rows (9..16 k-steps) use.
 #define KM_VARIANTS(KS)                                                                       \
   switch (variant) {                                                                        \
-    case 4: return launch_assign<KS, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 13: return launch_assign<KS, 4, 8, 2, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
-    case 14: return launch_assign<KS, 4, 8, 4, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 4: return launch_assign<KS, 1, 16, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
+    case 13: return launch_assign<KS, 4, 8, 2, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 14: return launch_assign<KS, 4, 8, 4, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     default: return HARP_EBADARG;                                                           \
   }
 
@@ -349,9 +349,12 @@ HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
   }
 }
 
-HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, long N, int dp, int Kp, int d, int* labels,
-                                   float* sums, int ld, float* op, float* md, int variant, hipStream_t s) {
-  if (N <= 0 || d + KM_ONES > dp || dp % 16 || Kp <= 0 || Kp % 128) return HARP_EBADARG;
+// X rows of dp (MFMA k) elements at a row stride of ldx >= dp elements (ldx % 8 == 0: 16-B
+// aligned rows; a 256-B multiple makes every row whole 128-B lines for the gather-sum).
+HARP_EXPORT int harp_kmeans_assign(const void* X, long ldx, const void* Cm2, long N, int dp, int Kp, int d,
+                                   int* labels, float* sums, int ld, float* op, float* md, int variant,
+                                   hipStream_t s) {
+  if (N <= 0 || d + KM_ONES > dp || dp % 16 || Kp <= 0 || Kp % 128 || ldx < dp || ldx % 8) return HARP_EBADARG;
   switch (dp / 16) {
     case 1: KM_VARIANTS(1)
     case 2: KM_VARIANTS(2)
@@ -362,7 +365,7 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, const void* Cm2, long N, int d
     case 7: KM_VARIANTS(7)
     case 8: KM_VARIANTS(8)
     // wide rows: one 32-point group per wave keeps the X fragments within budget
-#define KM_WIDE(KSV) case KSV: return launch_assign<KSV, 1, 16, 2>(X, Cm2, N, Kp, d, labels, sums, ld, op, md, s);
+#define KM_WIDE(KSV) case KSV: return launch_assign<KSV, 1, 16, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s);
     KM_WIDE(9) KM_WIDE(10) KM_WIDE(11) KM_WIDE(12) KM_WIDE(13) KM_WIDE(14) KM_WIDE(15) KM_WIDE(16)
 #undef KM_WIDE
     default: return HARP_EUNSUPPORTED;

@@ -133,7 +133,8 @@ __global__ __launch_bounds__(256) void bucket_kernel(const int* __restrict__ lab
 // running row sum in registers, and flushes it with one contiguous fp32 atomic row segment
 // whenever it crosses a bucket boundary (~1 flush per slot for buckets >> RUN).
 template <int LPR, int RUN>
-__global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restrict__ X, int dp, const int* __restrict__ perm,
+__global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restrict__ X, int dp, long ldx,
+                                                          const int* __restrict__ perm,
                                                           const int* __restrict__ start, int K, long n,
                                                           float* __restrict__ sums, int ld) {
   constexpr int SPW = 64 / LPR;  // slots per wave
@@ -176,17 +177,17 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restri
     for (; j + 4 <= stop; j += 4) {
       bf16x8 v0{}, v1{}, v2{}, v3{};
       if (active) {
-        v0 = *(const bf16x8*)(X + (long)perm[j] * dp + sl * 8);
-        v1 = *(const bf16x8*)(X + (long)perm[j + 1] * dp + sl * 8);
-        v2 = *(const bf16x8*)(X + (long)perm[j + 2] * dp + sl * 8);
-        v3 = *(const bf16x8*)(X + (long)perm[j + 3] * dp + sl * 8);
+        v0 = *(const bf16x8*)(X + (long)perm[j] * ldx + sl * 8);
+        v1 = *(const bf16x8*)(X + (long)perm[j + 1] * ldx + sl * 8);
+        v2 = *(const bf16x8*)(X + (long)perm[j + 2] * ldx + sl * 8);
+        v3 = *(const bf16x8*)(X + (long)perm[j + 3] * ldx + sl * 8);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += ((float)v0[e] + (float)v1[e]) + ((float)v2[e] + (float)v3[e]);
     }
     for (; j < stop; ++j) {
       if (active) {
-        const bf16x8 v = *(const bf16x8*)(X + (long)perm[j] * dp + sl * 8);
+        const bf16x8 v = *(const bf16x8*)(X + (long)perm[j] * ldx + sl * 8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
       }
@@ -241,15 +242,16 @@ HARP_EXPORT int harp_bucket_labels(const int* lab, long n, int K, int* ws, long*
 
 // sums[k][0..dp) += sum of bf16 rows X[perm[j]] for j in [start[k], start[k+1]) (sums must be
 // zeroed by the caller: partial rows are added with fp32 atomics at bucket boundaries)
-HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, const int* perm, const int* start, int K, long n,
-                                        float* sums, int ld, hipStream_t s) {
-  if (dp % 8 || dp > 256 || ld < dp || n <= 0) return n == 0 ? HARP_OK : HARP_EBADARG;
+// X rows of dp elements at a row stride of ldx >= dp (ldx % 8 == 0).
+HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, long ldx, const int* perm, const int* start, int K,
+                                        long n, float* sums, int ld, hipStream_t s) {
+  if (dp % 8 || dp > 256 || ld < dp || ldx < dp || ldx % 8 || n <= 0) return n == 0 ? HARP_OK : HARP_EBADARG;
   const int lpr_min = dp / 8;
   const __bf16* Xb = (const __bf16*)X;
   constexpr int RUN = 256;
   auto grid = [&](int lpr) { return dim3((unsigned)(((n + RUN - 1) / RUN * lpr + 255) / 256)); };
-  if (lpr_min <= 8) rowsum_bf16_kernel<8, RUN><<<grid(8), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
-  else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN><<<grid(16), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
-  else rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, perm, start, K, n, sums, ld);
+  if (lpr_min <= 8) rowsum_bf16_kernel<8, RUN><<<grid(8), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
+  else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN><<<grid(16), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
+  else rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
   return harp_launch_status();
 }

@@ -25,8 +25,8 @@ c_int, c_long, c_float, c_void_p, c_ulonglong, c_double = (
 # name -> argtypes (restype is always c_int status)
 _SIGNATURES = {
     "harp_kmeans_points_per_block": [c_int],
-    "harp_kmeans_assign": [c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                           c_void_p, c_int, c_void_p],
+    "harp_kmeans_assign": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                           c_void_p, c_void_p, c_int, c_void_p],
     "harp_kmeans_normalize": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "harp_kmeans_prepare": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "harp_uniform_rows_bf16": [c_void_p, c_long, c_int, c_int, c_float, c_float, c_ulonglong, c_long, c_int,

@@ -39,16 +39,25 @@ def padded_k(k: int) -> int:
     return (k + KP_ALIGN - 1) // KP_ALIGN * KP_ALIGN
 
 
+def row_stride(dp: int) -> int:
+    """GPU row stride of the point matrix: dp rounded up to 128 bf16 = 256 B, so every row
+    is whole 128-B lines. The MFMA k-range stays dp (the padding is never read by the
+    assign); the bucketed gather-sum then fetches 2 lines per row instead of ~2.5."""
+    return (dp + 127) // 128 * 128
+
+
 def pack_points(x: torch.Tensor, device: torch.device | str | None = None) -> torch.Tensor:
-    """[n, d] -> padded [n, dp] (bf16 on GPU, fp32 on CPU) with the count column."""
+    """[n, d] -> padded [n, dp] (bf16 on GPU, fp32 on CPU) with the count column. On the
+    GPU the result is a [n, dp] view of rows laid out at :func:`row_stride`."""
     device = torch.device(device) if device is not None else x.device
     n, d = x.shape
     dp = padded_dim(d)
     dt = torch.bfloat16 if device.type == "cuda" else torch.float32
-    out = torch.zeros((n, dp), dtype=dt, device=device)
+    ld = row_stride(dp) if device.type == "cuda" else dp
+    out = torch.zeros((n, ld), dtype=dt, device=device)
     out[:, :d] = x.to(device=device, dtype=dt)
     out[:, d:d + ONES] = 1.0
-    return out
+    return out[:, :dp]
 
 
 def generate_points(n: int, d: int, lo: float = 0.0, hi: float = 1000.0, seed: int = 0,
@@ -58,11 +67,12 @@ def generate_points(n: int, d: int, lo: float = 0.0, hi: float = 1000.0, seed: i
     device = torch.device(device)
     dp = padded_dim(d)
     if device.type == "cuda" and _lib.use_native(torch.empty(0, device=device)):
-        X = torch.empty((n, dp), dtype=torch.bfloat16, device=device)
-        _lib.check(_lib.kernels().harp_uniform_rows_bf16(X.data_ptr(), n, d, dp, float(lo), float(hi),
+        ld = row_stride(dp)
+        Xs = torch.empty((n, ld), dtype=torch.bfloat16, device=device)
+        _lib.check(_lib.kernels().harp_uniform_rows_bf16(Xs.data_ptr(), n, d, ld, float(lo), float(hi),
                                                          seed & 0xFFFFFFFFFFFFFFFF, row0, 1,
                                                          _lib.stream_ptr(device)), "uniform_rows")
-        return X
+        return Xs[:, :dp]
     g = torch.Generator().manual_seed(seed * 1000003 + row0)
     x = torch.rand((n, d), generator=g, dtype=torch.float32) * (hi - lo) + lo
     return pack_points(x, device)
@@ -145,7 +155,7 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             assert sums.dtype == torch.float32 and sums.shape[1] >= op.d + 1 and sums.is_contiguous()
             assert sums.shape[0] >= op.Cm2.shape[0], "sums needs Kp (padded) rows"
             assert sums.device == dev
-        assert X.dtype == torch.bfloat16 and X.is_contiguous() and op.Cm2.shape[1] == dp
+        assert X.dtype == torch.bfloat16 and X.stride(1) == 1 and X.stride(0) % 8 == 0 and op.Cm2.shape[1] == dp
         fused = sums if accumulate == "atomic" else None
         bucket = sums is not None and fused is None
         chunks = pipeline_chunks(n, ppb) if bucket else 1
@@ -155,7 +165,8 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
         for r0 in range(0, n, per):
             r1 = min(n, r0 + per)
             b0 = r0 // ppb
-            st = lib.harp_kmeans_assign(X[r0].data_ptr(), op.Cm2.data_ptr(), r1 - r0, dp, op.Cm2.shape[0], op.d,
+            st = lib.harp_kmeans_assign(X[r0].data_ptr(), X.stride(0), op.Cm2.data_ptr(), r1 - r0, dp,
+                                        op.Cm2.shape[0], op.d,
                                         labels[r0].data_ptr(), _lib.ptr(fused),
                                         fused.stride(0) if fused is not None else 0,
                                         obj_partial[b0].data_ptr() if want_objective else None,

@@ -18,8 +18,8 @@ _lib.register({
     "harp_bucket_workspace_ints": [_lib.c_long, _lib.c_int],
     "harp_bucket_labels": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                            _lib.c_void_p],
-    "harp_bucket_rowsum_bf16": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long,
-                                _lib.c_void_p, _lib.c_int, _lib.c_void_p],
+    "harp_bucket_rowsum_bf16": [_lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
+                                _lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_void_p],
 })
 _WS: Dict[Tuple, torch.Tensor] = {}
 
@@ -62,8 +62,9 @@ def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out:
         idx = torch.repeat_interleave(torch.arange(K), (start[1:] - start[:-1]).long())
         out[:K, : X.shape[1]].index_add_(0, idx, X[perm.long()].float())
         return out
-    assert X.dtype == torch.bfloat16 and X.is_contiguous() and out.dtype == torch.float32 and out.is_contiguous()
-    st = _lib.kernels().harp_bucket_rowsum_bf16(X.data_ptr(), X.shape[1], perm.data_ptr(), start.data_ptr(), K,
-                                                perm.numel(), out.data_ptr(), out.stride(0), _lib.stream_ptr(X.device))
+    assert X.dtype == torch.bfloat16 and X.stride(1) == 1 and out.dtype == torch.float32 and out.is_contiguous()
+    st = _lib.kernels().harp_bucket_rowsum_bf16(X.data_ptr(), X.shape[1], X.stride(0), perm.data_ptr(),
+                                                start.data_ptr(), K, perm.numel(), out.data_ptr(), out.stride(0),
+                                                _lib.stream_ptr(X.device))
     _lib.check(st, "bucket_rowsum")
     return out
