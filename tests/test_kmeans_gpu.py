@@ -159,3 +159,23 @@ def test_chunked_side_stream_pipeline_matches_single_pass(cuda, monkeypatch, chu
     assert b[1] == pytest.approx(a[1], rel=1e-9)
     assert torch.allclose(a[3], b[3], rtol=1e-5, atol=1e-2)
     assert int(b[3][:, d].sum().item()) == n
+
+
+def test_row_stride_view_matches_contiguous(cuda):
+    """GPU points live at a 256-B row stride (ops.kmeans.row_stride) as a [n, dp] view; the
+    assign and the bucketed gather-sum read that layout exactly like a dense copy."""
+    n, d, k = 50_000, 100, 700
+    torch.manual_seed(7)
+    X = K.pack_points(torch.rand(n, d, device=cuda) * 1000, cuda)
+    assert X.shape[1] == K.padded_dim(d) and X.stride(0) == K.row_stride(X.shape[1]) == 128
+    Xd = X.contiguous()
+    assert Xd.stride(0) == X.shape[1]
+    op = K.prepare(torch.rand(k, d, device=cuda) * 1000, X.shape[1])
+    out = []
+    for A in (X, Xd):
+        sums = torch.zeros((K.padded_k(k), X.shape[1]), dtype=torch.float32, device=cuda)
+        lab, obj = K.assign(A, op, sums=sums)
+        torch.cuda.synchronize()
+        out.append((lab.clone(), obj.item(), sums))
+    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == pytest.approx(out[1][1], rel=1e-12)
+    assert torch.allclose(out[0][2], out[1][2], rtol=1e-5, atol=1e-2)
