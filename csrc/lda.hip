@@ -289,13 +289,19 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     const long* __restrict__ tpos, const long* __restrict__ doc_off, unsigned short* __restrict__ zdoc,
     DT* __restrict__ ndk, int ldd,
     int* __restrict__ nwk, int ldw, const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, int Kp,
-    float alpha, float beta, unsigned long long seed, int ldelta) {
+    float alpha, float beta, unsigned long long seed, int ldelta, int wdelta) {
   extern __shared__ float smem[];
   float* s_qw = smem;
   // ldelta: this workgroup's topic-sum deltas accumulate in LDS (after s_qw) and are
   // flushed once when it exits, instead of two global atomics per moved token on only K
   // addresses shared by every workgroup of the GPU
   int* s_nkd = ldelta ? (int*)(smem + Kp) : nullptr;
+  // wdelta: each wave gathers its word-row moves in a private LDS row (plain adds by lane 0)
+  // and adds them to the global word row every WFLUSH of its tokens and at the chunk end,
+  // so other workgroups starting a chunk of the same word see the moves at most WFLUSH
+  // tokens late (a once-per-chunk flush cost 0.36 % likelihood after 5 sweeps)
+  constexpr int WFLUSH = 16;
+  int* s_wd = wdelta ? (int*)(smem + 2 * Kp) + (long)(threadIdx.x >> 6) * Kp : nullptr;
   __shared__ float s_bs[256];  // per-64-topic block sums of qw (Kp <= 16384)
   __shared__ float s_q;
   const int lane = threadIdx.x & 63;
@@ -304,6 +310,8 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
   __shared__ int s_c;
   if (ldelta)
     for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) s_nkd[t] = 0;
+  if (wdelta)
+    for (int t = threadIdx.x & 63; t < Kp; t += 64) s_wd[t] = 0;
   for (;;) {
     __syncthreads();  // the previous chunk's samplers are done with the LDS rows (and s_c)
     if (threadIdx.x == 0) s_c = atomicAdd(work, 1);
@@ -312,6 +320,16 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     const long c = order ? order[s_c] : s_c;
     const long a = chunk_start[c], b = chunk_start[c + 1];
     int* wrow = nwk + (long)tword[a] * ldw;
+    auto flush_wd = [&]() {  // this wave's word-row moves -> global row (all 64 lanes)
+      for (int t = lane; t < K; t += 64) {
+        const int v = s_wd[t];
+        if (v) {
+          atomicAdd(wrow + t, v);
+          s_wd[t] = 0;
+        }
+      }
+    };
+    int ntok = 0;
     for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
       s_qw[t] = t < K ? ((float)__builtin_nontemporal_load(wrow + t) + beta) * inv_nk[t] : 0.f;
     }
@@ -430,8 +448,13 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           atomicAdd(&s_bs[z >> 6], -inv_z);
           atomicAdd(&s_bs[nz >> 6], inv_nz);
           atomicAdd(&s_q, inv_nz - inv_z);
-          atomicSub(wrow + z, 1);
-          atomicAdd(wrow + nz, 1);
+          if (wdelta) {
+            s_wd[z] -= 1;
+            s_wd[nz] += 1;
+          } else {
+            atomicSub(wrow + z, 1);
+            atomicAdd(wrow + nz, 1);
+          }
           if (ldelta) {
             atomicSub(&s_nkd[z], 1);
             atomicAdd(&s_nkd[nz], 1);
@@ -444,12 +467,20 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
       // one wave are separate threads to the compiler, so order them explicitly
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (wdelta && ++ntok % WFLUSH == 0) {
+        flush_wd();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
+      }
       d = dn;
       z = zn;
       p = pn;
       lo = lon;
       hi = hin;
       inv_z = invn;
+    }
+    if (wdelta) {
+      flush_wd();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
   }
   if (ldelta) {  // every wave left the chunk loop together (the break follows a barrier)
@@ -520,7 +551,8 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
                   int* nk_delta, int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
   const int Kp = (K + 63) / 64 * 64;
   const int ldelta = Kp <= 4096;  // LDS topic-sum deltas while they cost at most 16 KB
-  const size_t lds = (ldelta ? 8 : 4) * (size_t)Kp;
+  const int wdelta = Kp <= 1024;  // per-wave word-row deltas: WAVES x 4 KB at most
+  const size_t lds = (ldelta ? 8 : 4) * (size_t)Kp + (wdelta ? 4 * (size_t)Kp * WAVES : 0);
   static size_t lds_set = 0;  // raise the dynamic-LDS cap past 64 KB once per instantiation
   if (lds > 65536 && lds > lds_set) {
     if (hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
@@ -536,7 +568,7 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
   if (blocks > 256 * per_cu) blocks = 256 * per_cu;
   lda_cgs_sparse_kernel<WAVES, DT><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
       tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
-      beta, seed, ldelta);
+      beta, seed, ldelta, wdelta);
   return harp_launch_status();
 }
 }  // namespace
