@@ -301,7 +301,10 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
   // so other workgroups starting a chunk of the same word see the moves at most WFLUSH
   // tokens late (a once-per-chunk flush cost 0.36 % likelihood after 5 sweeps)
   constexpr int WFLUSH = 16;
-  int* s_wd = wdelta ? (int*)(smem + 2 * Kp) + (long)(threadIdx.x >> 6) * Kp : nullptr;
+  // wdelta == 2 (Kp > 1024, no room for per-wave rows): one workgroup row right after s_qw,
+  // LDS atomics, flushed at the chunk end
+  int* s_wd = wdelta == 1 ? (int*)(smem + 2 * Kp) + (long)(threadIdx.x >> 6) * Kp
+                          : wdelta == 2 ? (int*)(smem + (ldelta ? 2 : 1) * Kp) : nullptr;
   __shared__ float s_bs[256];  // per-64-topic block sums of qw (Kp <= 16384)
   __shared__ float s_q;
   const int lane = threadIdx.x & 63;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
   __shared__ int s_c;
   if (ldelta)
     for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) s_nkd[t] = 0;
-  if (wdelta)
+  if (wdelta == 1)
     for (int t = threadIdx.x & 63; t < Kp; t += 64) s_wd[t] = 0;
   for (;;) {
     __syncthreads();  // the previous chunk's samplers are done with the LDS rows (and s_c)
@@ -332,6 +335,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     int ntok = 0;
     for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
       s_qw[t] = t < K ? ((float)__builtin_nontemporal_load(wrow + t) + beta) * inv_nk[t] : 0.f;
+      if (wdelta == 2) s_wd[t] = 0;
     }
     __syncthreads();
     for (int k = wv; k < nb; k += WAVES) {
@@ -448,9 +452,12 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           atomicAdd(&s_bs[z >> 6], -inv_z);
           atomicAdd(&s_bs[nz >> 6], inv_nz);
           atomicAdd(&s_q, inv_nz - inv_z);
-          if (wdelta) {
+          if (wdelta == 1) {
             s_wd[z] -= 1;
             s_wd[nz] += 1;
+          } else if (wdelta == 2) {
+            atomicSub(&s_wd[z], 1);
+            atomicAdd(&s_wd[nz], 1);
           } else {
             atomicSub(wrow + z, 1);
             atomicAdd(wrow + nz, 1);
@@ -467,7 +474,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
       // one wave are separate threads to the compiler, so order them explicitly
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (wdelta && ++ntok % WFLUSH == 0) {
+      if (wdelta == 1 && ++ntok % WFLUSH == 0) {
         flush_wd();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
       }
@@ -478,9 +485,13 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       hi = hin;
       inv_z = invn;
     }
-    if (wdelta) {
+    if (wdelta == 1) {
       flush_wd();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    } else if (wdelta == 2) {
+      __syncthreads();  // every wave's moves of this chunk are in the row
+      for (int t = threadIdx.x; t < K; t += 64 * WAVES)
+        if (s_wd[t]) atomicAdd(wrow + t, s_wd[t]);
     }
   }
   if (ldelta) {  // every wave left the chunk loop together (the break follows a barrier)
@@ -544,6 +555,16 @@ HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const l
 }
 
 namespace {
+// LDS modes of the sparse sampler by padded topic count: K_pad <= 1024: workgroup topic
+// deltas + per-wave word rows; <= 4096: workgroup topic deltas + one workgroup word row
+// (chunk-end flush); larger: qw only (both deltas as global atomics -- a second 40 KB row
+// would halve the resident workgroups at K = 10,000).
+int sparse_wdelta(int Kp) { return Kp <= 1024 ? 1 : Kp <= 4096 ? 2 : 0; }
+size_t sparse_lds_bytes(int Kp, int waves) {
+  const int wd = sparse_wdelta(Kp);
+  return (Kp <= 4096 ? 8 : 4) * (size_t)Kp + (wd == 1 ? 4 * (size_t)Kp * waves : wd == 2 ? 4 * (size_t)Kp : 0);
+}
+
 template <int WAVES, class DT>
 int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, const int* order,
                   int* work, const long* tpos,
@@ -551,8 +572,8 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
                   int* nk_delta, int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
   const int Kp = (K + 63) / 64 * 64;
   const int ldelta = Kp <= 4096;  // LDS topic-sum deltas while they cost at most 16 KB
-  const int wdelta = Kp <= 1024;  // per-wave word-row deltas: WAVES x 4 KB at most
-  const size_t lds = (ldelta ? 8 : 4) * (size_t)Kp + (wdelta ? 4 * (size_t)Kp * WAVES : 0);
+  const int wdelta = sparse_wdelta(Kp);
+  const size_t lds = sparse_lds_bytes(Kp, WAVES);
   static size_t lds_set = 0;  // raise the dynamic-LDS cap past 64 KB once per instantiation
   if (lds > 65536 && lds > lds_set) {
     if (hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
@@ -584,8 +605,15 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
   if (nchunks <= 0) return HARP_OK;
   if (K <= 0 || K > 16384 || ldw < K || (ndk && ldd < K) || !tpos || !doc_off || !zdoc || !work) return HARP_EBADARG;
   if (waves == 0) {  // auto: the smallest workgroup that still puts >= 24 waves on a CU
-    const long per_cu = 163840 / (4L * ((K + 63) / 64 * 64) + 1100);  // LDS-resident workgroups
-    waves = per_cu * 4 >= 24 ? 4 : per_cu * 8 >= 24 ? 8 : 16;
+    const int Kp = (K + 63) / 64 * 64;
+    waves = 16;
+    for (int w = 4; w <= 8; w *= 2) {
+      const long per_cu = 163840 / ((long)sparse_lds_bytes(Kp, w) + 1100);  // LDS-resident workgroups
+      if (per_cu * w >= 24) {
+        waves = w;
+        break;
+      }
+    }
   }
 #define SP_ARGS tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc
 #define SP_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
