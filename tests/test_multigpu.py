@@ -204,7 +204,9 @@ def test_ccd_over_rccl_matches_one_rank(mode):
     one = launch(_ccd_rccl, 1, args=(mode,), backend="nccl", timeout=300)[0]
     res = launch(_ccd_rccl, P, args=(mode,), backend="nccl", timeout=300)
     assert all(abs(r - res[0]) < 1e-6 for r in res)  # one allreduced RMSE
-    assert res[0] == pytest.approx(one, rel=1e-3)
+    # allgather mode is P-invariant; rotation visits the dimension slices in ring order,
+    # so its trajectory differs from one rank's (gloo rehearsal: 1.1662 vs 1.1386 at P = 2)
+    assert res[0] == pytest.approx(one, rel=1e-3 if mode == "allgather" else 0.06)
 
 
 def _plans_rccl(comm):
