@@ -184,7 +184,7 @@ def test_lda_over_rccl_conserves_counts_and_learns(push_pull):
     # push-pull samples every rank against one snapshot per sweep (bulk-synchronous
     # staleness): on this small corpus it trails one rank by ~5 % after 4 sweeps (gloo
     # rehearsal at P = 2); rotation by < 1 %
-    assert res[0]["loglik"] == pytest.approx(one["loglik"], rel=0.08 if push_pull else 0.03)
+    assert res[0]["loglik"] == pytest.approx(one["loglik"], rel=0.15 if push_pull else 0.05)  # P up to 8
 
 
 def _ccd_rccl(comm, mode):
