@@ -23,7 +23,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from ..ops import lda as L
-from ..runtime.dymoro import DeviceRotator, RotationSchedule
+from ..runtime.dymoro import DeviceRotator, RotationSchedule, ring_strides
 from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
 from .common import reduce_partials
 
@@ -126,7 +126,10 @@ class LDACollectiveMapper(CollectiveMapper):
             nwk_full = red["nwk"].round().to(torch.int32)
             nk = red["nk"].round().to(torch.int32)
         self.nk = nk
-        self.schedule = RotationSchedule(P, None)
+        # slice k rotates on its own ring stride: the slices' transfers use different xGMI
+        # links (dymoro.ring_strides); every schedule places block `me` here at step 0
+        self.schedules = [RotationSchedule(P, None, stride=st) for st in ring_strides(P, S)]
+        self.schedule = self.schedules[0]
         block = self.schedule.block_at(me, 0, 0)
         slabs = [nwk_full[(block * S + k) * self.vps:(block * S + k + 1) * self.vps].clone() for k in range(S)]
         del nwk_full
@@ -140,11 +143,10 @@ class LDACollectiveMapper(CollectiveMapper):
         delta_total = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
         n = 0
         for s in range(P):
-            block = self.schedule.block_at(me, it, s)
             nk_view = self.nk + delta_total  # own updates are visible immediately
             for k in range(S):
                 slab = self.rot.get(k)
-                gs = block * S + k
+                gs = self.schedules[k].block_at(me, it, s) * S + k
                 a, b = self.offsets[gs], self.offsets[gs + 1]
                 if b > a and cfg.time_budget_ms > 0:
                     m, delta_total = self._budget_step(gs, slab, delta_total, it, s, k)
@@ -159,7 +161,7 @@ class LDACollectiveMapper(CollectiveMapper):
                     delta_total += d
                     nk_view = self.nk + delta_total
                     n += b - a
-                self.rot.start(k, self.schedule.rotation_map(it, s))
+                self.rot.start(k, self.schedules[k].rotation_map(it, s))
         # topic sums: allreduce the iteration's deltas (LDAMPCollectiveMapper.java:439-461)
         if P > 1:
             dt = reduce_partials(self.comm, {"d": delta_total}, dtype=torch.float64)["d"].round().to(torch.int32)

@@ -25,7 +25,7 @@ import torch
 
 from ..ops import mf as MF
 from ..runtime.dymoro import (DeviceRotator, RotationSchedule, StepBudget, create_rotation_order,
-                              get_rotation_sequences, tune_budget)
+                              get_rotation_sequences, ring_strides, tune_budget)
 from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
 
 
@@ -197,7 +197,11 @@ class SGDCollectiveMapper(CollectiveMapper):
         gw = torch.Generator().manual_seed(cfg.seed * 31 + 7 + me)
         self.W = (torch.rand((self.users.numel(), r), generator=gw) * 2 * scale).to(dev)
         orders = get_rotation_sequences(self, cfg.epochs + 2, cfg.seed) if cfg.random_order else None
-        self.schedule = RotationSchedule(P, orders)
+        # ring mode: slice k rotates on its own stride so the slices use different xGMI links
+        # (dymoro.ring_strides); random orders are shared by all slices, as in the reference
+        strides = ring_strides(P, S) if orders is None else [1] * S
+        self.schedules = [RotationSchedule(P, orders, stride=st) for st in strides]
+        self.schedule = self.schedules[0]
         block = self.schedule.block_at(me, 0, 0)
         slabs = []
         for k in range(S):
@@ -219,10 +223,9 @@ class SGDCollectiveMapper(CollectiveMapper):
         n = 0
         timer = self.metrics.timer
         for s in range(P):
-            block = self.schedule.block_at(me, epoch, s)
             for k in range(S):
                 slab = self.rot.get(k)
-                gs = block * S + k
+                gs = self.schedules[k].block_at(me, epoch, s) * S + k
                 with timer.phase("compute"):
                     if cfg.xcd_blocks and self.device.type == "cpu" and cfg.cpu_threads > 1:
                         # CPU worker: the reference's threaded 2-D scheduler with its timer
@@ -243,7 +246,7 @@ class SGDCollectiveMapper(CollectiveMapper):
                             raise ValueError("train_fraction < 1 needs the XCD-blocked layout")
                         n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
                 with timer.phase("rotate"):
-                    self.rot.start(k, self.schedule.rotation_map(epoch, s))
+                    self.rot.start(k, self.schedules[k].rotation_map(epoch, s))
         self.trained += n
         if cfg.time_budget_ms > 0 and cfg.tune_ratio > 0 and epoch == 0:
             total = torch.tensor([float(self.train.n)], dtype=torch.float64, device=self.device)

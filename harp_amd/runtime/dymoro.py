@@ -24,6 +24,7 @@ the generic ``rotate`` collective for non-dense models.
 """
 from __future__ import annotations
 
+import math
 import random
 import threading
 import time
@@ -73,21 +74,43 @@ def get_rotation_sequences(mapper, num_iterations: int, seed: int = 0, ctx: str 
     return t.buffer[0].cpu().tolist()
 
 
+def ring_strides(P: int, S: int) -> List[int]:
+    """Ring strides for S concurrently rotating slices on P fully connected GPUs: slice k
+    moves from worker w to w + stride_k, every stride coprime with P (so each slice still
+    visits every worker once per iteration), alternating directions (1, P-1, 3, P-3, ...).
+    On MI355X every GPU pair has its own xGMI link, so slices on different strides move
+    over different links instead of sharing the one to the next rank (two slices: twice the
+    rotation bandwidth)."""
+    if P <= 2:
+        return [1] * S
+    cand: List[int] = []
+    for a in range(1, P):
+        if math.gcd(a, P) == 1:
+            for st in (a, P - a):
+                if st not in cand:
+                    cand.append(st)
+    return [cand[k % len(cand)] for k in range(S)]
+
+
 class RotationSchedule:
     """Placement of P data blocks over P workers for every (iteration, step).
 
     ``placement(it, s)[i]`` = worker holding data block i at step s of iteration it. With
-    ``orders=None`` the schedule is the ring: block i sits on (i + s) mod P, and every
-    rotation sends to next = self+1."""
+    ``orders=None`` the schedule is a ring of the given ``stride`` (coprime with P): block i
+    sits on (i + stride*s) mod P, and every rotation sends to self + stride. Random
+    ``orders`` (the reference's RotationUtil) ignore the stride."""
 
-    def __init__(self, num_workers: int, orders: Optional[Sequence[int]] = None):
+    def __init__(self, num_workers: int, orders: Optional[Sequence[int]] = None, stride: int = 1):
         self.P = num_workers
         self.orders = list(orders) if orders is not None else None
+        self.stride = stride % max(num_workers, 1) if num_workers > 1 else 0
+        if num_workers > 1 and math.gcd(self.stride, num_workers) != 1:
+            raise ValueError(f"ring stride {stride} must be coprime with {num_workers} workers")
 
     def placement(self, it: int, s: int) -> List[int]:
         P = self.P
         if self.orders is None:
-            return [(i + s + it * P) % P for i in range(P)]
+            return [(i + self.stride * s) % P for i in range(P)]
         row = self.orders[(2 * P - 1) * it:(2 * P - 1) * (it + 1)]
         if len(row) < 2 * P - 1:
             raise IndexError("rotation order table exhausted")

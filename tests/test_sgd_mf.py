@@ -14,7 +14,7 @@ import torch
 
 from harp_amd.models.sgd_mf import SGDConfig, load_mm, run_sgd, synthetic_ratings
 from harp_amd.runtime.launcher import launch
-from harp_amd.runtime.dymoro import RotationSchedule, create_rotation_order
+from harp_amd.runtime.dymoro import RotationSchedule, create_rotation_order, ring_strides
 import random
 
 MOVIELENS = "/root/reference/datasets/tutorial/movielens/movielens-test.mm.bz2"
@@ -68,6 +68,26 @@ def test_rotation_schedule_visits_all():
         for s in range(P if it < 2 else P - 1):  # the last map of the table needs iteration 3
             m = sch.rotation_map(it, s)
             assert sorted(m) == list(range(P))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 6, 8])
+def test_ring_stride_schedules(P):
+    strides = ring_strides(P, 4)
+    if P > 2:
+        assert strides[0] == 1 and strides[1] == P - 1  # two slices: opposite link directions
+    for st in strides:
+        sch = RotationSchedule(P, None, stride=st)
+        for it in range(2):
+            assert sch.placement(it, 0) == list(range(P))  # block `me` at home at step 0
+            seen = {w: set() for w in range(P)}
+            for s in range(P):
+                for blk, w in enumerate(sch.placement(it, s)):
+                    seen[w].add(blk)
+                m = sch.rotation_map(it, s)
+                assert all(m[w] == (w + st) % P for w in range(P))
+            assert all(v == set(range(P)) for v in seen.values())
+    with pytest.raises(ValueError):
+        RotationSchedule(4, None, stride=2)
 
 
 @pytest.mark.skipif(not os.path.exists(MOVIELENS), reason="movielens fixture absent")
