@@ -80,32 +80,37 @@ LD_ALIGN = 192  # sample padding: a multiple of every SYRK stage length (64, 48)
 
 
 class FeatureMajor:
-    """Feature-major bf16 copy of a data block for the MFMA SYRK: ``XT [d_pad, ld]`` with
-    samples contiguous, a row of ones at index ``d`` (so G[:, d] = column sums and
-    G[d, d] = n), zero padding to ``d_pad = round_up(d + 1, 128)`` features and
-    ``ld = round_up(n, 192)`` samples (whole 64- and 48-sample kernel stages)."""
+    """Blocked feature-major bf16 copy of a data block for the MFMA SYRK:
+    ``XT [ld/64, d_pad, 64]`` -- per 64-sample block, every feature's 64 samples contiguous
+    (a kernel stage's operand panel is one contiguous run; csrc/syrk.hip) -- with a row of
+    ones at feature ``d`` (so G[:, d] = column sums and G[d, d] = n), zero padding to
+    ``d_pad = round_up(d + 1, 128)`` features and ``ld = round_up(n, 192)`` samples."""
 
     def __init__(self, XT: torch.Tensor, n: int, d: int):
         self.XT, self.n, self.d = XT, n, d
 
     @property
     def d_pad(self) -> int:
-        return self.XT.shape[0]
+        return self.XT.shape[1]
 
     @property
     def ld(self) -> int:
-        return self.XT.shape[1]
+        return self.XT.shape[0] * KT
 
     @staticmethod
     def dims(n: int, d: int):
         return (d + 1 + MT - 1) // MT * MT, (n + LD_ALIGN - 1) // LD_ALIGN * LD_ALIGN
+
+    def dense(self) -> torch.Tensor:
+        """[d_pad, ld] feature-major view materialised (tests / debugging)."""
+        return self.XT.permute(1, 0, 2).reshape(self.d_pad, self.ld)
 
     @classmethod
     def from_rows(cls, X: torch.Tensor) -> "FeatureMajor":
         n, d = X.shape
         d_pad, ld = cls.dims(n, d)
         Xb = X.to(torch.bfloat16).contiguous()
-        XT = torch.empty((d_pad, ld), dtype=torch.bfloat16, device=X.device)
+        XT = torch.empty((ld // KT, d_pad, KT), dtype=torch.bfloat16, device=X.device)
         st = _lib.kernels().harp_to_feature_major_bf16(Xb.data_ptr(), n, d, Xb.stride(0), XT.data_ptr(), ld, d_pad, d,
                                                        _lib.stream_ptr(X.device))
         _lib.check(st, "to_feature_major")
@@ -113,18 +118,22 @@ class FeatureMajor:
 
     @classmethod
     def uniform(cls, n: int, d: int, lo: float = 0.0, hi: float = 1.0, seed: int = 0, device="cuda") -> "FeatureMajor":
-        """Synthetic U[lo,hi) data generated directly in feature-major layout on the device."""
+        """Synthetic U[lo,hi) data generated directly in the blocked layout on the device."""
         from .kmeans import _lib as _kl  # same library
 
         d_pad, ld = cls.dims(n, d)
-        XT = torch.empty((d_pad, ld), dtype=torch.bfloat16, device=device)
-        st = _kl.kernels().harp_uniform_rows_bf16(XT.data_ptr(), d_pad, ld, ld, float(lo), float(hi),
+        nb = ld // KT
+        XT = torch.empty((nb, d_pad, KT), dtype=torch.bfloat16, device=device)
+        st = _kl.kernels().harp_uniform_rows_bf16(XT.data_ptr(), nb * d_pad, KT, KT, float(lo), float(hi),
                                                   seed & 0xFFFFFFFFFFFFFFFF, 0, 0, _lib.stream_ptr(XT.device))
         _lib.check(st, "uniform_rows")
-        XT[d:].zero_()
-        XT[d, :n] = 1.0
-        if ld > n:
-            XT[:, n:].zero_()
+        XT[:, d:].zero_()
+        full, part = divmod(n, KT)  # whole sample blocks, samples in the partial block
+        XT[:full, d] = 1.0
+        if part:
+            XT[full, d, :part] = 1.0
+            XT[full, :, part:].zero_()
+        XT[full + (1 if part else 0):].zero_()
         return cls(XT, n, d)
 
 

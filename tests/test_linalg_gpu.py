@@ -19,9 +19,20 @@ def test_gram_stats_matches_fp64(cuda, n, d):
     assert torch.allclose(G.double(), ref, rtol=2e-5, atol=1e-3 * ref.abs().max().item() * 1e-3 + 1e-2)
 
 
+def test_feature_major_blocked_layout(cuda):
+    X = torch.rand(200, 30, device=cuda)
+    D = LA.FeatureMajor.from_rows(X).dense()
+    assert D.shape == (128, 384)
+    assert torch.equal(D[:30, :200], X.to(torch.bfloat16).t())
+    assert bool((D[30, :200] == 1).all()) and int(D[31:].float().abs().sum()) == 0 and int(D[:, 200:].float().abs().sum()) == 0
+
+
 def test_feature_major_uniform_and_cov(cuda):
     fm = LA.FeatureMajor.uniform(50000, 64, 0.0, 1.0, seed=3, device=cuda)
-    assert fm.XT.shape == (128, 50112)  # samples padded to a multiple of 192
+    assert fm.XT.shape == (50112 // 64, 128, 64)  # 64-sample blocks; samples padded to a multiple of 192
+    D = fm.dense()
+    assert bool((D[64, :50000] == 1).all()) and int(D[64].float().sum()) == 50000 and int(D[65:].float().abs().sum()) == 0
+    assert int(D[:, 50000:].float().abs().sum()) == 0
     cnt, s, G = LA.gram_stats(fm)
     n = cnt.item()
     mean = s.double() / n
