@@ -6,30 +6,38 @@
 // 121-147, daal_linreg/normaleq). N = 1e8 x d = 1000 is ~1e14 MFMA FLOP per pass.
 //
 // Design (MI355X-first):
-//  * data is stored FEATURE-MAJOR in 64-sample blocks, XT[ld/64][d_pad][64]: for
+//  * data is stored FEATURE-MAJOR in 48-sample blocks, XT[ld/48][d_pad][48]: for
 //    G = XT XT^T both MFMA operands want 8 consecutive samples of one feature per lane,
-//    which is then a plain 16-B read — no transposes anywhere — and one stage's MT x 64
-//    operand panel is ONE contiguous MT*128-B run. (A flat [d_pad][ld] layout puts the
+//    which is then a plain 16-B read — no transposes anywhere — and one stage's MT x 48
+//    operand panel is ONE contiguous MT*96-B run. (A flat [d_pad][ld] layout puts the
 //    panel's rows ld*2 = 200 MB apart at N = 1e8: every stage then touches 256-512
 //    distinct pages and the loads are address-translation bound, not L2 bound.) A row of
 //    ones in XT makes G's last column the column sums and G[ones][ones] = n, so moments
 //    come out of the same pass.
-//  * only upper-triangular 128x128 output tiles are computed (diagonal tiles in full);
-//    the sample dimension is split over workgroups (split-K) for >= 1000 workgroups, each
-//    workgroup adds its fp32 tile into G with contiguous 128-B atomic row segments.
-//  * per 64-sample step both 128-feature operand panels stream through double-buffered LDS
-//    by global_load_lds (LDS-DMA); a 16-B chunk XOR swizzle c ^ ((row >> 1) & 7), applied
-//    to the DMA source and the ds_read_b128 address, keeps every read lane group
-//    conflict-free. 4 waves, each a 64x64 sub-tile = 2x2 accumulators of
-//    v_mfma_f32_32x32x16_bf16.
+//  * only upper-triangular MT x MT output tiles are computed (diagonal tiles in pairs, see
+//    syrk_kernel); the sample dimension is split over workgroups (split-K), each workgroup
+//    adds its fp32 tile into G with contiguous 128-B atomic row segments.
+//  * per 48-sample stage both operand panels stream through a 3-deep LDS ring by
+//    global_load_lds (LDS-DMA) -- 2 x 3 x 24 KB = 144 KB of the 160 KB for 256-feature
+//    panels -- so a stage's loads are issued two stages ahead, with counted vmcnt waits and
+//    raw s_barriers (a __syncthreads() would drain the ring). A 64-sample stage fits only
+//    two buffers, one stage of look-ahead, and measured 0.106 s vs the MFMA-only 0.069 s
+//    (profiles/r2_syrk2). The 96-B LDS rows (6 chunks of 16 B) are rotated by one chunk for
+//    rows 16-31 of every 32-row block: conflict-free for ds_read_b128's lane groups
+//    (exhaustive search over the 6-chunk rotations; the rotation is applied on the DMA
+//    source side, the LDS image stays lane-linear). 8 waves, each a 64x128 sub-tile =
+//    2x4 accumulators of v_mfma_f32_32x32x16_bf16.
 #include "common.h"
 
 namespace {
 
-constexpr int KT = 64;        // samples per stage
-constexpr int CPR = KT / 8;   // 16-B chunks per LDS row (8)
+constexpr int KT = 48;        // samples per stage (= the layout's sample block)
+constexpr int CPR = KT / 8;   // 16-B chunks per LDS row (6)
+constexpr int NBUF = 3;       // LDS ring depth
 
-__device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+// LDS position of logical 16-B chunk c of panel row `row`, and its inverse
+__device__ __forceinline__ int swz_pos(int row, int c) { return (c + ((row >> 4) & 1)) % CPR; }
+__device__ __forceinline__ int swz_src(int row, int cp) { return (cp + (CPR - ((row >> 4) & 1))) % CPR; }
 
 // Workgroup geometry: MT x MT output tile; each wave owns (32*BA) x (32*BB).
 template <int MT_, int BA_, int BB_>
@@ -41,16 +49,16 @@ struct SyrkCfg {
   static constexpr int DMA = PANEL_BYTES / 1024;
 };
 
-// one MT x 64 panel of XT (features r0.., sample block k0/64 of d_pad x 64) -> LDS via LDS-DMA
+// one MT x 48 panel of XT (features r0.., sample block k0/48 of d_pad x 48) -> LDS via LDS-DMA
 template <class C>
 __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long d_pad, int r0, long k0, char* lds,
                                             int wave, int lane) {
-  const __bf16* blk = XT + k0 * d_pad + (long)r0 * KT;  // k0 % 64 == 0: the block's panel is contiguous
+  const __bf16* blk = XT + k0 * d_pad + (long)r0 * KT;  // k0 % KT == 0: the block's panel is contiguous
 #pragma unroll
   for (int j = wave; j < C::DMA; j += C::WAVES) {
     const int q = j * 64 + lane;          // chunk position in the LDS image
     const int row = q / CPR, cp = q % CPR;
-    const int c = swz(row, cp);           // involution: source chunk for this position
+    const int c = swz_src(row, cp);       // source chunk for this position
     const __bf16* src = blk + row * KT + c * 8;
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                      (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
@@ -58,9 +66,9 @@ __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ XT, long 
 }
 
 // MFMA fragment of 32-row block `blk` of a staged panel: lane (r, h) reads row blk*32 + r,
-// 16-B chunk kc = 2*kstep + h. swz(blk*32 + r, kc) does not depend on blk, so `lo` =
-// r*128 + (swz(r, kc) << 4) is per lane and k-step, and the block is an immediate offset.
-__device__ __forceinline__ int frag_off(int r, int kc) { return r * (CPR * 16) + (swz(r, kc) << 4); }
+// 16-B chunk kc = 2*kstep + h. swz_pos(blk*32 + r, kc) does not depend on blk, so `lo` =
+// r*96 + (swz_pos(r, kc) << 4) is per lane and k-step, and the block is an immediate offset.
+__device__ __forceinline__ int frag_off(int r, int kc) { return r * (CPR * 16) + (swz_pos(r, kc) << 4); }
 __device__ __forceinline__ bf16x8 frag(const char* P, int blk, int lo) {
   return *(const bf16x8*)(P + blk * (32 * CPR * 16) + lo);
 }
@@ -88,10 +96,6 @@ __device__ __forceinline__ void tri_step(const char* P, int lo, floatx16* acc) {
   for (int c = W; c < NB; ++c) mma<DIAG>(f[0], f[c - W], acc[c - W]);
 #pragma unroll
   for (int c = NB - 1 - W; c < NB; ++c) mma<DIAG>(f[NB - 1 - 2 * W], f[c - W], acc[NB - W + c - (NB - 1 - W)]);
-  // keep the next k-step's fragment reads below this one's MFMAs: hoisting all of a stage's
-  // reads (4 x NB fragments) on top of NB+1 accumulators would spill; the SIMD's other
-  // wave covers the LDS latency instead
-  __builtin_amdgcn_sched_barrier(0);
 }
 
 struct SyrkJob {
@@ -120,40 +124,50 @@ __device__ __forceinline__ void syrk_body(const SyrkJob& J, char* smem, int tid)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[j][v] = 0.f;
 
-  // buffers: A[c] = smem + c*PANEL, B[c] = smem + (2+c)*PANEL
-  stage_panel<C>(J.XT, J.dpad, J.ti * MT, J.kbeg, smem, wave, lane);
-  if (!J.one) stage_panel<C>(J.XT, J.dpad, J.tj * MT, J.kbeg, smem + 2 * PANEL, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int cur = 0;
-  for (long k0 = J.kbeg; k0 < J.kend; k0 += KT) {
-    if (J.sync) {
+  // ring: stage i in A = smem + (i%3)*PANEL, B = smem + (3 + i%3)*PANEL
+  static_assert(C::DMA == 3 * C::WAVES, "3 LDS-DMA pieces per wave per panel (the vmcnt counts below)");
+  const int nst = (int)((J.kend - J.kbeg) / KT);
+  auto issue = [&](int st) {
+    const long k = DIAG == 4 ? J.kbeg : J.kbeg + (long)st * KT;  // DIAG 4: re-read the first (L2-hot)
+    const int bf = st % NBUF;
+    stage_panel<C>(J.XT, J.dpad, J.ti * MT, k, smem + bf * PANEL, wave, lane);
+    if (!J.one) stage_panel<C>(J.XT, J.dpad, J.tj * MT, k, smem + (NBUF + bf) * PANEL, wave, lane);
+  };
+  issue(0);
+  if (DIAG != 1 && nst > 1) issue(1);
+  for (int i = 0; i < nst; ++i) {
+    // this wave's DMA of stage i landed (stage i+1's, issued later, may stay in flight) ...
+    if (DIAG != 1 && i + 1 < nst) {
+      if (J.one) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // ... then every wave's, and every wave is done reading stage i-1 (whose buffer stage
+    // i+2 reuses): raw barrier, no vmcnt drain
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (J.sync && i > 0 && i % J.sync_every == 0) {
       // soft lock-step of the split's tiles (they share feature panels through this XCD's
       // L2 only while they stream the same samples): every sync_every stages, arrive on the
       // split's counter and wait -- boundedly, so progress never depends on it -- until
       // every tile of the split has arrived. Correctness does not depend on the wait.
-      const int st = (int)((k0 - J.kbeg) / KT);
-      if (st > 0 && st % J.sync_every == 0) {
-        if (tid == 0) {
-          int* c = J.sync + J.split;
-          atomicAdd(c, 1);
-          const int target = J.ntiles * (st / J.sync_every);
-          for (int it = 0; it < 2000; ++it) {
-            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-            __builtin_amdgcn_s_sleep(4);
-          }
+      if (tid == 0) {
+        int* c = J.sync + J.split;
+        atomicAdd(c, 1);
+        const int target = J.ntiles * (i / J.sync_every);
+        for (int it = 0; it < 2000; ++it) {
+          if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+          __builtin_amdgcn_s_sleep(4);
         }
-        __syncthreads();
       }
+      __syncthreads();
     }
-    const bool more = DIAG != 1 && k0 + KT < J.kend;
-    const long kn = DIAG == 4 ? J.kbeg : k0 + KT;  // DIAG 4: every stage re-reads the first (L2-hot)
-    if (more) {
-      stage_panel<C>(J.XT, J.dpad, J.ti * MT, kn, smem + (cur ^ 1) * PANEL, wave, lane);
-      if (!J.one) stage_panel<C>(J.XT, J.dpad, J.tj * MT, kn, smem + (2 + (cur ^ 1)) * PANEL, wave, lane);
-    }
-    const char* A = smem + cur * PANEL;
-    const char* B = J.one ? A : smem + (2 + cur) * PANEL;
+    if (DIAG != 1 && i + 2 < nst) issue(i + 2);
+    const int bf = i % NBUF;
+    const char* A = smem + bf * PANEL;
+    const char* B = J.one ? A : smem + (NBUF + bf) * PANEL;
     if constexpr (DIAG != 3 && MODE >= 0) {
       const char* P = J.second ? B : A;
 #pragma unroll
@@ -172,9 +186,6 @@ __device__ __forceinline__ void syrk_body(const SyrkJob& J, char* smem, int tid)
           for (int bb = 0; bb < BB; ++bb) mma<DIAG>(af[a], bfr[bb], acc[a * BB + bb]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    cur ^= 1;
   }
   // D[i][j]: lane holds col = lane&31, rows (v&3) + 8*(v>>2) + 4h of each 32x32 block
   if constexpr (MODE >= 0) {
@@ -220,7 +231,7 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
   using C = SyrkCfg<MT_, BA_, BB_>;
   constexpr int MT = C::MT, PANEL = C::PANEL_BYTES, NB = MT / 32;
   static_assert(C::WAVES == NB && (NB == 4 || NB == 8), "diagonal pairs: NB/2 waves per panel");
-  __shared__ __attribute__((aligned(16))) char smem[4 * PANEL];
+  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * PANEL];
   const int tid = threadIdx.x, wave = tid >> 6;
   // XCD-aware remap (bijective): consecutive logical ids share an XCD (blocks b, b+8, ...
   // are co-located), so the tiles of one sample split hit the same L2
@@ -262,7 +273,7 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
   }
 }
 
-// row-major X[n][d] (bf16/any) -> blocked feature-major XT[ld/64][d_pad][64] bf16 with a
+// row-major X[n][d] (bf16/any) -> blocked feature-major XT[ld/48][d_pad][48] bf16 with a
 // ones row at index d (tiled transpose through LDS).
 __global__ void to_feature_major_kernel(const __bf16* __restrict__ X, long n, int d, long ldx,
                                         __bf16* __restrict__ XT, long ld, int d_pad, int ones_row) {
@@ -304,7 +315,7 @@ static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int
     // workgroups, one per CU. (Lone diagonal tiles: 24 x 10 = 240 workgroups, 0.143 s vs
     // 0.150 s for the ~1030-workgroup split-K grid, 0.122 s with the split lock-step hint:
     // L2 hit 49 % -> 71 %, the 75 % ceiling of 4 tiles per panel; profiles/r2_syrk.)
-    const int per_xcd = 32 * (MT >= 256 ? 1 : 2);  // one 256-tile / two 128-tile WGs per CU (LDS)
+    const int per_xcd = 32 * (MT >= 256 ? 1 : 2);  // one 256-tile (144 KB) / two 128-tile (72 KB) WGs per CU
     if (ntiles <= per_xcd) {
       num_splits = 8 * (per_xcd / ntiles);
     } else {
@@ -335,13 +346,11 @@ static int launch_syrk(const void* XT, long ld, long n, int d_pad, float* G, int
   return harp_launch_status();
 }
 
-// G[d_pad][ldg] (+)= XT XT^T over the upper tiles; XT [ld/64][d_pad][64] bf16 (blocked
-// feature-major), d_pad % 128 == 0, n % 64 == 0 (zero-padded samples), ld >= n, ld % 64 == 0.
+// G[d_pad][ldg] (+)= XT XT^T over the upper tiles; XT [ld/48][d_pad][48] bf16 (blocked
+// feature-major), d_pad % 128 == 0, n % 48 == 0 (zero-padded samples), ld >= n, ld % 48 == 0.
 // 256x256 tiles (8 waves) when d_pad % 256 == 0 and d_pad >= 512 (half the operand re-reads),
 // else 128x128 (4 waves).
-// variant 0 (the only one): 64-sample stages, double buffer. A 32-sample 4-deep LDS-DMA
-// ring (raw s_barrier, no vmcnt drain) measured 0.19-0.20 s vs 0.122 s and was removed
-// (profiles/r2_syrk). sync_ws (>= 1024 ints, may be null) + sync_every (stages, 0 = off):
+// variant 0 (the only one): 48-sample stages, 3-deep LDS-DMA ring. sync_ws (>= 1024 ints, may be null) + sync_every (stages, 0 = off):
 // the split lock-step hint of the 256-tile kernel (see syrk_kernel).
 HARP_EXPORT int harp_syrk_t_bf16(const void* XT, long ld, long n, int d_pad, float* G, int ldg, int num_splits,
                                  int variant, int* sync_ws, int sync_every, hipStream_t s) {

@@ -75,13 +75,13 @@ _lib.register({
 })
 
 MT = 128  # SYRK macro tile (features)
-KT = 64   # samples per SYRK stage
-LD_ALIGN = 192  # sample padding: a multiple of every SYRK stage length (64, 48)
+KT = 48   # samples per SYRK stage (= the layout's sample block)
+LD_ALIGN = 192  # sample padding (a multiple of KT)
 
 
 class FeatureMajor:
     """Blocked feature-major bf16 copy of a data block for the MFMA SYRK:
-    ``XT [ld/64, d_pad, 64]`` -- per 64-sample block, every feature's 64 samples contiguous
+    ``XT [ld/KT, d_pad, KT]`` (KT = 48) -- per sample block, every feature's KT samples contiguous
     (a kernel stage's operand panel is one contiguous run; csrc/syrk.hip) -- with a row of
     ones at feature ``d`` (so G[:, d] = column sums and G[d, d] = n), zero padding to
     ``d_pad = round_up(d + 1, 128)`` features and ``ld = round_up(n, 192)`` samples."""
@@ -140,7 +140,7 @@ class FeatureMajor:
 SYRK_VARIANT = 0  # the one shipped kernel (profiles/r2_syrk: alternatives measured slower, removed)
 
 
-SYRK_SYNC_EVERY = int(os.environ.get("HARP_SYRK_SYNC", "32"))  # stages between split lock-step points (0: off)
+SYRK_SYNC_EVERY = int(os.environ.get("HARP_SYRK_SYNC", "64"))  # stages between split lock-step points (0: off)
 _SYNC_WS: dict = {}
 
 

@@ -29,7 +29,7 @@ def test_feature_major_blocked_layout(cuda):
 
 def test_feature_major_uniform_and_cov(cuda):
     fm = LA.FeatureMajor.uniform(50000, 64, 0.0, 1.0, seed=3, device=cuda)
-    assert fm.XT.shape == (50112 // 64, 128, 64)  # 64-sample blocks; samples padded to a multiple of 192
+    assert fm.XT.shape == (50112 // LA.KT, 128, LA.KT)  # sample blocks; samples padded to a multiple of 192
     D = fm.dense()
     assert bool((D[64, :50000] == 1).all()) and int(D[64].float().sum()) == 50000 and int(D[65:].float().abs().sum()) == 0
     assert int(D[:, 50000:].float().abs().sum()) == 0
