@@ -58,6 +58,9 @@ def parse_args(argv=None):
     ap.add_argument("--sgd-epochs", type=int, default=5)
     ap.add_argument("--sgd-warmup", type=int, default=1)
     ap.add_argument("--sgd-slices", type=int, default=2, help="H slices per rank (rotation pipeline depth)")
+    ap.add_argument("--sgd-timeout", type=float, default=240.0,
+                    help="wall-clock bound (s) on the nested MF-SGD record; past it rank 0 prints the "
+                         "K-means line with an sgd error and every rank exits")
     ap.add_argument("--metrics-jsonl", default="", help="per-iteration phase/bytes records (JSONL)")
     return ap.parse_args(argv)
 
@@ -216,6 +219,44 @@ class _Reader:
         return 0
 
 
+class _SGDGuard:
+    """Bounds the nested MF-SGD record. If it has not finished after ``timeout_s``, rank 0
+    prints the (already measured) K-means record with ``sgd.error`` and every rank leaves
+    with ``os._exit(0)`` — the process teardown releases any RCCL kernel still waiting on a
+    peer. ``cancel()`` returns False when the guard has already fired."""
+
+    def __init__(self, timeout_s: float, rec: dict, rank: int):
+        import threading
+
+        self._lock = threading.Lock()
+        self._state = "armed"
+        self.rec, self.rank = rec, rank
+        self._t = threading.Timer(timeout_s, self._fire, args=(timeout_s,))
+        self._t.daemon = True
+        if timeout_s > 0:
+            self._t.start()
+
+    def _fire(self, timeout_s: float) -> None:
+        with self._lock:
+            if self._state != "armed":
+                return
+            self._state = "fired"
+        print(f"bench: MF-SGD record exceeded {timeout_s:g} s on rank {self.rank}; leaving", file=sys.stderr,
+              flush=True)
+        if self.rank == 0:
+            rec = dict(self.rec, sgd={"error": f"timeout after {timeout_s:g} s"})
+            print(json.dumps(rec), flush=True)
+        os._exit(0)
+
+    def cancel(self) -> bool:
+        with self._lock:
+            if self._state == "fired":
+                return False
+            self._state = "done"
+        self._t.cancel()
+        return True
+
+
 def sync(comm, torch):
     if comm.device.type == "cuda":
         torch.cuda.synchronize()
@@ -266,12 +307,17 @@ def run(args) -> int:
         torch.cuda.empty_cache()
     want_sgd = args.sgd == "on" or (args.sgd == "auto" and comm.device.type == "cuda")
     if want_sgd:
-        # the nested record must never cost the headline line: a failure is reported inside it
+        # the nested record must never cost the headline line: a failure is reported inside
+        # it, and a hang (e.g. a stuck RCCL peer in the rotation ring, which no Python
+        # exception interrupts) is bounded by a per-rank wall-clock guard
+        guard = _SGDGuard(args.sgd_timeout, rec, comm.rank)
         try:
             rec["sgd"] = bench_sgd(args, comm, torch)
         except Exception as e:  # noqa: BLE001
             rec["sgd"] = {"error": f"{type(e).__name__}: {e}"[:500]}
             print(f"bench: MF-SGD record failed on rank {comm.rank}: {e!r}", file=sys.stderr)
+        if not guard.cancel():
+            time.sleep(3600)  # the guard is printing / exiting this process
     if comm.rank == 0:
         print(json.dumps(rec), flush=True)
     shutdown()
