@@ -76,7 +76,7 @@ __device__ __forceinline__ bf16x8 frag(const char* P, int blk, int lo) {
 // DIAG (timing diagnostics only, results are garbage): 1 = no global loads after the first
 // stage (MFMA + LDS + barriers), 2 = no MFMA (loads + LDS reads + a VALU use of the
 // fragments), 3 = loads + barriers only, 4 = every stage loads the first stage's (L2-hot)
-// samples (same instruction stream, no L2 misses)
+// samples (same instruction stream, no L2 misses), 5 = off-diagonal tiles only (pairs exit)
 template <int DIAG>
 __device__ __forceinline__ void mma(const bf16x8& a, const bf16x8& b, floatx16& c) {
   if constexpr (DIAG == 2) c[0] += (float)a[0] * (float)b[7];
@@ -265,6 +265,7 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
   J.sync_every = sync_every;
   J.second = wave >= NB / 2;
   if (!pair) return syrk_body<C, -1, DIAG>(J, smem, tid);
+  if constexpr (DIAG == 5) return;  // diagnostics: off-diagonal tiles only
   switch (wave % (NB / 2)) {  // wave-uniform
     case 0: return syrk_body<C, 0, DIAG>(J, smem, tid);
     case 1: return syrk_body<C, 1, DIAG>(J, smem, tid);
@@ -380,6 +381,7 @@ HARP_EXPORT int harp_syrk_diag(const void* XT, long ld, long n, int d_pad, float
     case 2: return launch_syrk<256, 2, 4, 2>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     case 3: return launch_syrk<256, 2, 4, 3>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     case 4: return launch_syrk<256, 2, 4, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 5: return launch_syrk<256, 2, 4, 5>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     default: return HARP_EBADARG;
   }
 }

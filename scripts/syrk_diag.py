@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--d", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--modes", default="0,1,2,3,4", help="DIAG modes of csrc/syrk.hip (0-5)")
     a = ap.parse_args()
     import torch
 
@@ -28,7 +29,7 @@ def main():
     G = torch.zeros((fm.d_pad, fm.d_pad), dtype=torch.float32, device="cuda")
     lib = _lib.kernels()
     out = {"n": int(a.n), "d": a.d}
-    for mode in (0, 1, 2, 3, 4):
+    for mode in [int(m) for m in a.modes.split(",")]:
         def run():
             _lib.check(lib.harp_syrk_diag(fm.XT.data_ptr(), fm.ld, fm.ld, fm.d_pad, G.data_ptr(), G.stride(0),
                                           a.splits, mode, _lib.stream_ptr(G.device)), "syrk_diag")
