@@ -75,8 +75,8 @@ __device__ __forceinline__ void stage_dma(const __bf16* __restrict__ cm2, int ti
 
 template <int KS, int G, int WAVES, int RG, int PIPE>
 __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
-    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int ntiles, int dcount,
-    int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial,
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int ntiles, int tail_rg,
+    int dcount, int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial,
     float* __restrict__ mind) {
   using C = KMCfg<KS, G, WAVES, RG>;
   __shared__ __attribute__((aligned(16))) char smem[2 * C::TILE_BYTES + WAVES * 4];
@@ -116,7 +116,9 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
+  // full tiles; a last tile of only tail_rg (< RG) row groups runs after the loop
+  const int nfull = tail_rg ? ntiles - 1 : ntiles;
+  for (int t = 0; t < nfull; ++t) {
     if (t + 1 < ntiles) stage_dma<C>(Cm2, t + 1, smem + ((t + 1) & 1) * C::TILE_BYTES, wave, lane);
     const char* buf = smem + (t & 1) * C::TILE_BYTES;
     bf16x8 af[2][KS];
@@ -184,6 +186,29 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  if (tail_rg) {
+    // K not a multiple of the stage: only the live 32-row groups of the last tile (its DMA
+    // landed with the previous stage's wait + barrier; the rows past them are never read)
+    const int t = ntiles - 1;
+    const char* buf = smem + (t & 1) * C::TILE_BYTES;
+    for (int rg = 0; rg < tail_rg; ++rg) {
+      const char* nb = buf + rg * 32 * C::CPR * 16;
+      bf16x8 af[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) af[s] = *(const bf16x8*)(nb + aoff[s]);
+      const int tg = t * RG + rg;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        floatx16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], xf[g][s], acc, 0, 0, 0);
+        float m = keyed(acc[0], 0u);
+#pragma unroll
+        for (int i = 1; i < 16; ++i) m = fminf(m, keyed(acc[i], (unsigned)i));
+        if (m < best[g]) { best[g] = m; bestt[g] = tg; }
+      }
+    }
   }
 
   // ---- resolve argmin across the two lane halves, write labels / objective partials
@@ -321,14 +346,16 @@ template <int KS, int G, int WAVES, int RG, int PIPE = 0>
 int launch_assign(const void* X, long ldx, const void* Cm2, long N, int Kp, int d, int* labels, float* sums,
                   int ld_sums, float* obj_partial, float* mind, hipStream_t stream) {
   using C = KMCfg<KS, G, WAVES, RG>;
-  if (Kp % C::TILE) return HARP_EBADARG;
+  if (Kp % 32) return HARP_EBADARG;
   const long nblk = (N + C::PTS - 1) / C::PTS;
+  const int ntiles = (Kp + C::TILE - 1) / C::TILE, tail_rg = (Kp % C::TILE) / 32;
   kmeans_assign_kernel<KS, G, WAVES, RG, PIPE><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
-      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, Kp / C::TILE, d, labels, sums, ld_sums, obj_partial, mind);
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, ntiles, tail_rg, d, labels, sums, ld_sums, obj_partial, mind);
   return harp_launch_status();
 }
 
-// variant -> (G, WAVES, RG, PIPE). Kp must be a multiple of 128 for every variant.
+// variant -> (G, WAVES, RG, PIPE). Kp (the rows swept) must be a multiple of 32; Cm2 must
+// hold round_up(Kp, 128) rows (the last stage's DMA reads the whole tile).
 // Only the measured frontier ships (profiles/r1_kmeans_*): 14 is the default for
 // d <= 124, 13 its RG=2 neighbour, 4 the one-group shape wide rows (9..16 k-steps) use.
 #define KM_VARIANTS(KS)                                                                       \
@@ -354,7 +381,7 @@ HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
 HARP_EXPORT int harp_kmeans_assign(const void* X, long ldx, const void* Cm2, long N, int dp, int Kp, int d,
                                    int* labels, float* sums, int ld, float* op, float* md, int variant,
                                    hipStream_t s) {
-  if (N <= 0 || d + KM_ONES > dp || dp % 16 || Kp <= 0 || Kp % 128 || ldx < dp || ldx % 8) return HARP_EBADARG;
+  if (N <= 0 || d + KM_ONES > dp || dp % 16 || Kp <= 0 || Kp % 32 || ldx < dp || ldx % 8) return HARP_EBADARG;
   switch (dp / 16) {
     case 1: KM_VARIANTS(1)
     case 2: KM_VARIANTS(2)

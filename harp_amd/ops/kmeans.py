@@ -123,6 +123,12 @@ def prepare(c: torch.Tensor, dp: int, out: Optional[CentroidOperand] = None) -> 
     return out
 
 
+def swept_k(op: "CentroidOperand") -> int:
+    """Centroid rows the assign kernel sweeps: K rounded up to one 32-row MFMA group (the
+    kernel skips the rest of the 128-row padding; K = 1e4 sweeps 10,016 of 10,112 rows)."""
+    return min(op.Cm2.shape[0], (op.K + 31) // 32 * 32)
+
+
 def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = None,
            labels: Optional[torch.Tensor] = None, want_objective: bool = True, variant: int = DEFAULT_VARIANT,
            obj_partial: Optional[torch.Tensor] = None, accumulate: str = "bucket",
@@ -166,7 +172,7 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             r1 = min(n, r0 + per)
             b0 = r0 // ppb
             st = lib.harp_kmeans_assign(X[r0].data_ptr(), X.stride(0), op.Cm2.data_ptr(), r1 - r0, dp,
-                                        op.Cm2.shape[0], op.d,
+                                        swept_k(op), op.d,
                                         labels[r0].data_ptr(), _lib.ptr(fused),
                                         fused.stride(0) if fused is not None else 0,
                                         obj_partial[b0].data_ptr() if want_objective else None,
