@@ -41,6 +41,8 @@ class LDAConfig:
     block_words: int = 4096   # push/pull strategy: words per model partition
     sparse_comm: str = "off"  # push/pull: "on" moves nonzero counts only (profiles/r2_apps: the torch
                               # nonzero / index_add compaction costs 0.15-0.26 s per iteration)
+    rotate_codec: str = "auto"  # rotation: "on" sends word-topic slabs as sparse payloads (ops/slabcodec),
+                                # "auto" when that payload is at most half the dense slab, "off" dense
     checkpoint_dir: str = ""  # .hpt checkpoints (token topics, doc-topic, resident word slices)
     checkpoint_every: int = 0  # iterations between checkpoints (0: never)
     model_dir: str = ""       # word-model dumps every print_interval*10 iterations + at the end
@@ -132,10 +134,27 @@ class LDACollectiveMapper(CollectiveMapper):
         self.schedule = self.schedules[0]
         block = self.schedule.block_at(me, 0, 0)
         slabs = [nwk_full[(block * S + k) * self.vps:(block * S + k + 1) * self.vps].clone() for k in range(S)]
+        self.codec = self._rotation_codec(nwk_full, ns) if P > 1 else None
         del nwk_full
-        self.rot = DeviceRotator(self.comm, slabs, name="lda-w", metrics=self.metrics)
+        self.rot = DeviceRotator(self.comm, slabs, name="lda-w", metrics=self.metrics, codec=self.codec)
         self.vbeta = self.vocab * cfg.beta
         self.word_perm = perm  # slice s holds words perm[s*vps:(s+1)*vps]
+
+    def _rotation_codec(self, nwk_full: torch.Tensor, ns: int):
+        """Sparse slab payloads for the rotation when they pay. A word's token total (its
+        row sum) never changes during sampling, so the payload bound computed here from
+        the allreduced counts is the same on every worker and holds for the whole run."""
+        from ..ops.slabcodec import SlabCodec, capacity
+
+        mode = self.cfg.rotate_codec
+        if mode == "off" or self.Kp > 65536:
+            return None
+        tokens = nwk_full.sum(1, dtype=torch.int64)
+        cap = max(capacity(tokens[s * self.vps:(s + 1) * self.vps], self.Kp) for s in range(ns))
+        codec = SlabCodec(self.vps, self.Kp, cap, self.device)
+        if mode == "auto" and 2 * codec.nbytes > codec.dense_nbytes():
+            return None
+        return codec
 
     def iterate(self, it: int) -> int:
         cfg = self.cfg
@@ -241,7 +260,9 @@ class LDACollectiveMapper(CollectiveMapper):
             if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
             self._after_iteration(it)
-        self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start}
+        codec = getattr(self, "codec", None)
+        self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start,
+                       "rotate_payload_bytes": codec.nbytes if codec is not None else 0}
 
     # -- checkpoint / resume / model output --------------------------------------------------
     def _ckpt(self):
@@ -251,6 +272,8 @@ class LDACollectiveMapper(CollectiveMapper):
 
     def _after_iteration(self, it: int) -> None:
         cfg = self.cfg
+        if getattr(self, "codec", None) is not None:
+            self.codec.check_overflow()
         self.inject_fault(it)
         if self._ckpt().due(it):
             self.checkpoint(it)

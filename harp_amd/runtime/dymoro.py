@@ -139,11 +139,20 @@ class DeviceRotator:
     mapping to self into a spare buffer, on slice k's private communicator; ``get(k)``
     makes the current stream wait for it (no host sync) and returns the new slab."""
 
-    def __init__(self, comm: Communicator, slabs: Sequence[torch.Tensor], name: str = "rot", metrics=None):
+    def __init__(self, comm: Communicator, slabs: Sequence[torch.Tensor], name: str = "rot", metrics=None,
+                 codec=None):
         self.comm = comm
         self.name = name
         self.slabs = list(slabs)
-        self.spare = [torch.empty_like(s) for s in self.slabs]
+        # ``codec`` (ops.slabcodec.SlabCodec, optional): slabs travel as fixed-size sparse
+        # payloads, encoded on the compute stream after the slab's last use and decoded in
+        # place on arrival (no spare dense slab; the send buffer outlives the send)
+        self.codec = codec if comm.world_size > 1 else None
+        if self.codec is None:
+            self.spare = [torch.empty_like(s) for s in self.slabs]
+        else:
+            self.sendbuf = [self.codec.empty_payload() for _ in self.slabs]
+            self.recvbuf = [self.codec.empty_payload() for _ in self.slabs]
         self.channels = [comm.channel(f"{name}-{k}") for k in range(len(self.slabs))]
         self._work: Dict[int, list] = {}
         self._nops = 0
@@ -157,6 +166,10 @@ class DeviceRotator:
         if dst == me:
             return
         ch = self.channels[k]
+        if self.codec is not None:
+            self.codec.encode(self.slabs[k], self.sendbuf[k])
+            self._work[k] = ch.sendrecv({dst: self.sendbuf[k]}, {src: self.recvbuf[k]}, async_op=True)
+            return
         self._work[k] = ch.sendrecv({dst: self.slabs[k]}, {src: self.spare[k]}, async_op=True)
 
     def get(self, k: int) -> torch.Tensor:
@@ -166,15 +179,19 @@ class DeviceRotator:
                 # the wait makes the compute stream depend on the rotation; events around it
                 # time only the part of the transfer NOT hidden behind compute
                 slab = self.slabs[k]
+                nbytes = self.codec.nbytes if self.codec is not None else slab.numel() * slab.element_size()
                 with self.metrics.time_collective("rotate_wait", self.name, f"slice-{k}-{self._nops}",
-                                                  slab.numel() * slab.element_size(), self.comm.device):
+                                                  nbytes, self.comm.device):
                     for w in works:
                         w.wait()
                 self._nops += 1
             else:
                 for w in works:
                     w.wait()  # stream-level wait on GPU (RCCL), blocking on gloo
-            self.slabs[k], self.spare[k] = self.spare[k], self.slabs[k]
+            if self.codec is not None:
+                self.codec.decode(self.recvbuf[k], self.slabs[k])
+            else:
+                self.slabs[k], self.spare[k] = self.spare[k], self.slabs[k]
         return self.slabs[k]
 
     def wait_all(self) -> None:
