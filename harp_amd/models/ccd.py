@@ -44,6 +44,9 @@ class CCDConfig:
     mode: str = "allgather"   # "allgather": gather the opposite factor per phase; "rotation":
                               # rotate latent-dimension slices (memory O((m + n) r / P) per rank)
     slices_per_rank: int = 2  # rotation mode: dimension slices per rank (2 = transfer / compute overlap)
+    residual_resync: int = 10  # allgather mode, one worker: a phase's exact residuals are carried to the
+                               # other order by a fixed permutation; ResTask recomputes them every N
+                               # iterations (1 = before every phase, the reference's schedule)
 
 
 def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Tensor, n_users: int, n_items: int,
@@ -62,10 +65,24 @@ def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
     def csr(rows_local, cols_global, vals, n_rows):
         o = torch.argsort(rows_local, stable=True)
         r = rows_local[o].to(torch.int32).contiguous()
-        return r, C.row_ptr_of(r, n_rows), cols_global[o].to(torch.int32).contiguous(), vals[o].to(dt).contiguous()
+        return r, C.row_ptr_of(r, n_rows), cols_global[o].to(torch.int32).contiguous(), vals[o].to(dt).contiguous(), o
 
-    ur, uptr, uc, uval = csr(uu.to(dev) // P, ui.to(dev), uv.to(dev), my_users.numel())
-    ir, iptr, ic, ival = csr(ii.to(dev) // P, iu.to(dev), iv.to(dev), my_items.numel())
+    ur, uptr, uc, uval, ou = csr(uu.to(dev) // P, ui.to(dev), uv.to(dev), my_users.numel())
+    ir, iptr, ic, ival, oi = csr(ii.to(dev) // P, iu.to(dev), iv.to(dev), my_items.numel())
+    # One worker holds the same ratings in both orders: a phase leaves exact residuals
+    # (every coordinate update rewrites them), so the other order is a gather through a
+    # fixed permutation instead of a recompute over all nonzeros (ResTask: a 120-dim dot
+    # product per rating, ~20 ms at 1e8 ratings). With P > 1 the row and column blocks of a
+    # worker hold different ratings, so every phase recomputes (the reference's schedule).
+    carry = P == 1 and cfg.residual_resync > 1
+    if carry:
+        inv = torch.empty_like(ou)
+        inv[ou] = torch.arange(ou.numel(), device=ou.device)
+        i2u = inv[oi].contiguous()   # item-order position k holds user-order element i2u[k]
+        inv[oi] = torch.arange(oi.numel(), device=oi.device)
+        u2i = inv[ou].contiguous()
+        del inv
+    del ou, oi
     g = torch.Generator().manual_seed(cfg.seed)
     sc = cfg.init_scale if cfg.init_scale > 0 else cfg.rank ** -0.5
     W0 = (torch.rand((n_users, cfg.rank), generator=g, dtype=torch.float64) * sc).to(dev, dt)
@@ -82,10 +99,17 @@ def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
     for it in range(start, cfg.iterations):
         t0 = time.perf_counter()
         Hf = gather_factors(comm, my_items, H, n_items).contiguous()
-        C.residual(ur, uc, uval, W, Hf, res_u)  # ResTask
+        resync = not carry or it == start or (it - start) % cfg.residual_resync == 0
+        if resync:
+            C.residual(ur, uc, uval, W, Hf, res_u)  # ResTask
+        else:
+            torch.index_select(res_i, 0, u2i, out=res_u)
         C.phase(ur, uptr, uc, res_u, W, Hf, cfg.lam, ulong)
         Wf = gather_factors(comm, my_users, W, n_users).contiguous()
-        C.residual(ir, ic, ival, H, Wf, res_i)
+        if carry:
+            torch.index_select(res_u, 0, i2u, out=res_i)
+        else:
+            C.residual(ir, ic, ival, H, Wf, res_i)
         C.phase(ir, iptr, ic, res_i, H, Wf, cfg.lam, ilong)
         if dev.type == "cuda":
             torch.cuda.synchronize()

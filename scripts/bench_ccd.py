@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rank", type=int, default=120)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--mode", default="allgather", choices=["allgather", "rotation"])
+    ap.add_argument("--resync", type=int, default=10, help="CCDConfig.residual_resync (1 = recompute every phase)")
     a = ap.parse_args()
     import torch
 
@@ -36,13 +37,14 @@ def main():
     sl = slice(me * n // P, (me + 1) * n // P)
     t0 = time.perf_counter()
     out = train_ccd(comm, u[sl], i[sl], v[sl], a.users, a.items,
-                    CCDConfig(rank=a.rank, lam=0.1, iterations=a.iters + 1, mode=a.mode))
+                    CCDConfig(rank=a.rank, lam=0.1, iterations=a.iters + 1, mode=a.mode,
+                                                                  residual_resync=a.resync))
     wall = time.perf_counter() - t0
     its = [h["time_s"] for h in out["history"][1:]]
     s_it = sorted(its)[len(its) // 2]
     if me == 0:
         print(json.dumps({"metric": "MF-CCD seconds/iteration", "value": s_it, "unit": "s/iter", "n_gpus": P,
-                          "rank": a.rank, "nnz": n, "mode": a.mode,
+                          "rank": a.rank, "nnz": n, "mode": a.mode, "residual_resync": a.resync,
                           "peak_hbm_gb": torch.cuda.max_memory_allocated() / 2**30 if torch.cuda.is_available() else None, "coord_updates_per_s": 2 * n * a.rank / s_it,
                           "train_rmse": [h["train_rmse"] for h in out["history"]], "wall_s": wall}), flush=True)
     shutdown()

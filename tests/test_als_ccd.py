@@ -173,3 +173,14 @@ def test_ccd_rotation_mode_multi_rank(P):
     # memory: a rank holds S slices of (m + n) x ceil(r / (S P)) floats, not a full factor
     rs = -(-7 // (2 * P))
     assert rot[0]["slab"] == 2 * (P * -(-150 // P) + P * -(-60 // P)) * rs
+
+
+def test_ccd_residual_carry_equals_recompute():
+    """One worker carries a phase's residuals to the other order by permutation; it must
+    match recomputing them before every phase (ResTask, residual_resync=1)."""
+    u, i, v = _data()
+    a = CD.train_ccd(Communicator(), u, i, v, 40, 30, CD.CCDConfig(rank=3, lam=0.05, iterations=7, residual_resync=1))
+    b = CD.train_ccd(Communicator(), u, i, v, 40, 30, CD.CCDConfig(rank=3, lam=0.05, iterations=7, residual_resync=3))
+    assert torch.allclose(a["W"], b["W"], atol=1e-10) and torch.allclose(a["H"], b["H"], atol=1e-10)
+    for ha, hb in zip(a["history"], b["history"]):
+        assert abs(ha["train_rmse"] - hb["train_rmse"]) < 1e-10

@@ -71,3 +71,22 @@ def test_ccd_rotation_mode_matches_allgather_on_gpu(cuda):
     b = train_ccd(c, u, i, v, 5000, 800, CCDConfig(rank=24, iterations=3, mode="rotation", slices_per_rank=2))
     assert torch.allclose(a["W"], b["W"], rtol=1e-3, atol=1e-4)
     assert a["history"][-1]["train_rmse"] == pytest.approx(b["history"][-1]["train_rmse"], rel=1e-4)
+
+
+def test_ccd_residual_carry_gpu(cuda):
+    """fp32 residuals carried by permutation between phases (one GPU) stay within rounding
+    of the per-phase recompute over 6 iterations."""
+    from harp_amd.models.ccd import CCDConfig, train_ccd
+    from harp_amd.parallel.comm import Communicator
+
+    g = torch.Generator().manual_seed(3)
+    n = 300_000
+    u = torch.randint(0, 6000, (n,), generator=g)
+    i = (torch.rand(n, generator=g) ** 2 * 900).long()  # skewed items: long rows take the lockstep path
+    v = torch.rand(n, generator=g) * 4 + 1
+    c = Communicator(None, cuda)
+    a = train_ccd(c, u, i, v, 6000, 900, CCDConfig(rank=24, iterations=6, residual_resync=1))
+    b = train_ccd(c, u, i, v, 6000, 900, CCDConfig(rank=24, iterations=6))
+    for ha, hb in zip(a["history"], b["history"]):
+        assert hb["train_rmse"] == pytest.approx(ha["train_rmse"], rel=1e-5)
+    assert torch.allclose(a["W"], b["W"], rtol=1e-3, atol=1e-4)
