@@ -117,7 +117,111 @@ __global__ __launch_bounds__(256) void ccd_phase_kernel(const long* __restrict__
   }
 }
 
-// Rows with more than 64*RR nonzeros (e.g. every item in the column phase) run in
+// Medium rows (64*RR < n <= BT*RB nonzeros: most items in the column phase) get ONE
+// 1024-thread workgroup per row, column ids and residuals register-resident for the whole
+// t-loop, exactly the per-row update order of ccd_phase_kernel: per group of 4 dimensions
+// each thread gathers its RB float4 pieces of the other factor, and every coordinate
+// update reduces (up, down) over the workgroup (DPP per wave, then 16 wave partials in
+// double-buffered LDS: one barrier per dimension). One pass over the row's nonzeros per
+// phase instead of the lockstep path's k+2 streaming passes.
+constexpr int BT = 1024, BW = BT / 64;  // threads / waves per medium-row workgroup
+constexpr int RB = 8;                   // register-resident nonzeros per thread (rows <= 8192; 10+ spill)
+
+__global__ __launch_bounds__(BT) void ccd_block_kernel(const int* __restrict__ rows, int n_list,
+                                                       const long* __restrict__ row_ptr, const int* __restrict__ col,
+                                                       float* __restrict__ res, float* __restrict__ Fo,
+                                                       const float* __restrict__ Fx, int k, float lam) {
+  __shared__ float s_red[2][BW][2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int par = 0;
+  // one WG-wide (up, down) total; the parity buffer written here is not rewritten before
+  // every thread has passed the NEXT barrier, i.e. finished these reads
+  auto wg_total = [&](float up, float dn, float& U, float& D) {
+    up = wave_total(up);
+    dn = wave_total(dn);
+    if (lane == 0) { s_red[par][wv][0] = up; s_red[par][wv][1] = dn; }
+    __syncthreads();
+    U = 0.f;
+    D = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < BW; ++w2) { U += s_red[par][w2][0]; D += s_red[par][w2][1]; }
+    par ^= 1;
+  };
+  for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+    const int r = rows[li];
+    const long a = row_ptr[r], b = row_ptr[r + 1];
+    const float down0 = lam * (float)(b - a);
+    float* w = Fo + (long)r * k;
+    int cj[RB];
+    float rj[RB];
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      const long j = a + tid + (long)BT * q;
+      cj[q] = j < b ? col[j] : -1;
+      rj[q] = j < b ? res[j] : 0.f;
+    }
+    int t = 0;
+    if ((k & 3) == 0) {
+      for (; t < k; t += 4) {
+        float4 h4[RB];
+#pragma unroll
+        for (int q = 0; q < RB; ++q)
+          h4[q] = cj[q] >= 0 ? *(const float4*)(Fx + (long)cj[q] * k + t) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 w4 = *(const float4*)(w + t);
+        float wn[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          float up = 0.f, dn = 0.f;
+#pragma unroll
+          for (int q = 0; q < RB; ++q) {
+            const float h = tt == 0 ? h4[q].x : tt == 1 ? h4[q].y : tt == 2 ? h4[q].z : h4[q].w;
+            up = fmaf(fmaf(wn[tt], h, rj[q]), h, up);
+            dn = fmaf(h, h, dn);
+          }
+          float U, D;
+          wg_total(up, dn, U, D);
+          D += down0;
+          const float z = D > 0.f ? U / D : wn[tt];
+          const float delta = z - wn[tt];
+#pragma unroll
+          for (int q = 0; q < RB; ++q) {
+            const float h = tt == 0 ? h4[q].x : tt == 1 ? h4[q].y : tt == 2 ? h4[q].z : h4[q].w;
+            rj[q] = fmaf(-delta, h, rj[q]);
+          }
+          wn[tt] = z;
+        }
+        if (tid == 0) *(float4*)(w + t) = make_float4(wn[0], wn[1], wn[2], wn[3]);
+      }
+    }
+    for (; t < k; ++t) {
+      const float wt = w[t];
+      float hv[RB];
+      float up = 0.f, dn = 0.f;
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        hv[q] = cj[q] >= 0 ? Fx[(long)cj[q] * k + t] : 0.f;
+        up = fmaf(fmaf(wt, hv[q], rj[q]), hv[q], up);
+        dn = fmaf(hv[q], hv[q], dn);
+      }
+      float U, D;
+      wg_total(up, dn, U, D);
+      D += down0;
+      const float z = D > 0.f ? U / D : wt;
+      const float delta = z - wt;
+#pragma unroll
+      for (int q = 0; q < RB; ++q) rj[q] = fmaf(-delta, hv[q], rj[q]);
+      __syncthreads();  // every thread read w[t] before it changes
+      if (tid == 0) w[t] = z;
+    }
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      const long j = a + tid + (long)BT * q;
+      if (j < b) res[j] = rj[q];
+    }
+  }
+}
+
+// Rows with more than BT*RB nonzeros (the most popular items in the column phase) run in
 // LOCKSTEP over the dimensions: they are cut into chunks spread over many workgroups and
 // launch t (t = 0..k+1) does, per chunk,
 //   (a) t-1 < k, t >= 1: res_j -= (z_{t-1} - w_{t-1}) h_{j,t-1}, z from the complete sums
@@ -223,6 +327,18 @@ HARP_EXPORT int harp_ccd_phase(const long* row_ptr, const int* col, float* res, 
   if (blocks > 16384) blocks = 16384;
   ccd_phase_kernel<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(row_ptr, col, res, n_rows, F_own, F_other, k, lam,
                                                                 skip_long);
+  return harp_launch_status();
+}
+
+// medium rows (rows[] lists them; each must have <= harp_ccd_block_max() nonzeros)
+HARP_EXPORT int harp_ccd_block_max() { return BT * RB; }
+
+HARP_EXPORT int harp_ccd_block(const int* rows, int n_list, const long* row_ptr, const int* col, float* res,
+                               float* F_own, const float* F_other, int k, float lam, hipStream_t s) {
+  if (n_list <= 0) return HARP_OK;
+  if (k <= 0) return HARP_EBADARG;
+  const int blocks = n_list < 8192 ? n_list : 8192;
+  ccd_block_kernel<<<dim3(blocks), dim3(BT), 0, s>>>(rows, n_list, row_ptr, col, res, F_own, F_other, k, lam);
   return harp_launch_status();
 }
 

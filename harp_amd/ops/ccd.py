@@ -12,6 +12,9 @@ _lib.register({
     "harp_ccd_lockstep": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                           _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_float, _lib.c_void_p,
                           _lib.c_void_p, _lib.c_void_p],
+    "harp_ccd_block_max": [],
+    "harp_ccd_block": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                       _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_void_p],
     "harp_ccd_residual": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p],
 })
@@ -24,17 +27,30 @@ def row_ptr_of(rows: torch.Tensor, n_rows: int) -> torch.Tensor:
     return ptr
 
 
-LONG_ROW = 256  # rows above this many nonzeros run the lockstep (chunked, per-dimension) path
+LONG_ROW = 256  # rows above this many nonzeros leave the wave-per-row kernel
 CHUNK = 4096
 
 
-class RowPlan:
-    """Per-phase launch plan: the chunks of every row longer than LONG_ROW."""
+def block_max() -> int:
+    """Longest row of the workgroup-per-row kernel (csrc/ccd.hip ccd_block_kernel); longer
+    rows run the lockstep (chunked, per-dimension) path. 0 without a GPU library."""
+    try:
+        return int(_lib.kernels().harp_ccd_block_max())
+    except _lib.NativeUnavailable:
+        return 0
 
-    def __init__(self, row_ptr: torch.Tensor):
+
+class RowPlan:
+    """Per-phase launch plan: rows of LONG_ROW < n <= block_max() nonzeros (one workgroup
+    each) and the chunks of every longer row (lockstep)."""
+
+    def __init__(self, row_ptr: torch.Tensor, block_rows: bool = True):
         lens = (row_ptr[1:] - row_ptr[:-1]).cpu()
         rp = row_ptr.cpu()
-        longr = torch.nonzero(lens > LONG_ROW).reshape(-1)
+        bmax = block_max() if (block_rows and row_ptr.is_cuda) else 0
+        mid = torch.nonzero((lens > LONG_ROW) & (lens <= bmax)).reshape(-1) if bmax else torch.empty(0, dtype=torch.long)
+        self.mid = mid.to(torch.int32).to(row_ptr.device)
+        longr = torch.nonzero(lens > max(LONG_ROW, bmax)).reshape(-1)
         self.n_long = longr.numel()
         ch = []
         for slot, r in enumerate(longr.tolist()):
@@ -61,8 +77,13 @@ def phase(rows: torch.Tensor, row_ptr: torch.Tensor, cols: torch.Tensor, res: to
         lib = _lib.kernels()
         stream = _lib.stream_ptr(res.device)
         st = lib.harp_ccd_phase(row_ptr.data_ptr(), cols.data_ptr(), res.data_ptr(), n_rows, F_own.data_ptr(),
-                                F_other.data_ptr(), k, float(lam), 1 if plan.n_long else 0, stream)
+                                F_other.data_ptr(), k, float(lam), 1 if (plan.n_long or plan.mid.numel()) else 0,
+                                stream)
         _lib.check(st, "ccd_phase")
+        if plan.mid.numel():
+            st = lib.harp_ccd_block(plan.mid.data_ptr(), plan.mid.numel(), row_ptr.data_ptr(), cols.data_ptr(),
+                                    res.data_ptr(), F_own.data_ptr(), F_other.data_ptr(), k, float(lam), stream)
+            _lib.check(st, "ccd_block")
         if plan.n_long:
             FxT = F_other.t().contiguous()  # feature-major: one dimension = one L2-resident column
             if getattr(plan, "hbuf", None) is None or plan.hbuf.numel() != res.numel():
