@@ -124,14 +124,19 @@ __global__ __launch_bounds__(256) void ccd_phase_kernel(const long* __restrict__
 // update reduces (up, down) over the workgroup (DPP per wave, then 16 wave partials in
 // double-buffered LDS: one barrier per dimension). One pass over the row's nonzeros per
 // phase instead of the lockstep path's k+2 streaming passes.
+// RB = 8: column ids and residuals in registers (rows <= 8192; 10+ spill). RB = 12 (rows
+// <= 12288): the column ids move to LDS (48 KB; read once per 4 dimensions), residuals and
+// the gathered float4 pieces stay in registers (14+ spill).
 constexpr int BT = 1024, BW = BT / 64;  // threads / waves per medium-row workgroup
-constexpr int RB = 8;                   // register-resident nonzeros per thread (rows <= 8192; 10+ spill)
 
+template <int RB>
 __global__ __launch_bounds__(BT) void ccd_block_kernel(const int* __restrict__ rows, int n_list,
                                                        const long* __restrict__ row_ptr, const int* __restrict__ col,
                                                        float* __restrict__ res, float* __restrict__ Fo,
                                                        const float* __restrict__ Fx, int k, float lam) {
+  constexpr bool CJ_LDS = RB > 8;
   __shared__ float s_red[2][BW][2];
+  __shared__ int s_cj[CJ_LDS ? BT * RB : 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int par = 0;
   // one WG-wide (up, down) total; the parity buffer written here is not rewritten before
@@ -152,21 +157,30 @@ __global__ __launch_bounds__(BT) void ccd_block_kernel(const int* __restrict__ r
     const long a = row_ptr[r], b = row_ptr[r + 1];
     const float down0 = lam * (float)(b - a);
     float* w = Fo + (long)r * k;
-    int cj[RB];
+    int cjr[CJ_LDS ? 1 : RB];
     float rj[RB];
+    if (CJ_LDS) __syncthreads();  // the previous row's readers of s_cj are done
 #pragma unroll
     for (int q = 0; q < RB; ++q) {
       const long j = a + tid + (long)BT * q;
-      cj[q] = j < b ? col[j] : -1;
+      const int c = j < b ? col[j] : -1;
+      if constexpr (CJ_LDS) s_cj[q * BT + tid] = c;  // own slots only: no barrier needed
+      else cjr[q] = c;
       rj[q] = j < b ? res[j] : 0.f;
     }
+    auto cj = [&](int q) -> int {
+      if constexpr (CJ_LDS) return s_cj[q * BT + tid];
+      else return cjr[q];
+    };
     int t = 0;
     if ((k & 3) == 0) {
       for (; t < k; t += 4) {
         float4 h4[RB];
 #pragma unroll
-        for (int q = 0; q < RB; ++q)
-          h4[q] = cj[q] >= 0 ? *(const float4*)(Fx + (long)cj[q] * k + t) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < RB; ++q) {
+          const int c = cj(q);
+          h4[q] = c >= 0 ? *(const float4*)(Fx + (long)c * k + t) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         const float4 w4 = *(const float4*)(w + t);
         float wn[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
@@ -199,7 +213,8 @@ __global__ __launch_bounds__(BT) void ccd_block_kernel(const int* __restrict__ r
       float up = 0.f, dn = 0.f;
 #pragma unroll
       for (int q = 0; q < RB; ++q) {
-        hv[q] = cj[q] >= 0 ? Fx[(long)cj[q] * k + t] : 0.f;
+        const int c = cj(q);
+        hv[q] = c >= 0 ? Fx[(long)c * k + t] : 0.f;
         up = fmaf(fmaf(wt, hv[q], rj[q]), hv[q], up);
         dn = fmaf(hv[q], hv[q], dn);
       }
@@ -330,15 +345,19 @@ HARP_EXPORT int harp_ccd_phase(const long* row_ptr, const int* col, float* res, 
   return harp_launch_status();
 }
 
-// medium rows (rows[] lists them; each must have <= harp_ccd_block_max() nonzeros)
-HARP_EXPORT int harp_ccd_block_max() { return BT * RB; }
+// medium rows (rows[] lists them): wide = 0 takes rows of <= harp_ccd_block_max(0) nonzeros,
+// wide = 1 rows of <= harp_ccd_block_max(1)
+HARP_EXPORT int harp_ccd_block_max(int wide) { return BT * (wide ? 12 : 8); }
 
 HARP_EXPORT int harp_ccd_block(const int* rows, int n_list, const long* row_ptr, const int* col, float* res,
-                               float* F_own, const float* F_other, int k, float lam, hipStream_t s) {
+                               float* F_own, const float* F_other, int k, float lam, int wide, hipStream_t s) {
   if (n_list <= 0) return HARP_OK;
   if (k <= 0) return HARP_EBADARG;
   const int blocks = n_list < 8192 ? n_list : 8192;
-  ccd_block_kernel<<<dim3(blocks), dim3(BT), 0, s>>>(rows, n_list, row_ptr, col, res, F_own, F_other, k, lam);
+  if (wide)
+    ccd_block_kernel<12><<<dim3(blocks), dim3(BT), 0, s>>>(rows, n_list, row_ptr, col, res, F_own, F_other, k, lam);
+  else
+    ccd_block_kernel<8><<<dim3(blocks), dim3(BT), 0, s>>>(rows, n_list, row_ptr, col, res, F_own, F_other, k, lam);
   return harp_launch_status();
 }
 

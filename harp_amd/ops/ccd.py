@@ -12,9 +12,9 @@ _lib.register({
     "harp_ccd_lockstep": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                           _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_float, _lib.c_void_p,
                           _lib.c_void_p, _lib.c_void_p],
-    "harp_ccd_block_max": [],
+    "harp_ccd_block_max": [_lib.c_int],
     "harp_ccd_block": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
-                       _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_void_p],
+                       _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_int, _lib.c_void_p],
     "harp_ccd_residual": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p,
                           _lib.c_int, _lib.c_void_p, _lib.c_void_p],
 })
@@ -31,26 +31,30 @@ LONG_ROW = 256  # rows above this many nonzeros leave the wave-per-row kernel
 CHUNK = 4096
 
 
-def block_max() -> int:
-    """Longest row of the workgroup-per-row kernel (csrc/ccd.hip ccd_block_kernel); longer
-    rows run the lockstep (chunked, per-dimension) path. 0 without a GPU library."""
+def block_max(wide: bool = False) -> int:
+    """Longest row of the workgroup-per-row kernel (csrc/ccd.hip ccd_block_kernel: 8192
+    nonzeros, ``wide`` 12288); longer rows run the lockstep (chunked, per-dimension) path.
+    0 without a GPU library."""
     try:
-        return int(_lib.kernels().harp_ccd_block_max())
+        return int(_lib.kernels().harp_ccd_block_max(1 if wide else 0))
     except _lib.NativeUnavailable:
         return 0
 
 
 class RowPlan:
     """Per-phase launch plan: rows of LONG_ROW < n <= block_max() nonzeros (one workgroup
-    each) and the chunks of every longer row (lockstep)."""
+    each; ``mid``), rows up to block_max(wide=True) (``wide``), and the chunks of every
+    longer row (lockstep)."""
 
     def __init__(self, row_ptr: torch.Tensor, block_rows: bool = True):
         lens = (row_ptr[1:] - row_ptr[:-1]).cpu()
         rp = row_ptr.cpu()
         bmax = block_max() if (block_rows and row_ptr.is_cuda) else 0
-        mid = torch.nonzero((lens > LONG_ROW) & (lens <= bmax)).reshape(-1) if bmax else torch.empty(0, dtype=torch.long)
-        self.mid = mid.to(torch.int32).to(row_ptr.device)
-        longr = torch.nonzero(lens > max(LONG_ROW, bmax)).reshape(-1)
+        wmax = block_max(True) if bmax else 0
+        pick = lambda lo, hi: torch.nonzero((lens > lo) & (lens <= hi)).reshape(-1).to(torch.int32).to(row_ptr.device)
+        self.mid = pick(LONG_ROW, bmax)
+        self.wide = pick(max(LONG_ROW, bmax), wmax)
+        longr = torch.nonzero(lens > max(LONG_ROW, wmax)).reshape(-1)
         self.n_long = longr.numel()
         ch = []
         for slot, r in enumerate(longr.tolist()):
@@ -77,13 +81,15 @@ def phase(rows: torch.Tensor, row_ptr: torch.Tensor, cols: torch.Tensor, res: to
         lib = _lib.kernels()
         stream = _lib.stream_ptr(res.device)
         st = lib.harp_ccd_phase(row_ptr.data_ptr(), cols.data_ptr(), res.data_ptr(), n_rows, F_own.data_ptr(),
-                                F_other.data_ptr(), k, float(lam), 1 if (plan.n_long or plan.mid.numel()) else 0,
-                                stream)
+                                F_other.data_ptr(), k, float(lam),
+                                1 if (plan.n_long or plan.mid.numel() or plan.wide.numel()) else 0, stream)
         _lib.check(st, "ccd_phase")
-        if plan.mid.numel():
-            st = lib.harp_ccd_block(plan.mid.data_ptr(), plan.mid.numel(), row_ptr.data_ptr(), cols.data_ptr(),
-                                    res.data_ptr(), F_own.data_ptr(), F_other.data_ptr(), k, float(lam), stream)
-            _lib.check(st, "ccd_block")
+        for wide, lst in ((0, plan.mid), (1, plan.wide)):
+            if lst.numel():
+                st = lib.harp_ccd_block(lst.data_ptr(), lst.numel(), row_ptr.data_ptr(), cols.data_ptr(),
+                                        res.data_ptr(), F_own.data_ptr(), F_other.data_ptr(), k, float(lam), wide,
+                                        stream)
+                _lib.check(st, "ccd_block")
         if plan.n_long:
             FxT = F_other.t().contiguous()  # feature-major: one dimension = one L2-resident column
             if getattr(plan, "hbuf", None) is None or plan.hbuf.numel() != res.numel():

@@ -12,9 +12,11 @@ pytestmark = pytest.mark.gpu
 def test_ccd_phase_and_residual(cuda, k):
     g = torch.Generator().manual_seed(k)
     n_rows, n_cols = 300, 500
-    # rows 7 / 13 / 17 (257-8192 nonzeros): workgroup-per-row kernel; row 11 (> 8192): lockstep
+    # rows 7 / 13 / 17 (257-8192 nonzeros): workgroup-per-row kernel; row 11 (8193-12288): its
+    # wide form (column ids in LDS); row 19 (> 12288): lockstep
     rows = torch.cat([torch.randint(0, n_rows, (20000,), generator=g), torch.full((700,), 7),
-                      torch.full((9000,), 11), torch.full((5000,), 13), torch.full((200,), 17)])
+                      torch.full((9000,), 11), torch.full((5000,), 13), torch.full((200,), 17),
+                      torch.full((13000,), 19)])
     cols = torch.randint(0, n_cols, (rows.numel(),), generator=g)
     vals = torch.rand(rows.numel(), generator=g, dtype=torch.float64) * 4 + 1
     o = torch.argsort(rows, stable=True)
