@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--skew", type=float, default=2.0, help="item popularity skew (1 = uniform)")
     ap.add_argument("--blocks-per-xcd", type=int, default=128)
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (only 0 is built)")
+    ap.add_argument("--slices", type=int, default=2, help="H slices per rank (rotation slice steps per epoch)")
     a = ap.parse_args()
     import torch
 
@@ -43,7 +44,7 @@ def main():
     gen_s = time.perf_counter() - t0
     cfg = SGDConfig(rank=a.rank, lam=a.lam, lr=a.lr, epochs=a.warmup + a.epochs, chunk=a.chunk, test_every=0,
                     xcd_blocks=a.layout == "xcd", blocks_per_xcd=a.blocks_per_xcd,
-                    kernel_variant=a.variant)
+                    kernel_variant=a.variant, num_slices=a.slices)
     m = SGDCollectiveMapper(comm, cfg, a.users, a.items, (u, i, v), None)
     m.init_model(KeyValReader([]))
     del u, i, v
@@ -77,7 +78,7 @@ def main():
                           "value": n / dt, "unit": "updates/s", "n_gpus": comm.world_size, "epochs": a.epochs,
                           "s_per_epoch": dt / a.epochs, "train_rmse": tr, "data_gen_s": gen_s,
                           "ratings": a.ratings, "rank": a.rank, "dtype": "fp32 factors",
-                          "layout": a.layout, "skew": a.skew, "chunk": a.chunk, "blocks_per_xcd": a.blocks_per_xcd, "variant": a.variant}), flush=True)
+                          "layout": a.layout, "skew": a.skew, "chunk": a.chunk, "blocks_per_xcd": a.blocks_per_xcd, "variant": a.variant, "slices": a.slices}), flush=True)
     shutdown()
 
 
