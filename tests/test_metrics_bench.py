@@ -132,3 +132,14 @@ def test_bench_single_rank_with_sgd_record():
     assert rec["n_gpus"] == 1 and rec["metric"].startswith("sec/iteration K-means")
     s = rec["sgd"]
     assert s["updates_per_sec"] > 0 and s["epochs"] == 2 and 0 < s["train_rmse"] < 2
+
+
+def test_bench_sgd_guard_keeps_headline_line():
+    """A nested MF-SGD record that exceeds --sgd-timeout (a hung rotation peer on a real
+    node) still yields exactly one JSON line: the measured K-means record with sgd.error,
+    and every rank exits 0."""
+    rec = _run_bench(["--gpus", "2", "--points", "2e4", "--centroids", "128", "--backend", "gloo", "--steps", "2",
+                      "--warmup", "1", "--sgd", "on", "--sgd-users", "2000", "--sgd-items", "300",
+                      "--sgd-ratings", "20000", "--sgd-rank", "16", "--sgd-timeout", "0.01"])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0
+    assert "timeout" in rec["sgd"]["error"]
