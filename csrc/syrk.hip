@@ -76,7 +76,8 @@ __device__ __forceinline__ bf16x8 frag(const char* P, int blk, int lo) {
 // DIAG (timing diagnostics only, results are garbage): 1 = no global loads after the first
 // stage (MFMA + LDS + barriers), 2 = no MFMA (loads + LDS reads + a VALU use of the
 // fragments), 3 = loads + barriers only, 4 = every stage loads the first stage's (L2-hot)
-// samples (same instruction stream, no L2 misses), 5 = off-diagonal tiles only (pairs exit)
+// samples (same instruction stream, no L2 misses), 5 = off-diagonal tiles only (pairs exit),
+// 6 = diagonal pairs only
 template <int DIAG>
 __device__ __forceinline__ void mma(const bf16x8& a, const bf16x8& b, floatx16& c) {
   if constexpr (DIAG == 2) c[0] += (float)a[0] * (float)b[7];
@@ -264,6 +265,9 @@ __global__ __launch_bounds__((MT_ / (32 * BA_)) * (MT_ / (32 * BB_)) * 64) void 
   J.sync = sync;
   J.sync_every = sync_every;
   J.second = wave >= NB / 2;
+  if constexpr (DIAG == 6) {  // diagnostics: diagonal pairs only
+    if (!pair) return;
+  }
   if (!pair) return syrk_body<C, -1, DIAG>(J, smem, tid);
   if constexpr (DIAG == 5) return;  // diagnostics: off-diagonal tiles only
   switch (wave % (NB / 2)) {  // wave-uniform
@@ -382,6 +386,7 @@ HARP_EXPORT int harp_syrk_diag(const void* XT, long ld, long n, int d_pad, float
     case 3: return launch_syrk<256, 2, 4, 3>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     case 4: return launch_syrk<256, 2, 4, 4>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     case 5: return launch_syrk<256, 2, 4, 5>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
+    case 6: return launch_syrk<256, 2, 4, 6>(XT, ld, n, d_pad, G, ldg, num_splits, 1024, s);
     default: return HARP_EBADARG;
   }
 }
