@@ -150,6 +150,63 @@ __global__ __launch_bounds__(kThreads) void als_normal_kernel(const long* __rest
   if (tid < f) rhs[r * (long)f + tid] = racc;
 }
 
+// Batched SPD solve A x = rhs (fp32, f <= 64), ONE WAVE PER SYSTEM and no barriers: lane i
+// holds row i of A (zero-padded to 64, identity rows past f) in 64 VGPRs. Right-looking
+// Cholesky over the unrolled columns j: the pivot and the column entries L[k][j] are wave
+// broadcasts (v_readlane), each lane updates its own row; L y = b broadcasts y_j; L^T x = y
+// takes x_j = (y_j - sum_{k>j} L[k][j] x_k) / L[j][j] as a wave reduction per column. The
+// fused kernel's in-LDS Cholesky spent 3 workgroup barriers per column (about 70 % of a
+// 131k-row block, profiles/r2_als); this one is VALU-issue bound.
+__global__ __launch_bounds__(256) void als_chol_solve_kernel(const float* __restrict__ A, const float* __restrict__ rhs,
+                                                            int f, long m, float* __restrict__ X,
+                                                            int* __restrict__ info) {
+  const int lane = threadIdx.x & 63;
+  const long r = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= m) return;  // wave-uniform
+  float a[kMaxF];
+  const float* Ar = A + r * (long)f * f + (long)lane * f;
+#pragma unroll
+  for (int k = 0; k < kMaxF; ++k) a[k] = lane < f ? (k < f ? Ar[k] : 0.f) : (k == lane ? 1.f : 0.f);
+  float b = lane < f ? rhs[r * (long)f + lane] : 0.f;
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxF; ++j) {
+    float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), j));
+    if (!(d > 0.f)) {
+      bad = 1;
+      d = 1.f;
+    }
+    const float sq = sqrtf(d), inv = 1.f / sq;
+    a[j] = lane == j ? sq : a[j] * inv;  // column j of L (rows > j); the diagonal
+#pragma unroll
+    for (int k = j + 1; k < kMaxF; ++k) {
+      const float lk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), k));
+      a[k] = fmaf(-a[j], lk, a[k]);  // row `lane`, column k (only k <= lane is ever read)
+    }
+  }
+  // L y = b
+#pragma unroll
+  for (int j = 0; j < kMaxF; ++j) {
+    const float ljj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), j));
+    const float yj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b), j)) / ljj;
+    if (lane == j) b = yj;
+    else if (lane > j) b = fmaf(-a[j], yj, b);
+  }
+  // L^T x = y
+  float x = 0.f;
+#pragma unroll
+  for (int j = kMaxF - 1; j >= 0; --j) {
+    float t = lane > j ? a[j] * x : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    const float ljj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), j));
+    const float yj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b), j));
+    if (lane == j) x = (yj - t) / ljj;
+  }
+  if (lane < f) X[r * (long)f + lane] = x;
+  if (lane == 0) info[r] = bad;
+}
+
 template <typename T>
 int launch(const long* crow, const long* cols, const T* vals, const T* F, int f, const T* G, int implicit, T alpha,
            T lam, int scale_lam, T* A, T* rhs, long row0, long nrows, T* X, int* info, hipStream_t s) {
@@ -176,4 +233,14 @@ HARP_EXPORT int harp_als_normal_f64(const long* crow, const long* cols, const do
                                     double* rhs, long row0, long nrows, double* X, int* info, hipStream_t s) {
   return launch<double>(crow, cols, vals, F, f, G, implicit, alpha, lam, scale_lam, A, rhs, row0, nrows, X, info,
                         s);
+}
+
+// X [m, f] = A [m, f, f]^-1 rhs [m, f] for SPD A (fp32, f <= 64; one wave per system);
+// info[r] = 1 marks a non-positive pivot (that row's X is not a solution)
+HARP_EXPORT int harp_als_chol_solve_f32(const float* A, const float* rhs, int f, long m, float* X, int* info,
+                                        hipStream_t s) {
+  if (m <= 0) return HARP_OK;
+  if (f <= 0 || f > kMaxF || !A || !rhs || !X || !info || m > 0x7fffffffL / 4) return HARP_EBADARG;
+  als_chol_solve_kernel<<<dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s>>>(A, rhs, f, m, X, info);
+  return harp_launch_status();
 }

@@ -41,6 +41,8 @@ class ALSConfig:
     weighted_lambda: bool = False  # lambda * n_u (ALS-WR) instead of lambda
     seed: int = 0
     block_bytes: int = 1 << 28
+    wave_solve: bool = True   # fp32 GPU: build A / rhs, then the one-wave-per-system Cholesky kernel
+                              # (False: the fused build + in-LDS solve kernel)
     checkpoint_dir: str = ""  # .hpt checkpoints of X / Y (global row ids: any world size resumes)
     checkpoint_every: int = 0
     model_dir: str = ""       # final text dump W-<worker> (users), H-<worker> (items)
@@ -83,6 +85,16 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
             # not SPD (info) send the block through rocSOLVER with the lstsq fallback
             scale = cfg.weighted_lambda or not cfg.implicit
             info = torch.empty(b - a, dtype=torch.int32, device=dev)
+            if dt == torch.float32 and cfg.wave_solve:
+                # build pass, then one wave per system (register Cholesky, no workgroup
+                # barriers): the fused kernel's in-LDS solve was ~70 % of its time
+                A = torch.empty((b - a, f, f), dtype=dt, device=dev)
+                rhs = torch.empty((b - a, f), dtype=dt, device=dev)
+                OA.normal_equations(crow, cols64, vals_dt, F, G, cfg.implicit, cfg.alpha, cfg.lam, scale, A, rhs, a)
+                OA.chol_solve(A, rhs, out[a:b], info)
+                if bool(info.any()):
+                    out[a:b] = _solve(A, rhs)
+                continue
             OA.normal_equations(crow, cols64, vals_dt, F, G, cfg.implicit, cfg.alpha, cfg.lam, scale, None, None, a,
                                 X=out[a:b], info=info)
             if bool(info.any()):

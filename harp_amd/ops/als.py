@@ -15,6 +15,8 @@ _lib.register({
            _lib.c_void_p]
     for name, ct in (("harp_als_normal_f32", _lib.c_float), ("harp_als_normal_f64", _lib.c_double))
 })
+_lib.register({"harp_als_chol_solve_f32": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_void_p,
+                                           _lib.c_void_p, _lib.c_void_p]})
 
 
 def available(t: torch.Tensor) -> bool:
@@ -49,3 +51,16 @@ def normal_equations(crow: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
             int(bool(scale_lam)), None if solve else A.data_ptr(), None if solve else rhs.data_ptr(), int(row0), m,
             X.data_ptr() if solve else None, info.data_ptr() if solve else None, _lib.stream_ptr(F.device))
     _lib.check(st, "als_normal")
+
+
+def chol_solve(A: torch.Tensor, rhs: torch.Tensor, X: torch.Tensor, info: torch.Tensor) -> None:
+    """X[r] = A[r]^-1 rhs[r] for a batch of SPD fp32 systems (f <= 64) on the GPU: one wave
+    per system, Cholesky in registers (csrc/als.hip als_chol_solve_kernel); info[r] = 1
+    marks a non-positive pivot."""
+    m, f = rhs.shape
+    assert A.shape == (m, f, f) and A.dtype == rhs.dtype == X.dtype == torch.float32 and f <= MAX_F
+    assert X.shape == (m, f) and info.shape == (m,) and info.dtype == torch.int32
+    for t in (A, rhs, X, info):
+        assert t.is_contiguous() and t.device == A.device
+    _lib.check(_lib.kernels().harp_als_chol_solve_f32(A.data_ptr(), rhs.data_ptr(), f, m, X.data_ptr(),
+                                                      info.data_ptr(), _lib.stream_ptr(A.device)), "als_chol_solve")

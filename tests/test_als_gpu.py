@@ -23,10 +23,11 @@ def _problem(n_rows, n_cols, nnz, f, seed):
 
 
 @pytest.mark.parametrize("implicit", [False, True])
-@pytest.mark.parametrize("f,dt", [(8, torch.float64), (50, torch.float32), (64, torch.float64)])
-def test_solve_rows_native_matches_torch(cuda, implicit, f, dt):
+@pytest.mark.parametrize("f,dt,wave", [(8, torch.float64, True), (50, torch.float32, True), (50, torch.float32, False),
+                                       (64, torch.float32, True), (64, torch.float64, True)])
+def test_solve_rows_native_matches_torch(cuda, implicit, f, dt, wave):
     rows, cols, vals, F = _problem(700, 300, 6000, f, f)
-    cfg = A.ALSConfig(factors=f, implicit=implicit, alpha=2.0, lam=0.1, block_bytes=1 << 22)
+    cfg = A.ALSConfig(factors=f, implicit=implicit, alpha=2.0, lam=0.1, block_bytes=1 << 22, wave_solve=wave)
     want = A.solve_rows(rows, cols, vals, 700, F, cfg)  # CPU: torch path, fp64
     got = A.solve_rows(rows.to(cuda), cols.to(cuda), vals.to(cuda), 700, F.to(cuda, dt), cfg)
     tol = 1e-9 if dt == torch.float64 else 2e-3
@@ -71,3 +72,24 @@ def test_fused_solve_flags_non_spd_rows(cuda):
     got = A.solve_rows(rows.to(cuda), cols.to(cuda), vals.to(cuda), 64, F.to(cuda), cfg)
     # the flagged block went through the rocSOLVER path; its SPD rows agree with the fused solve
     assert torch.allclose(got[:61].cpu(), X[:61].cpu(), rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.parametrize("f", [1, 7, 32, 64])
+def test_wave_chol_solve_matches_torch(cuda, f):
+    """One-wave-per-system register Cholesky (als_chol_solve_kernel) vs torch.linalg.solve
+    in fp64 on random SPD systems; a non-SPD system is flagged, the others are unaffected."""
+    g = torch.Generator().manual_seed(f)
+    m = 37
+    B = torch.randn(m, f, f + 3, generator=g, dtype=torch.float64)
+    Am = B @ B.transpose(1, 2) + 0.5 * torch.eye(f, dtype=torch.float64)
+    rhs = torch.randn(m, f, generator=g, dtype=torch.float64)
+    Am[5] = -torch.eye(f, dtype=torch.float64)  # not SPD
+    want = torch.linalg.solve(Am, rhs[:, :, None])[:, :, 0]
+    X = torch.empty(m, f, device=cuda)
+    info = torch.full((m,), 7, dtype=torch.int32, device=cuda)
+    OA.chol_solve(Am.to(cuda, torch.float32).contiguous(), rhs.to(cuda, torch.float32).contiguous(), X, info)
+    info = info.cpu()
+    assert info[5] == 1 and int(info.sum()) == 1
+    ok = torch.arange(m) != 5
+    scale = want[ok].abs().max()
+    assert torch.allclose(X.cpu().double()[ok], want[ok], rtol=2e-3, atol=2e-4 * float(scale))
