@@ -103,6 +103,15 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
   int bestt[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) { best[g] = KM_BIG; bestt[g] = 0; }
+  // argmin of one 32x32 tile into (best, bestt)[g]: the 16 candidates' register index rides
+  // in the low mantissa bits (one v_and_or per candidate). A plain v_min3 with the index
+  // searched only on improvement measured 5 % slower (it spills; profiles/r2_ktail).
+  auto tile_argmin = [&](const floatx16& ac, int g, int tg) {
+    float m = keyed(ac[0], 0u);
+#pragma unroll
+    for (int q = 1; q < 16; ++q) m = fminf(m, keyed(ac[q], (unsigned)q));
+    if (m < best[g]) { best[g] = m; bestt[g] = tg; }
+  };
 
   // per-lane byte offsets of its A-fragment chunks inside a 32-row group
   int aoff[KS];
@@ -150,11 +159,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
 #pragma unroll
           for (int s = 0; s < KS; ++s) an = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg1 & 1][s], xf[g1][s], an, 0, 0, 0);
         }
-        const floatx16& ac = acc[i & 1];
-        float m = keyed(ac[0], 0u);
-#pragma unroll
-        for (int q = 1; q < 16; ++q) m = fminf(m, keyed(ac[q], (unsigned)q));
-        if (m < best[g]) { best[g] = m; bestt[g] = t * RG + rg; }
+        tile_argmin(acc[i & 1], g, t * RG + rg);
         if constexpr (PIPE == 2) {
 #pragma unroll
           for (int s = 0; s < KS; ++s) {
@@ -178,10 +183,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
 #pragma unroll
         for (int s = 0; s < KS; ++s)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][s], xf[g][s], acc, 0, 0, 0);
-        float m = keyed(acc[0], 0u);
-#pragma unroll
-        for (int i = 1; i < 16; ++i) m = fminf(m, keyed(acc[i], (unsigned)i));
-        if (m < best[g]) { best[g] = m; bestt[g] = tg; }
+        tile_argmin(acc, g, tg);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -203,10 +205,7 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
         floatx16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], xf[g][s], acc, 0, 0, 0);
-        float m = keyed(acc[0], 0u);
-#pragma unroll
-        for (int i = 1; i < 16; ++i) m = fminf(m, keyed(acc[i], (unsigned)i));
-        if (m < best[g]) { best[g] = m; bestt[g] = tg; }
+        tile_argmin(acc, g, tg);
       }
     }
   }
