@@ -151,6 +151,10 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             raise NotImplementedError(f"native K-means supports d <= {256 - ONES} (got d={op.d})")
         if dp > 128:
             variant = 4  # the only instantiation for 9..16 k-steps
+        elif variant == DEFAULT_VARIANT and dp // 16 == 5:
+            # the default tiling spills 22 VGPRs at 5 k-steps (d = 61..76); its RG=2 neighbour
+            # does not: 112.1 vs 128.5 ms per assign at N = 1e8, d = 64 (profiles/r2_ktail)
+            variant = 13
         ppb = lib.harp_kmeans_points_per_block(variant)
         if ppb <= 0:
             raise ValueError(f"unknown kmeans kernel variant {variant}")

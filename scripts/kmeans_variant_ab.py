@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of assign-kernel variants in one process (N = 1e8, d = 100, K = 1e4): time per
-assign and label agreement with the first variant. python scripts/kmeans_variant_ab.py 14 15 14"""
+assign and label agreement with the first variant. python scripts/kmeans_variant_ab.py [d=100] 14 13 14"""
 import json
 import os
 import sys
@@ -13,8 +13,10 @@ def main():
 
     from harp_amd.ops import kmeans as K
 
-    variants = [int(v) for v in sys.argv[1:]] or [14, 15, 14]
-    n, d, k = 100_000_000, 100, 10_000
+    args = [a for a in sys.argv[1:] if not a.startswith("d=")]
+    variants = [int(v) for v in args] or [14, 13, 14]
+    d = int(next((a[2:] for a in sys.argv[1:] if a.startswith("d=")), 100))
+    n, k = 100_000_000, 10_000
     X = K.generate_points(n, d, seed=1, device="cuda")
     c = torch.rand(k, d, device="cuda") * 1000
     op = K.prepare(c, X.shape[1])
