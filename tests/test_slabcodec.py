@@ -59,10 +59,12 @@ def _job(comm, cfg, nd, V, toks):
     return run_lda(comm, cfg, nd, V, toks)
 
 
-def test_lda_rotation_codec_matches_dense():
+@pytest.mark.parametrize("P", [2, 3])
+def test_lda_rotation_codec_matches_dense(P):
+    """P = 3 rotates its two slices on different ring strides (1 and 2)."""
     corpus = synthetic_corpus(300, 2000, 8, 40, seed=2)
     base = dict(num_topics=64, alpha=0.1, beta=0.01, iterations=6, print_interval=2, num_slices=2)
-    dense = launch(_job, 2, args=(LDAConfig(rotate_codec="off", **base), 300, 2000, corpus), timeout=300)
-    sparse = launch(_job, 2, args=(LDAConfig(rotate_codec="on", **base), 300, 2000, corpus), timeout=300)
+    dense = launch(_job, P, args=(LDAConfig(rotate_codec="off", **base), 300, 2000, corpus), timeout=300)
+    sparse = launch(_job, P, args=(LDAConfig(rotate_codec="on", **base), 300, 2000, corpus), timeout=300)
     assert dense[0]["rotate_payload_bytes"] == 0 and sparse[0]["rotate_payload_bytes"] > 0
     assert dense[0]["loglik"] == sparse[0]["loglik"], (dense[0]["loglik"], sparse[0]["loglik"])
