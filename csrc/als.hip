@@ -157,18 +157,37 @@ __global__ __launch_bounds__(kThreads) void als_normal_kernel(const long* __rest
 // takes x_j = (y_j - sum_{k>j} L[k][j] x_k) / L[j][j] as a wave reduction per column. The
 // fused kernel's in-LDS Cholesky spent 3 workgroup barriers per column (about 70 % of a
 // 131k-row block, profiles/r2_als); this one is VALU-issue bound.
+// LDS_BCAST = 1: column j of L goes through a per-wave LDS row (one ds_write, then
+// same-address broadcast reads the compiler merges into ds_read_b128) instead of 63 - j
+// v_readlane + SGPR-operand FMA pairs (measured in profiles/r2_als).
+template <int LDS_BCAST>
 __global__ __launch_bounds__(256) void als_chol_solve_kernel(const float* __restrict__ A, const float* __restrict__ rhs,
                                                             int f, long m, float* __restrict__ X,
                                                             int* __restrict__ info) {
-  const int lane = threadIdx.x & 63;
+  __shared__ __attribute__((aligned(16))) float scol[4][kMaxF];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long r = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (r >= m) return;  // wave-uniform
   float a[kMaxF];
   const float* Ar = A + r * (long)f * f + (long)lane * f;
+  if ((f & 3) == 0) {
 #pragma unroll
-  for (int k = 0; k < kMaxF; ++k) a[k] = lane < f ? (k < f ? Ar[k] : 0.f) : (k == lane ? 1.f : 0.f);
+    for (int k = 0; k < kMaxF; k += 4) {
+      if (lane < f && k < f) {
+        const float4 v = *(const float4*)(Ar + k);
+        a[k] = v.x; a[k + 1] = v.y; a[k + 2] = v.z; a[k + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[k + q] = k + q == lane ? 1.f : 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kMaxF; ++k) a[k] = lane < f ? (k < f ? Ar[k] : 0.f) : (k == lane ? 1.f : 0.f);
+  }
   float b = lane < f ? rhs[r * (long)f + lane] : 0.f;
   int bad = 0;
+  float* col = scol[wv];
 #pragma unroll
   for (int j = 0; j < kMaxF; ++j) {
     float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), j));
@@ -178,10 +197,20 @@ __global__ __launch_bounds__(256) void als_chol_solve_kernel(const float* __rest
     }
     const float sq = sqrtf(d), inv = 1.f / sq;
     a[j] = lane == j ? sq : a[j] * inv;  // column j of L (rows > j); the diagonal
+    if constexpr (LDS_BCAST) {
+      col[lane] = a[j];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int k = j + 1; k < kMaxF; ++k) {
-      const float lk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), k));
-      a[k] = fmaf(-a[j], lk, a[k]);  // row `lane`, column k (only k <= lane is ever read)
+      for (int k = j + 1; k < kMaxF; ++k) a[k] = fmaf(-a[j], col[k], a[k]);  // row `lane`, column k
+      __builtin_amdgcn_wave_barrier();  // every lane read col before the next column overwrites it
+    } else {
+#pragma unroll
+      for (int k = j + 1; k < kMaxF; ++k) {
+        const float lk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a[j]), k));
+        a[k] = fmaf(-a[j], lk, a[k]);  // row `lane`, column k (only k <= lane is ever read)
+      }
     }
   }
   // L y = b
@@ -237,10 +266,14 @@ HARP_EXPORT int harp_als_normal_f64(const long* crow, const long* cols, const do
 
 // X [m, f] = A [m, f, f]^-1 rhs [m, f] for SPD A (fp32, f <= 64; one wave per system);
 // info[r] = 1 marks a non-positive pivot (that row's X is not a solution)
+// variant 0: LDS column broadcast (default), 1: v_readlane broadcast
 HARP_EXPORT int harp_als_chol_solve_f32(const float* A, const float* rhs, int f, long m, float* X, int* info,
-                                        hipStream_t s) {
+                                        int variant, hipStream_t s) {
   if (m <= 0) return HARP_OK;
-  if (f <= 0 || f > kMaxF || !A || !rhs || !X || !info || m > 0x7fffffffL / 4) return HARP_EBADARG;
-  als_chol_solve_kernel<<<dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s>>>(A, rhs, f, m, X, info);
+  if (f <= 0 || f > kMaxF || !A || !rhs || !X || !info || m > 0x7fffffffL / 4 || variant < 0 || variant > 1)
+    return HARP_EBADARG;
+  const dim3 g((unsigned)((m + 3) / 4)), bl(256);
+  if (variant == 0) als_chol_solve_kernel<1><<<g, bl, 0, s>>>(A, rhs, f, m, X, info);
+  else als_chol_solve_kernel<0><<<g, bl, 0, s>>>(A, rhs, f, m, X, info);
   return harp_launch_status();
 }

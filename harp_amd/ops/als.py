@@ -16,7 +16,8 @@ _lib.register({
     for name, ct in (("harp_als_normal_f32", _lib.c_float), ("harp_als_normal_f64", _lib.c_double))
 })
 _lib.register({"harp_als_chol_solve_f32": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_long, _lib.c_void_p,
-                                           _lib.c_void_p, _lib.c_void_p]})
+                                           _lib.c_void_p, _lib.c_int, _lib.c_void_p]})
+CHOL_VARIANT = 0  # 0: LDS column broadcast, 1: v_readlane broadcast (profiles/r2_als)
 
 
 def available(t: torch.Tensor) -> bool:
@@ -53,7 +54,8 @@ def normal_equations(crow: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     _lib.check(st, "als_normal")
 
 
-def chol_solve(A: torch.Tensor, rhs: torch.Tensor, X: torch.Tensor, info: torch.Tensor) -> None:
+def chol_solve(A: torch.Tensor, rhs: torch.Tensor, X: torch.Tensor, info: torch.Tensor,
+               variant: int | None = None) -> None:
     """X[r] = A[r]^-1 rhs[r] for a batch of SPD fp32 systems (f <= 64) on the GPU: one wave
     per system, Cholesky in registers (csrc/als.hip als_chol_solve_kernel); info[r] = 1
     marks a non-positive pivot."""
@@ -62,5 +64,6 @@ def chol_solve(A: torch.Tensor, rhs: torch.Tensor, X: torch.Tensor, info: torch.
     assert X.shape == (m, f) and info.shape == (m,) and info.dtype == torch.int32
     for t in (A, rhs, X, info):
         assert t.is_contiguous() and t.device == A.device
+    v = CHOL_VARIANT if variant is None else variant
     _lib.check(_lib.kernels().harp_als_chol_solve_f32(A.data_ptr(), rhs.data_ptr(), f, m, X.data_ptr(),
-                                                      info.data_ptr(), _lib.stream_ptr(A.device)), "als_chol_solve")
+                                                      info.data_ptr(), v, _lib.stream_ptr(A.device)), "als_chol_solve")

@@ -44,6 +44,9 @@ def main():
                                                           X=X, info=info))
     out["build_only_ms"] = t(lambda: OA.normal_equations(crow, cols, vals, F, G, True, 1.0, 0.1, False, A, rhs, 0))
     out["ratings_in_block"] = int(crow[m] - crow[0])
+    OA.normal_equations(crow, cols, vals, F, G, True, 1.0, 0.1, False, A, rhs, 0)
+    for v in (0, 1):
+        out[f"wave_solve_v{v}_ms"] = t(lambda: OA.chol_solve(A, rhs, X, info, variant=v))
     print(json.dumps(out), flush=True)
 
 
