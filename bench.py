@@ -11,6 +11,11 @@ ranks), lower is better. One timed step = one full iteration of the reference's 
 the 1e4 x 112 fp32 partial sums (``--strategy``: allreduce, or the reference's headline
 regroup -> average at owner -> allgather), normalize, centroid operand prepare.
 
+Nested ``pca`` / ``lda`` records (on GPUs; ``--extras off`` skips them): BASELINE configs 4
+and 5 -- one PCA correlation pass over N = 1e8 x d = 1000 (MFMA SYRK partial result +
+allreduce + fp64 eig) and LDA-CGS over 1M docs x 1M vocab x 1000 topics with the push-pull
+collective, each split over the ranks and bounded by ``--extras-timeout``.
+
 MF-SGD (nested ``sgd`` record): 480,189 x 17,770, 100,480,507 synthetic ratings, rank
 128, H split into 2 slices per rank that rotate around the ring (model rotation); epochs
 timed after warmup; updates/sec = ratings trained / epoch time
@@ -61,6 +66,18 @@ def parse_args(argv=None):
     ap.add_argument("--sgd-timeout", type=float, default=240.0,
                     help="wall-clock bound (s) on the nested MF-SGD record; past it rank 0 prints the "
                          "K-means line with an sgd error and every rank exits")
+    ap.add_argument("--extras", choices=("auto", "on", "off"), default="auto",
+                    help="nested PCA (BASELINE config 4) and LDA (config 5) records (auto: on GPUs)")
+    ap.add_argument("--pca-n", type=float, default=1e8)
+    ap.add_argument("--pca-d", type=int, default=1000)
+    ap.add_argument("--pca-steps", type=int, default=3)
+    ap.add_argument("--lda-docs", type=float, default=1e6)
+    ap.add_argument("--lda-vocab", type=float, default=1e6)
+    ap.add_argument("--lda-topics", type=int, default=1000)
+    ap.add_argument("--lda-len", type=int, default=100)
+    ap.add_argument("--lda-iters", type=int, default=3)
+    ap.add_argument("--lda-strategy", choices=("push_pull", "rotation"), default="push_pull")
+    ap.add_argument("--extras-timeout", type=float, default=300.0, help="wall-clock bound (s) per nested record")
     ap.add_argument("--metrics-jsonl", default="", help="per-iteration phase/bytes records (JSONL)")
     return ap.parse_args(argv)
 
@@ -210,6 +227,91 @@ def bench_sgd(args, comm, torch):
     }
 
 
+# ----------------------------------------------------------------------------- PCA (config 4)
+def bench_pca(args, comm, torch):
+    """One PCA / correlation pass per step over N x d synthetic U[0,1) samples split over
+    the ranks: MFMA SYRK partial result (G = [X 1]^T [X 1], upper tiles), one allreduce,
+    fp64 correlation + eigenvalues (PCADaalCollectiveMapper.java:121-147)."""
+    from harp_amd.models.common import reduce_partials
+    from harp_amd.ops import linalg as LA
+
+    P, r = comm.world_size, comm.rank
+    N, d = int(args.pca_n), args.pca_d
+    n = N // P + (1 if r < N % P else 0)
+    fm = LA.FeatureMajor.uniform(n, d, 0.0, 1.0, seed=11 + r, device=comm.device)
+
+    def one_pass():
+        G = LA.syrk_t(fm)
+        Gs = LA.symmetrize_upper(reduce_partials(comm, {"g": G}, dtype=torch.float32)["g"]).double()
+        cnt = Gs[d, d]
+        mean = Gs[:d, d] / cnt
+        cov = (Gs[:d, :d] - cnt * torch.outer(mean, mean)) / (cnt - 1)
+        sd = torch.diagonal(cov).sqrt()
+        return torch.linalg.eigvalsh(cov / torch.outer(sd, sd))
+
+    one_pass()
+    sync(comm, torch)
+    t0 = time.perf_counter()
+    for _ in range(args.pca_steps):
+        ev = one_pass()
+    sync(comm, torch)
+    dt = reduce_max(comm, torch, time.perf_counter() - t0) / args.pca_steps
+    s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+    s.record()
+    LA.syrk_t(fm)
+    e.record()
+    e.synchronize()
+    syrk_s = reduce_max(comm, torch, s.elapsed_time(e) / 1e3)
+    del fm
+    return {"metric": "PCA correlation pass s/pass (N x d, MFMA SYRK + allreduce + fp64 eig)", "s_per_pass": round(dt, 6),
+            "syrk_s": round(syrk_s, 6), "N": N, "d": d, "steps": args.pca_steps,
+            "gram_equiv_tflops": round(2.0 * N * d * d / P / syrk_s / 1e12, 1),
+            "max_eigenvalue": round(float(ev.max()), 6), "dtype": "bf16 in / fp32 acc / fp64 finalize",
+            "data": "synthetic U[0,1) generated on device", "scaling": "strong"}
+
+
+# ----------------------------------------------------------------------------- LDA (config 5)
+def bench_lda(args, comm, torch):
+    """LDA collapsed Gibbs sweeps over a synthetic corpus of docs x len tokens (vocab
+    words, topics topics); push-pull parameter-server collective by default
+    (LDAMPCollectiveMapper.java / contrib LDAMapperDyn.java push :380 / pull :429)."""
+    from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, LDAPushPullMapper, synthetic_corpus
+    from harp_amd.runtime.mapper import KeyValReader
+
+    nd, V, K = int(args.lda_docs), int(args.lda_vocab), args.lda_topics
+    t0 = time.perf_counter()
+    toks = synthetic_corpus(nd, V, 1000, args.lda_len, seed=3, device=comm.device)
+    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=1 + args.lda_iters)
+    cls = LDAPushPullMapper if args.lda_strategy == "push_pull" else LDACollectiveMapper
+    m = cls(comm, cfg, nd, V, toks)
+    m.init_model(KeyValReader([]))
+    del toks
+    setup_s = time.perf_counter() - t0
+    m.iterate(0)
+    if hasattr(m, "rot"):
+        m.rot.wait_all()
+    sync(comm, torch)
+    t0 = time.perf_counter()
+    n = 0
+    for it in range(1, 1 + args.lda_iters):
+        n += m.iterate(it)
+    if hasattr(m, "rot"):
+        m.rot.wait_all()
+    sync(comm, torch)
+    dt = reduce_max(comm, torch, time.perf_counter() - t0)
+    ll = m.log_likelihood(1 + args.lda_iters)
+    nt = torch.tensor([float(n)], dtype=torch.float64, device=comm.device)
+    if comm.world_size > 1:
+        comm.all_reduce(nt)
+    n = float(nt.item())
+    del m
+    return {"metric": f"LDA-CGS sampled tokens/sec ({args.lda_strategy})", "tokens_per_sec": round(n / dt, 1),
+            "s_per_iter": round(dt / args.lda_iters, 6), "iters": args.lda_iters, "warmup": 1,
+            "docs": nd, "vocab": V, "topics": K, "tokens_per_iter": int(n) // args.lda_iters,
+            "loglik_end": ll, "setup_s": round(setup_s, 3), "data": "synthetic corpus generated on device",
+            "scaling": "strong"}
+
+
 # ----------------------------------------------------------------------------- helpers
 class _Reader:
     def __iter__(self):
@@ -219,13 +321,14 @@ class _Reader:
         return 0
 
 
-class _SGDGuard:
-    """Bounds the nested MF-SGD record. If it has not finished after ``timeout_s``, rank 0
-    prints the (already measured) K-means record with ``sgd.error`` and every rank leaves
-    with ``os._exit(0)`` — the process teardown releases any RCCL kernel still waiting on a
+class _NestedGuard:
+    """Bounds one nested record. If it has not finished after ``timeout_s``, rank 0 prints
+    the (already measured) record with ``<name>.error`` and every rank leaves with
+    ``os._exit(0)`` — the process teardown releases any RCCL kernel still waiting on a
     peer. ``cancel()`` returns False when the guard has already fired."""
 
-    def __init__(self, timeout_s: float, rec: dict, rank: int):
+    def __init__(self, timeout_s: float, rec: dict, rank: int, name: str = "sgd"):
+        self.name = name
         import threading
 
         self._lock = threading.Lock()
@@ -241,10 +344,10 @@ class _SGDGuard:
             if self._state != "armed":
                 return
             self._state = "fired"
-        print(f"bench: MF-SGD record exceeded {timeout_s:g} s on rank {self.rank}; leaving", file=sys.stderr,
-              flush=True)
+        print(f"bench: nested {self.name} record exceeded {timeout_s:g} s on rank {self.rank}; leaving",
+              file=sys.stderr, flush=True)
         if self.rank == 0:
-            rec = dict(self.rec, sgd={"error": f"timeout after {timeout_s:g} s"})
+            rec = dict(self.rec, **{self.name: {"error": f"timeout after {timeout_s:g} s"}})
             print(json.dumps(rec), flush=True)
         os._exit(0)
 
@@ -255,6 +358,19 @@ class _SGDGuard:
             self._state = "done"
         self._t.cancel()
         return True
+
+
+def _nested(rec, name, fn, timeout_s, args, comm, torch):
+    """rec[name] = fn(...) under a wall-clock guard; a failure is reported inside the
+    record, never at the cost of the headline line."""
+    guard = _NestedGuard(timeout_s, rec, comm.rank, name)
+    try:
+        rec[name] = fn(args, comm, torch)
+    except Exception as e:  # noqa: BLE001
+        rec[name] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        print(f"bench: nested {name} record failed on rank {comm.rank}: {e!r}", file=sys.stderr)
+    if not guard.cancel():
+        time.sleep(3600)  # the guard is printing / exiting this process
 
 
 def sync(comm, torch):
@@ -310,14 +426,13 @@ def run(args) -> int:
         # the nested record must never cost the headline line: a failure is reported inside
         # it, and a hang (e.g. a stuck RCCL peer in the rotation ring, which no Python
         # exception interrupts) is bounded by a per-rank wall-clock guard
-        guard = _SGDGuard(args.sgd_timeout, rec, comm.rank)
-        try:
-            rec["sgd"] = bench_sgd(args, comm, torch)
-        except Exception as e:  # noqa: BLE001
-            rec["sgd"] = {"error": f"{type(e).__name__}: {e}"[:500]}
-            print(f"bench: MF-SGD record failed on rank {comm.rank}: {e!r}", file=sys.stderr)
-        if not guard.cancel():
-            time.sleep(3600)  # the guard is printing / exiting this process
+        _nested(rec, "sgd", bench_sgd, args.sgd_timeout, args, comm, torch)
+    want_extras = args.extras == "on" or (args.extras == "auto" and comm.device.type == "cuda")
+    if want_extras:
+        for name, fn in (("pca", bench_pca), ("lda", bench_lda)):
+            if comm.device.type == "cuda":
+                torch.cuda.empty_cache()
+            _nested(rec, name, fn, args.extras_timeout, args, comm, torch)
     if comm.rank == 0:
         print(json.dumps(rec), flush=True)
     shutdown()
