@@ -77,7 +77,7 @@ def parse_args(argv=None):
     ap.add_argument("--lda-len", type=int, default=100)
     ap.add_argument("--lda-iters", type=int, default=3)
     ap.add_argument("--lda-strategy", choices=("push_pull", "rotation"), default="push_pull")
-    ap.add_argument("--extras-timeout", type=float, default=300.0, help="wall-clock bound (s) per nested record")
+    ap.add_argument("--extras-timeout", type=float, default=180.0, help="wall-clock bound (s) per nested record")
     ap.add_argument("--metrics-jsonl", default="", help="per-iteration phase/bytes records (JSONL)")
     return ap.parse_args(argv)
 
