@@ -41,6 +41,7 @@ class LDAConfig:
     block_words: int = 4096   # push/pull strategy: words per model partition
     sparse_comm: str = "off"  # push/pull: "on" moves nonzero counts only (profiles/r2_apps: the torch
                               # nonzero / index_add compaction costs 0.15-0.26 s per iteration)
+    local_server: bool = True  # push-pull, one worker owning every touched block: sample in the table
     rotate_codec: str = "auto"  # rotation: "on" sends word-topic slabs as sparse payloads (ops/slabcodec),
                                 # "auto" when that payload is at most half the dense slab, "off" dense
     checkpoint_dir: str = ""  # .hpt checkpoints (token topics, doc-topic, resident word slices)
@@ -406,18 +407,25 @@ class LDAPushPullMapper(LDACollectiveMapper):
         nblocks = math.ceil(self.vocab / B)
         owned = list(range(me, nblocks, P))
         # distributed global table: owned word blocks, one packed [n_owned, B, K_pad] slab
-        self.glob = PackedTable(owned, torch.zeros((len(owned), B, self.Kp), dtype=torch.int32, device=dev),
-                                table_id=1, combiner=self.sum)
         # one persistent buffer of the blocks this worker's tokens touch: pulled into, sampled
         # on in place, turned into the count delta and pushed back (cached comm plans)
         nneed = len(self.need)
         self.pull_buf = slab.view(nneed, B, self.Kp) if nneed else torch.zeros((0, B, self.Kp), dtype=torch.int32,
                                                                               device=dev)
-        self.before = torch.empty_like(self.pull_buf)
+        # a single worker that owns every block its tokens touch, in the same order: its
+        # server table IS the sampled slab, so pull (a copy), the before-snapshot, the delta
+        # and push (an add back) are four full-model passes that leave the same counts;
+        # the table aliases the slab and they are skipped (cfg.local_server=False keeps them)
+        self.local_server = P == 1 and cfg.local_server and self.need == owned
+        gbuf = self.pull_buf if self.local_server else torch.zeros((len(owned), B, self.Kp), dtype=torch.int32,
+                                                                   device=dev)
+        self.glob = PackedTable(owned, gbuf, table_id=1, combiner=self.sum)
+        self.before = None if self.local_server else torch.empty_like(self.pull_buf)
         self.want_pt = PackedTable(self.need, self.pull_buf, table_id=3, combiner=self.sum)
         for t in (self.glob, self.want_pt):
             t.static_layout = True
-        self._push_delta()  # initial counts = a delta against an all-zero model
+        if not self.local_server:
+            self._push_delta()  # initial counts = a delta against an all-zero model
         self.vbeta = self.vocab * cfg.beta
 
     def _sparse(self) -> bool:
@@ -444,6 +452,14 @@ class LDAPushPullMapper(LDACollectiveMapper):
 
     def iterate(self, it: int) -> int:
         cfg = self.cfg
+        if self.local_server:
+            n = self.tz.numel()
+            if n:
+                d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, self.pull_buf.view(-1, self.Kp),
+                                 self.nk, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
+                                 (cfg.seed << 40) ^ (it << 20) ^ 0x5A, self.doc_index)
+                self.nk += d
+            return n
         slab = self._pull()
         self.before.copy_(self.pull_buf)
         before = self.before.view(-1, self.Kp)
@@ -487,7 +503,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
             if self.cfg.print_interval and ((it + 1) % self.cfg.print_interval == 0 or it + 1 == self.cfg.iterations):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
             self._after_iteration(it)
-        self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start}
+        self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start,
+                       "local_server": self.local_server}
 
     def _state_tables(self, it: int) -> dict:
         from ..utils.checkpoint import blob_table, tensor_table

@@ -71,6 +71,17 @@ def test_lda_push_pull(corpus, P):
     assert abs(ll[-1] - rot) / abs(rot) < 0.08
 
 
+def test_lda_push_pull_local_server_equals_general_path(corpus):
+    """One worker owning every touched block samples in its server table; the general
+    pull / snapshot / delta / push path must give the same counts and likelihoods."""
+    base = dict(num_topics=10, alpha=0.1, beta=0.01, iterations=6, print_interval=2, block_words=64)
+    fast = launch(_pp_job, 1, args=(LDAConfig(local_server=True, **base), 300, 400, corpus))[0]
+    slow = launch(_pp_job, 1, args=(LDAConfig(local_server=False, **base), 300, 400, corpus))[0]
+    assert fast[0]["local_server"] and not slow[0]["local_server"]
+    assert fast[0]["loglik"] == slow[0]["loglik"]
+    assert torch.equal(fast[1], slow[1]) and torch.equal(fast[1], fast[2])
+
+
 def test_doc_index_build_and_sync():
     g = torch.Generator().manual_seed(0)
     tdoc = torch.randint(0, 50, (2000,), generator=g, dtype=torch.int32)
