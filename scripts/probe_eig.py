@@ -32,6 +32,13 @@ def main():
     out["gpu_to_cpu_fp64_eigvalsh_ms"] = timeit(lambda: torch.linalg.eigvalsh(Cg.cpu()))
     out["gpu_fp64_eigh_ms"] = timeit(lambda: torch.linalg.eigh(Cg))
     out["cpu_fp64_eigh_ms"] = timeit(lambda: torch.linalg.eigh(C), cuda=False)
+    for lib in ("magma", "cusolver"):
+        try:
+            torch.backends.cuda.preferred_linalg_library(lib)
+            out[f"gpu_fp64_eigvalsh_{lib}_ms"] = timeit(lambda: torch.linalg.eigvalsh(Cg))
+        except Exception as e:  # noqa: BLE001
+            out[f"gpu_fp64_eigvalsh_{lib}_ms"] = f"{type(e).__name__}: {e}"[:120]
+    torch.backends.cuda.preferred_linalg_library("default")
     ref = torch.linalg.eigvalsh(C)
     out["fp32_max_rel_err"] = float(((torch.linalg.eigvalsh(Cg.float()).double().cpu() - ref).abs() / ref.abs().max()).max())
     print(json.dumps(out), flush=True)
