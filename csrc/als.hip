@@ -17,6 +17,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunk = 32;   // rated rows staged per LDS trip
 constexpr int kMaxF = 64;    // f x f entries = 4096 = 16 per thread
+int ALS_BUILD_DMA = 1;       // host switch for A/B (harp_als_set_build_dma)
 
 
 // A[r] = sum_j aw_j F[c_j] F[c_j]^T + G + lam_r I ;  rhs[r] = sum_j bw_j F[c_j]
@@ -150,6 +151,90 @@ __global__ __launch_bounds__(kThreads) void als_normal_kernel(const long* __rest
   if (tid < f) rhs[r * (long)f + tid] = racc;
 }
 
+// Build-only fp32 variant (f % 4 == 0): the rated factor rows of chunk c+1 stream into the
+// other half of a double-buffered LDS slab by LDS-DMA (global_load_lds, 16 B per lane,
+// 4 rows of 256 B per wave-instruction) while chunk c is accumulated, so the gather latency
+// no longer sits between the chunk barriers. Columns past f read a zero source.
+__device__ __attribute__((aligned(16))) float g_als_zero[4] = {0.f, 0.f, 0.f, 0.f};
+
+__global__ __launch_bounds__(kThreads) void als_build_dma_kernel(const long* __restrict__ crow,
+                                                                 const long* __restrict__ cols,
+                                                                 const float* __restrict__ vals,
+                                                                 const float* __restrict__ F, int f,
+                                                                 const float* __restrict__ G, int implicit,
+                                                                 float alpha, float lam, int scale_lam,
+                                                                 float* __restrict__ A, float* __restrict__ rhs,
+                                                                 long row0) {
+  __shared__ __attribute__((aligned(16))) float sF[2][kChunk][kMaxF];
+  __shared__ float sa[2][kChunk], sb[2][kChunk];
+  const long r = blockIdx.x;
+  const long s = crow[row0 + r], e = crow[row0 + r + 1];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int ti = (tid >> 4) * 4, tk = (tid & 15) * 4;
+  float acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = 0.f;
+  float racc = 0.f;
+  auto stage = [&](int buf, long j0) {
+    const int m = (int)((e - j0) < kChunk ? (e - j0) : kChunk);
+    // kChunk rows x 256 B = 8 one-KiB DMA pieces; wave wv issues pieces wv and wv + 4
+#pragma unroll
+    for (int q = wv; q < kChunk / 4; q += kThreads / 64) {
+      const int jj = q * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+      const float* src = (jj < m && c4 < f) ? F + cols[j0 + jj] * (long)f + c4 : g_als_zero;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)&sF[buf][q * 4][0], 16, 0, 0);
+    }
+    if (tid < m) {
+      const float v = vals[j0 + tid];
+      sa[buf][tid] = implicit ? alpha * v : 1.f;
+      sb[buf][tid] = implicit ? (v > 0.f ? 1.f + alpha * v : 0.f) : v;
+    }
+  };
+  int buf = 0;
+  if (s < e) stage(0, s);
+  for (long j0 = s; j0 < e; j0 += kChunk, buf ^= 1) {
+    const int m = (int)((e - j0) < kChunk ? (e - j0) : kChunk);
+    // this wave's DMA pieces of chunk j0 landed; the barrier makes every wave's visible and
+    // ends every wave's reads of the other buffer (the next prefetch target)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (j0 + kChunk < e) stage(buf ^ 1, j0 + kChunk);
+    for (int jj = 0; jj < m; ++jj) {
+      const float w = sa[buf][jj];
+      float a[4], b[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        a[x] = w * sF[buf][jj][ti + x];
+        b[x] = sF[buf][jj][tk + x];
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * b[y];
+    }
+    if (tid < f)
+      for (int jj = 0; jj < m; ++jj) racc += sb[buf][jj] * sF[buf][jj][tid];
+  }
+  const long n_r = e - s;
+  const float lr = scale_lam ? lam * (float)(n_r > 0 ? n_r : 1) : lam;
+  float* Ar = A + r * (long)f * f;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int i = ti + x, k = tk + y;
+      if (i < f && k < f) {
+        float a = acc[x][y] + (G ? G[i * f + k] : 0.f);
+        if (i == k) a += lr;
+        Ar[i * f + k] = a;
+      }
+    }
+  if (tid < f) rhs[r * (long)f + tid] = racc;
+}
+
 // Batched SPD solve A x = rhs (fp32, f <= 64), ONE WAVE PER SYSTEM and no barriers: lane i
 // holds row i of A (zero-padded to 64, identity rows past f) in 64 VGPRs. Right-looking
 // Cholesky over the unrolled columns j: the pivot and the column entries L[k][j] are wave
@@ -254,6 +339,13 @@ int launch(const long* crow, const long* cols, const T* vals, const T* F, int f,
 HARP_EXPORT int harp_als_normal_f32(const long* crow, const long* cols, const float* vals, const float* F, int f,
                                     const float* G, int implicit, float alpha, float lam, int scale_lam, float* A,
                                     float* rhs, long row0, long nrows, float* X, int* info, hipStream_t s) {
+  if (!X && f % 4 == 0 && ALS_BUILD_DMA) {
+    if (nrows <= 0) return HARP_OK;
+    if (f <= 0 || f > kMaxF || !A || !rhs || nrows * (long)kThreads > 0xffffffffL) return HARP_EBADARG;
+    als_build_dma_kernel<<<dim3((unsigned)nrows), dim3(kThreads), 0, s>>>(crow, cols, vals, F, f, G, implicit, alpha,
+                                                                        lam, scale_lam, A, rhs, row0);
+    return harp_launch_status();
+  }
   return launch<float>(crow, cols, vals, F, f, G, implicit, alpha, lam, scale_lam, A, rhs, row0, nrows, X, info, s);
 }
 
@@ -276,4 +368,10 @@ HARP_EXPORT int harp_als_chol_solve_f32(const float* A, const float* rhs, int f,
   if (variant == 0) als_chol_solve_kernel<1><<<g, bl, 0, s>>>(A, rhs, f, m, X, info);
   else als_chol_solve_kernel<0><<<g, bl, 0, s>>>(A, rhs, f, m, X, info);
   return harp_launch_status();
+}
+
+// A/B switch for the LDS-DMA build variant (1 = on, the default)
+HARP_EXPORT int harp_als_set_build_dma(int on) {
+  ALS_BUILD_DMA = on ? 1 : 0;
+  return HARP_OK;
 }

@@ -42,7 +42,17 @@ def main():
     out = {"rows": m, "f": f}
     out["fused_solve_ms"] = t(lambda: OA.normal_equations(crow, cols, vals, F, G, True, 1.0, 0.1, False, None, None, 0,
                                                           X=X, info=info))
-    out["build_only_ms"] = t(lambda: OA.normal_equations(crow, cols, vals, F, G, True, 1.0, 0.1, False, A, rhs, 0))
+    from harp_amd.ops import _lib
+    _lib.register({"harp_als_set_build_dma": [_lib.c_int]})
+    lib = _lib.kernels()
+    ref = {}
+    for dma in (0, 1):
+        lib.harp_als_set_build_dma(dma)
+        out[f"build_only_dma{dma}_ms"] = t(lambda: OA.normal_equations(crow, cols, vals, F, G, True, 1.0, 0.1, False,
+                                                                       A, rhs, 0))
+        ref[dma] = (A[:1000].clone(), rhs[:1000].clone())
+    out["dma_max_abs_diff_A"] = float((ref[0][0] - ref[1][0]).abs().max())
+    out["dma_max_abs_diff_rhs"] = float((ref[0][1] - ref[1][1]).abs().max())
     out["ratings_in_block"] = int(crow[m] - crow[0])
     OA.normal_equations(crow, cols, vals, F, G, True, 1.0, 0.1, False, A, rhs, 0)
     for v in (0, 1):
