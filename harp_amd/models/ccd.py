@@ -78,9 +78,10 @@ def train_ccd(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
     if carry:
         inv = torch.empty_like(ou)
         inv[ou] = torch.arange(ou.numel(), device=ou.device)
-        i2u = inv[oi].contiguous()   # item-order position k holds user-order element i2u[k]
+        idx_t = torch.int32 if ou.numel() < 2**31 else torch.int64  # int32: half the index bytes per gather
+        i2u = inv[oi].to(idx_t).contiguous()   # item-order position k holds user-order element i2u[k]
         inv[oi] = torch.arange(oi.numel(), device=oi.device)
-        u2i = inv[ou].contiguous()
+        u2i = inv[ou].to(idx_t).contiguous()
         del inv
     del ou, oi
     g = torch.Generator().manual_seed(cfg.seed)
