@@ -157,12 +157,15 @@ def test_bench_spawns_rccl_ranks():
     assert rec["sgd"]["updates_per_sec"] > 0
 
 
-def _lda_rccl(comm, push_pull):
+def _lda_rccl(comm, mode):
     from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, LDAPushPullMapper, synthetic_corpus
     from harp_amd.runtime.mapper import KeyValReader
 
+    push_pull = mode == "push_pull"
     doc, word = synthetic_corpus(400, 900, 8, 60, seed=11)
-    cfg = LDAConfig(num_topics=32, iterations=4, print_interval=4, block_words=128)
+    # rotation_codec: the word-slice slabs cross RCCL as sparse payloads (ops/slabcodec)
+    cfg = LDAConfig(num_topics=32, iterations=4, print_interval=4, block_words=128,
+                    rotate_codec="on" if mode == "rotation_codec" else "off")
     cls = LDAPushPullMapper if push_pull else LDACollectiveMapper
     m = cls(comm, cfg, 400, 900, (doc, word))
     m.run(KeyValReader([]))
@@ -170,21 +173,21 @@ def _lda_rccl(comm, push_pull):
 
 
 @need2
-@pytest.mark.parametrize("push_pull", [False, True])
-def test_lda_over_rccl_conserves_counts_and_learns(push_pull):
+@pytest.mark.parametrize("mode", ["rotation", "rotation_codec", "push_pull"])
+def test_lda_over_rccl_conserves_counts_and_learns(mode):
     """LDA-CGS on device tensors over RCCL (word-slice rotation or the push-pull PS table):
     every token sampled by exactly one rank, topic sums identical on every rank and equal to
     the token count, and the likelihood within a few % of the 1-rank run."""
     P = P_LIST[-1]
-    one = launch(_lda_rccl, 1, args=(push_pull,), backend="nccl", timeout=300)[0]
-    res = launch(_lda_rccl, P, args=(push_pull,), backend="nccl", timeout=300)
+    one = launch(_lda_rccl, 1, args=(mode,), backend="nccl", timeout=300)[0]
+    res = launch(_lda_rccl, P, args=(mode,), backend="nccl", timeout=300)
     assert sum(r["tokens"] for r in res) == one["total"]
     for r in res:
         assert torch.equal(r["nk"], res[0]["nk"]) and int(r["nk"].sum()) == one["total"]
     # push-pull samples every rank against one snapshot per sweep (bulk-synchronous
     # staleness): on this small corpus it trails one rank by ~5 % after 4 sweeps (gloo
     # rehearsal at P = 2); rotation by < 1 %
-    assert res[0]["loglik"] == pytest.approx(one["loglik"], rel=0.15 if push_pull else 0.05)  # P up to 8
+    assert res[0]["loglik"] == pytest.approx(one["loglik"], rel=0.15 if mode == "push_pull" else 0.05)  # P up to 8
 
 
 def _ccd_rccl(comm, mode):
