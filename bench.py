@@ -21,6 +21,11 @@ MF-SGD (nested ``sgd`` record): 480,189 x 17,770, 100,480,507 synthetic ratings,
 timed after warmup; updates/sec = ratings trained / epoch time
 (SGDCollectiveMapper.java:294-298).
 
+Every record reports the mean (wall clock around the timed loop, max over ranks) and the
+median / min / max of per-step times (HIP events at step boundaries, each step's max over
+ranks) -- BASELINE.md's protocol; nested records time >= 10 iterations by default. A nested
+record that hangs past its guard leaves the headline line printed and exits 124.
+
 Usage:
   python bench.py [--gpus N] [--steps K] [--warmup W]
   With N > 1 and no torchrun environment, the parent process spawns the N ranks itself
@@ -60,7 +65,7 @@ def parse_args(argv=None):
     ap.add_argument("--sgd-items", type=int, default=17770)
     ap.add_argument("--sgd-ratings", type=int, default=100480507)
     ap.add_argument("--sgd-rank", type=int, default=128)
-    ap.add_argument("--sgd-epochs", type=int, default=5)
+    ap.add_argument("--sgd-epochs", type=int, default=10)
     ap.add_argument("--sgd-warmup", type=int, default=1)
     ap.add_argument("--sgd-slices", type=int, default=2, help="H slices per rank (rotation pipeline depth)")
     ap.add_argument("--sgd-timeout", type=float, default=240.0,
@@ -70,13 +75,16 @@ def parse_args(argv=None):
                     help="nested PCA (BASELINE config 4) and LDA (config 5) records (auto: on GPUs)")
     ap.add_argument("--pca-n", type=float, default=1e8)
     ap.add_argument("--pca-d", type=int, default=1000)
-    ap.add_argument("--pca-steps", type=int, default=3)
+    ap.add_argument("--pca-steps", type=int, default=10)
     ap.add_argument("--lda-docs", type=float, default=1e6)
     ap.add_argument("--lda-vocab", type=float, default=1e6)
     ap.add_argument("--lda-topics", type=int, default=1000)
     ap.add_argument("--lda-len", type=int, default=100)
-    ap.add_argument("--lda-iters", type=int, default=3)
+    ap.add_argument("--lda-iters", type=int, default=10)
     ap.add_argument("--lda-strategy", choices=("push_pull", "rotation"), default="push_pull")
+    ap.add_argument("--lda-local-server", choices=("auto", "off"), default="auto",
+                    help="push-pull at P=1: auto aliases the server table to the sampled slab; off runs the "
+                         "pull / delta / push passes (with auto, a 1-rank run also records the off case)")
     ap.add_argument("--extras-timeout", type=float, default=180.0, help="wall-clock bound (s) per nested record")
     ap.add_argument("--metrics-jsonl", default="", help="per-iteration phase/bytes records (JSONL)")
     return ap.parse_args(argv)
@@ -136,11 +144,15 @@ def bench_kmeans(args, comm, torch):
     sync(comm, torch)
     m.metrics.timer.reset()
     m.metrics.collectives.clear()
+    clock = StepClock(comm, torch)
     t0 = time.perf_counter()
+    clock.mark()
     for it in range(args.steps):
         m.step(args.warmup + it)
+        clock.mark()
     sync(comm, torch)
     elapsed = time.perf_counter() - t0
+    step_s = clock.durations()
     phases = m.metrics.timer.flush()
     coll = m.metrics.summary()["collectives"]
     elapsed = reduce_max(comm, torch, elapsed)
@@ -169,6 +181,8 @@ def bench_kmeans(args, comm, torch):
         "data": "synthetic U[0,1000) points generated on device; random-init centroids",
         "config": {"model": f"kmeans-{args.strategy}", "N": N, "d": args.dim, "K": args.centroids,
                    "global_batch": N, "seq_len": None, "parallelism": f"dp{P}"},
+        "median_s_per_iter": round(step_stats(step_s)["median"], 6),
+        "step_s": step_stats(step_s),
         "points_per_sec": round(N / sec_per_iter, 1),
         "effective_tflops": round(flops / sec_per_iter / 1e12, 1),
         "phase_ms_per_iter": {k: round(v / args.steps * 1e3, 3) for k, v in phases.items()},
@@ -183,11 +197,17 @@ def bench_kmeans(args, comm, torch):
     return rec
 
 
+def _window_bytes(metrics, kinds=None) -> int:
+    """Bytes of the collectives a mapper recorded (optionally of the given kinds)."""
+    return sum(c["bytes"] for c in metrics.collectives if kinds is None or c["kind"] in kinds)
+
+
 # ----------------------------------------------------------------------------- MF-SGD
 def bench_sgd(args, comm, torch):
     from harp_amd.models.sgd_mf import SGDCollectiveMapper, SGDConfig, synthetic_ratings
 
     dev = comm.device
+    P = comm.world_size
     t0 = time.perf_counter()
     u, i, v = synthetic_ratings(args.sgd_users, args.sgd_items, args.sgd_ratings, seed=7, device=dev)
     cfg = SGDConfig(rank=args.sgd_rank, epochs=args.sgd_warmup + args.sgd_epochs, test_every=0,
@@ -200,24 +220,37 @@ def bench_sgd(args, comm, torch):
         m.train_epoch(ep)
     m.rot.wait_all()
     sync(comm, torch)
+    m.metrics.resolve()
+    m.metrics.collectives.clear()
+    clock = StepClock(comm, torch)
     t0 = time.perf_counter()
     n = 0
+    clock.mark()
     for ep in range(args.sgd_warmup, args.sgd_warmup + args.sgd_epochs):
         n += m.train_epoch(ep)
+        clock.mark()
     m.rot.wait_all()
     sync(comm, torch)
     dt = reduce_max(comm, torch, time.perf_counter() - t0)
+    ep_s = clock.durations()
+    rot_bytes = _window_bytes(m.metrics, ("rotate_wait",))
     nt = torch.tensor([float(n)], dtype=torch.float64, device=dev)
-    if comm.world_size > 1:
+    if P > 1:
         comm.all_reduce(nt)
     n = float(nt.item())
     train_rmse, _ = m._eval_ring(args.sgd_warmup + args.sgd_epochs - 1)
+    st = step_stats(ep_s)
     return {
         "metric": "MF-SGD updates/sec (Netflix-shape synthetic, model rotation)",
         "updates_per_sec": round(n / dt, 1),
+        "median_updates_per_sec": round(n / args.sgd_epochs / st["median"], 1) if st["median"] > 0 else None,
         "s_per_epoch": round(dt / args.sgd_epochs, 6),
+        "epoch_s": st,
         "epochs": args.sgd_epochs,
         "warmup": args.sgd_warmup,
+        "n_gpus": P,
+        "sync_bytes_per_iter": int(rot_bytes / max(args.sgd_epochs, 1)),
+        "rotation_strides": [s.stride for s in m.schedules],
         "train_rmse": round(train_rmse, 6),
         "users": args.sgd_users, "items": args.sgd_items, "ratings": args.sgd_ratings, "rank": args.sgd_rank,
         "slices_per_rank": cfg.num_slices,
@@ -231,57 +264,81 @@ def bench_sgd(args, comm, torch):
 def bench_pca(args, comm, torch):
     """One PCA / correlation pass per step over N x d synthetic U[0,1) samples split over
     the ranks: MFMA SYRK partial result (G = [X 1]^T [X 1], upper tiles), one allreduce,
-    fp64 correlation + eigenvalues (PCADaalCollectiveMapper.java:121-147)."""
+    fp64 correlation, eigenvalues on the master then broadcast
+    (PCADaalCollectiveMapper.java:121-147: step 2 runs on the master only). CPU ranks
+    (gloo rehearsal) form the same G with an fp32 matmul."""
     from harp_amd.models.common import reduce_partials
-    from harp_amd.ops import linalg as LA
 
     P, r = comm.world_size, comm.rank
     N, d = int(args.pca_n), args.pca_d
     n = N // P + (1 if r < N % P else 0)
-    fm = LA.FeatureMajor.uniform(n, d, 0.0, 1.0, seed=11 + r, device=comm.device)
+    dev = comm.device
+    if dev.type == "cuda":
+        from harp_amd.ops import linalg as LA
+
+        fm = LA.FeatureMajor.uniform(n, d, 0.0, 1.0, seed=11 + r, device=dev)
+        syrk, upper = (lambda: LA.syrk_t(fm)), LA.symmetrize_upper
+    else:
+        g = torch.Generator().manual_seed(11 + r)
+        Xa = torch.cat([torch.rand((n, d), generator=g), torch.ones((n, 1))], 1)
+        syrk, upper = (lambda: Xa.t() @ Xa), (lambda G: G)
 
     def one_pass():
-        G = LA.syrk_t(fm)
-        Gs = LA.symmetrize_upper(reduce_partials(comm, {"g": G}, dtype=torch.float32)["g"]).double()
+        G = syrk()
+        Gs = upper(reduce_partials(comm, {"g": G}, dtype=torch.float32)["g"])[:d + 1, :d + 1].double()
         cnt = Gs[d, d]
         mean = Gs[:d, d] / cnt
         cov = (Gs[:d, :d] - cnt * torch.outer(mean, mean)) / (cnt - 1)
         sd = torch.diagonal(cov).sqrt()
-        return torch.linalg.eigvalsh(cov / torch.outer(sd, sd))
+        if r == 0:
+            ev = torch.linalg.eigvalsh(cov / torch.outer(sd, sd))
+        else:
+            ev = torch.empty(d, dtype=torch.float64, device=dev)
+        if P > 1:
+            comm.broadcast(ev, 0)
+        return ev, G.numel() * 4
 
     one_pass()
     sync(comm, torch)
+    clock = StepClock(comm, torch)
     t0 = time.perf_counter()
+    clock.mark()
     for _ in range(args.pca_steps):
-        ev = one_pass()
+        ev, gbytes = one_pass()
+        clock.mark()
     sync(comm, torch)
     dt = reduce_max(comm, torch, time.perf_counter() - t0) / args.pca_steps
-    s, e = torch.cuda.Event(True), torch.cuda.Event(True)
-    s.record()
-    LA.syrk_t(fm)
-    e.record()
-    e.synchronize()
-    syrk_s = reduce_max(comm, torch, s.elapsed_time(e) / 1e3)
-    del fm
-    return {"metric": "PCA correlation pass s/pass (N x d, MFMA SYRK + allreduce + fp64 eig)", "s_per_pass": round(dt, 6),
-            "syrk_s": round(syrk_s, 6), "N": N, "d": d, "steps": args.pca_steps,
-            "gram_equiv_tflops": round(2.0 * N * d * d / P / syrk_s / 1e12, 1),
-            "max_eigenvalue": round(float(ev.max()), 6), "dtype": "bf16 in / fp32 acc / fp64 finalize",
+    st = step_stats(clock.durations())
+    sclock = StepClock(comm, torch)  # the SYRK alone (device time on GPUs)
+    sclock.mark()
+    syrk()
+    sclock.mark()
+    sync(comm, torch)
+    syrk_s = sclock.durations()[0]
+    # useful SYRK work: the upper triangle (diagonal included) of the (d+1)^2 Gram of [X 1]
+    # over this rank's rows -- what the kernel must compute, not the full-Gram equivalent
+    flop = float(n) * (d + 1) * (d + 2)
+    sync_bytes = (gbytes + d * 8) if P > 1 else 0
+    return {"metric": "PCA correlation pass s/pass (N x d, MFMA SYRK + allreduce + fp64 eig)",
+            "s_per_pass": round(dt, 6), "median_s_per_pass": round(st["median"], 6), "pass_s": st,
+            "syrk_s": round(syrk_s, 6), "N": N, "d": d, "steps": args.pca_steps, "n_gpus": P,
+            "syrk_tflops": round(flop / syrk_s / 1e12, 1) if syrk_s > 0 else None,
+            "syrk_flop_per_rank": flop, "sync_bytes_per_iter": int(sync_bytes),
+            "max_eigenvalue": round(float(ev.max()), 6),
+            "dtype": "bf16 in / fp32 acc / fp64 finalize" if dev.type == "cuda" else "fp32 (CPU rehearsal)",
             "data": "synthetic U[0,1) generated on device", "scaling": "strong"}
 
 
 # ----------------------------------------------------------------------------- LDA (config 5)
-def bench_lda(args, comm, torch):
-    """LDA collapsed Gibbs sweeps over a synthetic corpus of docs x len tokens (vocab
-    words, topics topics); push-pull parameter-server collective by default
-    (LDAMPCollectiveMapper.java / contrib LDAMapperDyn.java push :380 / pull :429)."""
+def _lda_run(args, comm, torch, local_server: bool, iters: int) -> dict:
     from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, LDAPushPullMapper, synthetic_corpus
     from harp_amd.runtime.mapper import KeyValReader
 
     nd, V, K = int(args.lda_docs), int(args.lda_vocab), args.lda_topics
+    P = comm.world_size
     t0 = time.perf_counter()
     toks = synthetic_corpus(nd, V, 1000, args.lda_len, seed=3, device=comm.device)
-    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=1 + args.lda_iters)
+    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=1 + iters, local_server=local_server)
     cls = LDAPushPullMapper if args.lda_strategy == "push_pull" else LDACollectiveMapper
     m = cls(comm, cfg, nd, V, toks)
     m.init_model(KeyValReader([]))
@@ -291,25 +348,56 @@ def bench_lda(args, comm, torch):
     if hasattr(m, "rot"):
         m.rot.wait_all()
     sync(comm, torch)
+    m.metrics.resolve()
+    m.metrics.collectives.clear()
+    clock = StepClock(comm, torch)
     t0 = time.perf_counter()
     n = 0
-    for it in range(1, 1 + args.lda_iters):
+    clock.mark()
+    for it in range(1, 1 + iters):
         n += m.iterate(it)
+        clock.mark()
     if hasattr(m, "rot"):
         m.rot.wait_all()
     sync(comm, torch)
     dt = reduce_max(comm, torch, time.perf_counter() - t0)
-    ll = m.log_likelihood(1 + args.lda_iters)
+    st = step_stats(clock.durations())
+    coll = _window_bytes(m.metrics)
+    if P > 1:
+        coll += iters * m.Kp * 8  # the topic-sum delta allreduce (fp64) of every iteration
+    ll = m.log_likelihood(1 + iters)
     nt = torch.tensor([float(n)], dtype=torch.float64, device=comm.device)
-    if comm.world_size > 1:
+    if P > 1:
         comm.all_reduce(nt)
     n = float(nt.item())
+    out = {"tokens_per_sec": round(n / dt, 1), "s_per_iter": round(dt / iters, 6),
+           "median_s_per_iter": round(st["median"], 6), "iter_s": st, "iters": iters,
+           "sync_bytes_per_iter": int(coll / max(iters, 1)), "loglik_end": ll, "setup_s": round(setup_s, 3),
+           "local_server": bool(getattr(m, "local_server", False)), "tokens_per_iter": int(n) // iters}
     del m
-    return {"metric": f"LDA-CGS sampled tokens/sec ({args.lda_strategy})", "tokens_per_sec": round(n / dt, 1),
-            "s_per_iter": round(dt / args.lda_iters, 6), "iters": args.lda_iters, "warmup": 1,
-            "docs": nd, "vocab": V, "topics": K, "tokens_per_iter": int(n) // args.lda_iters,
-            "loglik_end": ll, "setup_s": round(setup_s, 3), "data": "synthetic corpus generated on device",
-            "scaling": "strong"}
+    return out
+
+
+def bench_lda(args, comm, torch):
+    """LDA collapsed Gibbs sweeps over a synthetic corpus of docs x len tokens (vocab
+    words, topics topics); push-pull parameter-server collective by default
+    (LDAMPCollectiveMapper.java / contrib LDAMapperDyn.java push :380 / pull :429).
+    At one rank the server table can alias the sampled slab (``local_server``); the
+    record then also carries the same sweep with pull / delta / push running, so the
+    collective's single-GPU cost is on record."""
+    nd, V, K = int(args.lda_docs), int(args.lda_vocab), args.lda_topics
+    local = args.lda_local_server == "auto"
+    rec = {"metric": f"LDA-CGS sampled tokens/sec ({args.lda_strategy})", "n_gpus": comm.world_size,
+           "docs": nd, "vocab": V, "topics": K, "warmup": 1, "data": "synthetic corpus generated on device",
+           "scaling": "strong"}
+    rec.update(_lda_run(args, comm, torch, local, args.lda_iters))
+    if args.lda_strategy == "push_pull" and comm.world_size == 1 and rec["local_server"]:
+        if comm.device.type == "cuda":
+            torch.cuda.empty_cache()
+        off = _lda_run(args, comm, torch, False, args.lda_iters)
+        rec["no_local_server"] = {k: off[k] for k in ("tokens_per_sec", "s_per_iter", "median_s_per_iter",
+                                                       "sync_bytes_per_iter", "loglik_end")}
+    return rec
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -321,11 +409,62 @@ class _Reader:
         return 0
 
 
+class StepClock:
+    """Per-step durations of a timed loop without a host sync inside it: a HIP event is
+    recorded on the current stream at every step boundary (host clock on CPU ranks).
+    :meth:`durations` (after the loop's closing sync) returns each step's max over the
+    ranks -- BASELINE.md's protocol reports the median over >= 10 timed iterations."""
+
+    def __init__(self, comm, torch):
+        self.comm, self.torch = comm, torch
+        self.cuda = comm.device.type == "cuda"
+        self.marks = []
+
+    def mark(self) -> None:
+        if self.cuda:
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append(e)
+        else:
+            self.marks.append(time.perf_counter())
+
+    def durations(self):
+        torch = self.torch
+        if self.cuda:
+            self.marks[-1].synchronize()
+            d = [a.elapsed_time(b) / 1e3 for a, b in zip(self.marks, self.marks[1:])]
+        else:
+            d = [b - a for a, b in zip(self.marks, self.marks[1:])]
+        t = torch.tensor(d, dtype=torch.float64, device=self.comm.device)
+        if self.comm.world_size > 1 and t.numel():
+            import torch.distributed as dist
+
+            self.comm.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.cpu().tolist()
+
+
+def step_stats(d) -> dict:
+    """median / mean / min / max of per-step seconds."""
+    if not d:
+        return {"median": 0.0, "mean": 0.0, "min": 0.0, "max": 0.0, "n": 0}
+    x = sorted(d)
+    k = len(x)
+    med = x[k // 2] if k % 2 else 0.5 * (x[k // 2 - 1] + x[k // 2])
+    return {"median": round(med, 6), "mean": round(sum(x) / k, 6), "min": round(x[0], 6), "max": round(x[-1], 6),
+            "n": k}
+
+
+# exit status of a rank whose nested-record watchdog fired: the headline line was printed,
+# a nested record did not finish (GNU timeout's code, so launchers read it as a time limit)
+NESTED_TIMEOUT_EXIT = 124
+
+
 class _NestedGuard:
     """Bounds one nested record. If it has not finished after ``timeout_s``, rank 0 prints
     the (already measured) record with ``<name>.error`` and every rank leaves with
-    ``os._exit(0)`` — the process teardown releases any RCCL kernel still waiting on a
-    peer. ``cancel()`` returns False when the guard has already fired."""
+    ``os._exit(NESTED_TIMEOUT_EXIT)`` -- non-zero, so a hung peer is never reported as a
+    clean run; the process teardown releases any RCCL kernel still waiting on a peer.
+    ``cancel()`` returns False when the guard has already fired."""
 
     def __init__(self, timeout_s: float, rec: dict, rank: int, name: str = "sgd"):
         self.name = name
@@ -349,7 +488,7 @@ class _NestedGuard:
         if self.rank == 0:
             rec = dict(self.rec, **{self.name: {"error": f"timeout after {timeout_s:g} s"}})
             print(json.dumps(rec), flush=True)
-        os._exit(0)
+        os._exit(NESTED_TIMEOUT_EXIT)
 
     def cancel(self) -> bool:
         with self._lock:

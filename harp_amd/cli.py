@@ -238,8 +238,13 @@ def _run_lda(comm, cfg):
     vocab = cfg.get("vocab") or _allmax(comm, int(word.max()) + 1 if word.numel() else 0)
     n_docs = sum(counts)
     doc, word = shuffle_coo(comm, doc % comm.world_size, doc, word)
+    # minBound / maxBound (LDAMPCollectiveMapper.java:98-118): a band below 100 % turns on the
+    # timer-bounded steps, starting at the reference's 1 s step and retuned every iteration
+    lo, hi = cfg["min_bound"], cfg["max_bound"]
+    tune = (lo > 0 or hi > 0) and hi != 100
     lc = LDAConfig(num_topics=cfg["num_topics"], alpha=cfg["alpha"], beta=cfg["beta"], iterations=cfg["iterations"],
-                   print_interval=max(1, cfg["iterations"]))
+                   print_interval=max(1, cfg["iterations"]), time_budget_ms=1000.0 if tune else 0.0,
+                   min_bound=lo if tune else 0, max_bound=hi if tune else 0)
     res = run_lda(comm, lc, n_docs, vocab, (doc.cpu(), word.cpu()))
     if comm.rank == 0:
         _write(os.path.join(cfg["work_dir"], "likelihood"), "\n".join(f"{i} {v}" for i, v in res["loglik"]) + "\n")

@@ -23,7 +23,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from ..ops import lda as L
-from ..runtime.dymoro import DeviceRotator, RotationSchedule, ring_strides
+from ..runtime.dymoro import BudgetTuner, DeviceRotator, RotationSchedule, StepBudget, ring_strides
 from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
 from .common import reduce_partials
 
@@ -49,6 +49,8 @@ class LDAConfig:
     model_dir: str = ""       # word-model dumps every print_interval*10 iterations + at the end
     time_budget_ms: float = 0.0  # >0: time-bounded rotation steps (LDAMPCollectiveMapper timer); 0: full sweeps
     budget_pieces: int = 8    # launches a step's word chunks are cut into
+    min_bound: int = 0        # with a budget: retune it every iteration so the trained percentage lands
+    max_bound: int = 0        # in [min_bound, max_bound] (dymoro.BudgetTuner); 0 / 0: the budget stays fixed
 
 
 def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, seed: int = 0, device="cpu"):
@@ -69,6 +71,9 @@ def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, s
 
 
 class LDACollectiveMapper(CollectiveMapper):
+    budget = None  # StepBudget when cfg.time_budget_ms > 0
+    tuner = None   # BudgetTuner when a [min_bound, max_bound] band is set
+
     def __init__(self, comm=None, config: Optional[LDAConfig] = None, n_docs: int = 0, vocab: int = 0,
                  tokens=None, metrics=None):
         super().__init__(comm, metrics)
@@ -140,6 +145,20 @@ class LDACollectiveMapper(CollectiveMapper):
         self.rot = DeviceRotator(self.comm, slabs, name="lda-w", metrics=self.metrics, codec=self.codec)
         self.vbeta = self.vocab * cfg.beta
         self.word_perm = perm  # slice s holds words perm[s*vps:(s+1)*vps]
+        self._init_budget()
+
+    def _init_budget(self) -> None:
+        cfg = self.cfg
+        self.budget = StepBudget(cfg.time_budget_ms / 1e3, self.device) if cfg.time_budget_ms > 0 else None
+        self._chunk_cursor, self._chunks_host = {}, {}
+        self.tuner = BudgetTuner(cfg.min_bound, cfg.max_bound) if (
+            self.budget is not None and (cfg.min_bound > 0 or cfg.max_bound > 0)) else None
+        self.budget_history: List[float] = [self.budget.budget_s] if self.budget is not None else []
+        if self.tuner is not None:  # the tuner's denominator: every worker's tokens
+            t = torch.tensor([float(self.tdoc.numel())], dtype=torch.float64, device=self.device)
+            if self.get_num_workers() > 1:
+                self.comm.all_reduce(t)
+            self.total_tokens = int(t.item())
 
     def _rotation_codec(self, nwk_full: torch.Tensor, ns: int):
         """Sparse slab payloads for the rotation when they pay. A word's token total (its
@@ -162,6 +181,7 @@ class LDACollectiveMapper(CollectiveMapper):
         P, me, S = self.get_num_workers(), self.get_self_id(), cfg.num_slices
         delta_total = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
         n = 0
+        c0 = self.budget.compute_s if self.budget is not None else 0.0
         for s in range(P):
             nk_view = self.nk + delta_total  # own updates are visible immediately
             for k in range(S):
@@ -188,19 +208,17 @@ class LDACollectiveMapper(CollectiveMapper):
         else:
             dt = delta_total
         self.nk += dt
+        if self.tuner is not None:  # LDAMPCollectiveMapper.java:295-314
+            self.budget.budget_s = self.tuner(self, self.budget.budget_s, self.budget.compute_s - c0, n,
+                                              self.total_tokens, P * S, it, "lda")
+            self.budget_history.append(self.budget.budget_s)
         return n
 
     def _budget_step(self, gs: int, slab, delta_total, it: int, s: int, k: int):
         """Sample slice ``gs`` for at most the step budget, in pieces of consecutive word
         chunks; a per-slice chunk cursor makes the next visit continue where the budget
         cut this one (tokens not reached keep their topic for this iteration)."""
-        from ..runtime.dymoro import StepBudget
-
         cfg = self.cfg
-        if getattr(self, "budget", None) is None:
-            self.budget = StepBudget(cfg.time_budget_ms / 1e3, self.device)
-            self._chunk_cursor = {}
-            self._chunks_host = {}
         ch = self.chunks[gs]
         chh = self._chunks_host.get(gs)
         if chh is None:

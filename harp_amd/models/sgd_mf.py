@@ -210,6 +210,11 @@ class SGDCollectiveMapper(CollectiveMapper):
             slabs.append((torch.rand((self.ips, r), generator=gh) * 2 * scale).to(dev))
         self.rot = DeviceRotator(self.comm, slabs, name="sgd-h", metrics=self.metrics)
         self.trained = 0
+        # timer-bounded steps: one budget for every path (GPU pieces, CPU pieces, and the
+        # threaded CPU BlockScheduler, which adds its step times so the tuner can read them)
+        self.budget = StepBudget(cfg.time_budget_ms / 1e3, dev) if cfg.time_budget_ms > 0 else None
+        self.budget_history = [self.budget.budget_s] if self.budget is not None else []
+        self._cursor = {}
 
     def _all_users_of(self, me: int) -> torch.Tensor:
         allu = torch.arange(self.n_users, device=self._train[0].device)
@@ -230,9 +235,12 @@ class SGDCollectiveMapper(CollectiveMapper):
                     if cfg.xcd_blocks and self.device.type == "cpu" and cfg.cpu_threads > 1:
                         # CPU worker: the reference's threaded 2-D scheduler with its timer
                         r_, c_, v_, off, hoff = self.train.get_cells(gs)
-                        budget = cfg.time_budget_ms / 1e3 if cfg.time_budget_ms > 0 else None
+                        budget = self.budget.budget_s if self.budget is not None else None
+                        t0 = time.perf_counter()
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
                                                    host_off=hoff, threads=cfg.cpu_threads, time_budget=budget)
+                        if self.budget is not None:
+                            self.budget.compute_s += time.perf_counter() - t0
                     elif cfg.time_budget_ms > 0:
                         n += self._budget_step(gs, slab)
                     elif cfg.xcd_blocks:
@@ -261,10 +269,6 @@ class SGDCollectiveMapper(CollectiveMapper):
         """Train slice ``gs`` for at most the step budget, in ``budget_pieces`` pieces
         that each train one window of every cell (see below)."""
         cfg = self.cfg
-        if getattr(self, "budget", None) is None:
-            self.budget = StepBudget(cfg.time_budget_ms / 1e3, self.device)
-            self.budget_history = [self.budget.budget_s]
-            self._cursor = {}
         if cfg.xcd_blocks:
             r_, c_, v_, off, hoff = self.train.get_cells(gs)
             sizes = [hoff[c + 1] - hoff[c] for c in range(len(hoff) - 1)]

@@ -117,6 +117,9 @@ def _native_tsqr(X: torch.Tensor) -> bool:
     return X.device.type == "cuda" and X.shape[1] <= TSQR_MAX_D and _lib.use_native(X)
 
 CHOLQR_MAX_DIAG_RATIO = 1e5  # max(diag R) / min(diag R) beyond which CholeskyQR2 is not trusted
+# max |R2 - I| of the second pass beyond which Q1 was too far from orthogonal for the second
+# pass to repair (Kahan-like input can pass the diagonal test with cond(X) ~ 1e14)
+CHOLQR_MAX_R2_DEV = 1e-3
 
 
 def cholesky_qr2(X: torch.Tensor, comm: Optional[Communicator] = None) -> Optional[Dict[str, torch.Tensor]]:
@@ -126,9 +129,11 @@ def cholesky_qr2(X: torch.Tensor, comm: Optional[Communicator] = None) -> Option
     handful of times, against D sequential Householder steps of the panel kernels.
 
     Stable while cond(X) is well below 1e8; returns None (the caller falls back to
-    Householder TSQR) when the Cholesky fails or the R1 diagonal spread -- a lower bound of
-    cond(X) -- exceeds ``CHOLQR_MAX_DIAG_RATIO``. The decision is taken from allreduced
-    values, so every worker takes the same branch."""
+    Householder TSQR) when the Cholesky fails, when the R1 diagonal spread -- a lower bound
+    of cond(X) -- exceeds ``CHOLQR_MAX_DIAG_RATIO``, or when the second factor R2 is not
+    within ``CHOLQR_MAX_R2_DEV`` of the identity (R2^T R2 = Q1^T Q1: Q1 was not near
+    orthogonal, which a small diagonal spread does not rule out). Every decision is taken
+    from allreduced values, so every worker takes the same branch."""
     comm = _local(comm)
     Xd = X.double().contiguous()
     Q, R = Xd, None
@@ -141,6 +146,10 @@ def cholesky_qr2(X: torch.Tensor, comm: Optional[Communicator] = None) -> Option
         dg = torch.diagonal(Rk)
         if R is None and float(dg.max()) > CHOLQR_MAX_DIAG_RATIO * float(dg.min().clamp_min(1e-300)):
             return None
+        if R is not None:
+            eye = torch.eye(Rk.shape[0], dtype=Rk.dtype, device=Rk.device)
+            if float((Rk - eye).abs().max()) > CHOLQR_MAX_R2_DEV:
+                return None
         # Q R^-1 as one GEMM with the d x d triangular inverse (a right-side TRSM over the
         # tall matrix measured ~200x slower in rocBLAS and runs out of workspace)
         eye = torch.eye(Rk.shape[0], dtype=Rk.dtype, device=Rk.device)

@@ -47,6 +47,11 @@ class SlabCodec:
         if cols > 65536:
             raise ValueError(f"topic ids travel as uint16: cols {cols} > 65536")
         self.rows, self.cols, self.cap = int(rows), int(cols), max(int(cap), 0)
+        if self.cap >= 2**31 - 1:
+            raise ValueError(f"slab codec capacity {self.cap} does not fit the int32 row offsets")
+        # a slab with >= 2^31 cells could hold more nonzeros than int32 offsets count when its
+        # counts break the token bound: such slabs sum the row counts in int64 and clamp at cap
+        self.wide = self.rows * self.cols >= 2**31
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -81,14 +86,19 @@ class SlabCodec:
             _lib.check(lib.harp_slab_nnz(slab.data_ptr(), self.rows, self.cols, slab.stride(0), self._nnz.data_ptr(), st),
                        "slab_nnz")
             off[0].zero_()
-            torch.cumsum(self._nnz, 0, dtype=torch.int32, out=off[1:])
+            if self.wide:
+                c64 = torch.cumsum(self._nnz, 0, dtype=torch.int64)
+                torch.maximum(self.overflow, (c64[-1:] > self.cap).to(torch.int32), out=self.overflow)
+                off[1:].copy_(c64.clamp_max(self.cap))
+            else:
+                torch.cumsum(self._nnz, 0, dtype=torch.int32, out=off[1:])
             _lib.check(lib.harp_slab_pack(slab.data_ptr(), self.rows, self.cols, slab.stride(0), off.data_ptr(),
                                           self.cap, counts.data_ptr(), topics.data_ptr(), self.overflow.data_ptr(), st),
                        "slab_pack")
             return buf
         nz = slab != 0
         off[0] = 0
-        torch.cumsum(nz.sum(1, dtype=torch.int32), 0, dtype=torch.int32, out=off[1:])
+        off[1:] = torch.cumsum(nz.sum(1, dtype=torch.int64), 0).clamp_max(self.cap).to(torch.int32)
         r, c = nz.nonzero(as_tuple=True)  # row-major: column order within a row
         n = r.numel()
         if n > self.cap:

@@ -310,6 +310,77 @@ def tune_budget(mapper, compute_s: float, items: int, total_items: int, steps: i
     return ratio / max(frac, 1e-12) * avg_step
 
 
+class BudgetTuner:
+    """Per-iteration retuning of the rotation-step time budget so the share of all items
+    trained per iteration lands in ``[min_bound, max_bound]`` percent (the reference's LDA
+    ``adjustMiniBatch``, LDAMPCollectiveMapper.java:295-314, 477-557).
+
+    Each iteration every worker's (compute time, items trained) is all-gathered; the
+    trained percentage is scaled by (predicted / actual) compute time, where predicted =
+    budget x P x slices x P (every step of every worker running exactly to the budget), so
+    steps that overran or finished early are normalised out. Over ``max_bound``: halve the
+    budget. Under ``min_bound``: double it (and keep doubling while the projection stays
+    under); an under-train after an over-train starts a ``break_period`` (1, 2, 4, ...
+    iterations) during which the budget is left alone, which damps oscillation.
+
+    The first tuning (``proportional_first``) instead sets the budget in one proportional
+    step toward the band's midpoint (the SGD ``adjustMiniBatch`` rule,
+    SGDCollectiveMapper.java:623-668): the reference starts LDA at a 1 s CPU step, and a
+    GPU step is milliseconds, so plain halving would need ~10 iterations to get there.
+    Returns the new budget in seconds. Bounds outside (0, 100] fall back to 50/50 and
+    ``max_bound == 100`` disables tuning, as in the reference (:98-118)."""
+
+    def __init__(self, min_bound: int, max_bound: int, proportional_first: bool = True):
+        lo = min_bound if 0 < min_bound <= 100 else 50
+        hi = max_bound if 0 < max_bound <= 100 else 50
+        hi = max(hi, lo)
+        self.enabled = hi != 100
+        self.min_bound, self.max_bound = (100, 100) if not self.enabled else (lo, hi)
+        self.proportional_first = proportional_first
+        self.has_over_trained = False
+        self.last_under_train = 0
+        self.break_period = 0
+        self.tuned = 0
+        self.history: List[dict] = []
+
+    def __call__(self, mapper, budget_s: float, compute_s: float, items: int, total_items: int, steps: int,
+                 it: int, ctx: str = "lda") -> float:
+        if not self.enabled:
+            return budget_s
+        P = mapper.get_num_workers()
+        t = PackedTable([mapper.get_self_id()], torch.tensor([[compute_s, float(items)]], dtype=torch.float64,
+                                                             device=mapper.device), combiner=ArrCombiner(Operation.SUM))
+        if not mapper.allgather(ctx, f"allgather-compute-status-{it}", t):
+            raise IOError("allgather of compute status failed")
+        tot_time, tot_items = t.buffer.sum(0).cpu().tolist()
+        real = 100.0 * tot_items / max(float(total_items), 1.0)
+        predicted = budget_s * P * steps
+        pct = real * predicted / max(tot_time, 1e-12)
+        new = budget_s
+        rec = {"iter": it, "trained_pct": round(real, 3), "projected_pct": round(pct, 3), "budget_s": budget_s}
+        if self.tuned == 0 and self.proportional_first:
+            if pct > self.max_bound or pct < self.min_bound:
+                target = 0.5 * (self.min_bound + self.max_bound)
+                new = budget_s * target / max(pct, 1e-9)
+        elif self.last_under_train == 0 or it - self.last_under_train >= self.break_period:
+            if pct > self.max_bound:
+                self.has_over_trained = True
+                new = budget_s / 2
+            elif pct < self.min_bound:
+                if self.has_over_trained:
+                    self.last_under_train = it
+                    self.break_period = 1 if self.break_period == 0 else 2 * self.break_period
+                new = budget_s * 2
+                potential = 2 * pct
+                while potential < self.min_bound and potential > 0:
+                    potential *= 2
+                    new *= 2
+        self.tuned += 1
+        rec["new_budget_s"] = new
+        self.history.append(rec)
+        return new
+
+
 # ---------------------------------------------------------------- 2-D block scheduler
 class BlockScheduler:
     """Conflict-free 2-D (row split x column split) block scheduler.

@@ -38,9 +38,37 @@ def _roctx():
         return None
 
 
+# pending HIP event pairs kept before the completed ones are folded in (without a device
+# sync); past PENDING_HARD_CAP the rest are resolved with one sync. Long runs that never
+# flush (no metrics path set) therefore hold a bounded number of events.
+PENDING_SWEEP = 1024
+PENDING_HARD_CAP = 8192
+
+
+def _sweep_pending(pending: List[tuple], fold) -> None:
+    """Fold every event pair whose end event has completed (``fold(item, seconds)``);
+    keep the rest, in order. Synchronises only when the list is still over the hard cap."""
+    if len(pending) < PENDING_SWEEP:
+        return
+    keep = []
+    for item in pending:
+        s, e = item[-2], item[-1]
+        if e.query():
+            fold(item, s.elapsed_time(e) / 1e3)
+        else:
+            keep.append(item)
+    if len(keep) >= PENDING_HARD_CAP:
+        torch.cuda.synchronize()
+        for item in keep:
+            fold(item, item[-2].elapsed_time(item[-1]) / 1e3)
+        keep = []
+    pending[:] = keep
+
+
 class PhaseTimer:
     """Accumulates named phase times. On GPU uses hipEvents recorded on the current
-    stream, resolved at :meth:`flush`; on CPU uses perf_counter."""
+    stream, resolved at :meth:`flush` (completed pairs are folded in as the list grows);
+    on CPU uses perf_counter."""
 
     def __init__(self, use_events: Optional[bool] = None, annotate: bool = False):
         self.use_events = torch.cuda.is_available() if use_events is None else use_events
@@ -63,6 +91,7 @@ class PhaseTimer:
             finally:
                 e.record()
                 self._pending.append((name, s, e))
+                _sweep_pending(self._pending, self._fold)
                 if nvtx is not None:
                     nvtx.range_pop()
         else:
@@ -75,12 +104,15 @@ class PhaseTimer:
                 if nvtx is not None:
                     nvtx.range_pop()
 
+    def _fold(self, item: tuple, seconds: float) -> None:
+        self.totals[item[0]] += seconds
+        self.counts[item[0]] += 1
+
     def flush(self) -> Dict[str, float]:
         if self._pending:
             torch.cuda.synchronize()
-            for name, s, e in self._pending:
-                self.totals[name] += s.elapsed_time(e) / 1e3
-                self.counts[name] += 1
+            for item in self._pending:
+                self._fold(item, item[1].elapsed_time(item[2]) / 1e3)
             self._pending.clear()
         return dict(self.totals)
 
@@ -175,9 +207,15 @@ class Metrics:
         self.collectives.append(rec)
         if events is not None:
             self._pending.append((rec, events[0], events[1]))
+            # completed pairs resolve in place, so the list stays bounded without metrics output
+            _sweep_pending(self._pending, self._fold)
         if len(self.collectives) > 10000:
             del self.collectives[:5000]
         return rec
+
+    @staticmethod
+    def _fold(item: tuple, seconds: float) -> None:
+        item[0]["s"] = seconds
 
     @contextlib.contextmanager
     def time_collective(self, kind: str, ctx: str, op: str, nbytes: int = 0, device: Optional[torch.device] = None):

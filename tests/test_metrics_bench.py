@@ -103,14 +103,14 @@ def test_sgd_jsonl_rotation_bytes(tmp_path):
         assert x["trained"] > 0 and x["updates_per_s"] > 0
 
 
-def _run_bench(args, env=None):
+def _run_bench(args, env=None, rc=0):
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         e.pop(k, None)
     e.update(env or {})
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
                        timeout=600, env=e, cwd=ROOT)
-    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.returncode == rc, r.stdout + r.stderr
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     return json.loads(lines[0])
@@ -137,9 +137,96 @@ def test_bench_single_rank_with_sgd_record():
 def test_bench_sgd_guard_keeps_headline_line():
     """A nested MF-SGD record that exceeds --sgd-timeout (a hung rotation peer on a real
     node) still yields exactly one JSON line: the measured K-means record with sgd.error,
-    and every rank exits 0."""
+    and the run exits non-zero (124) so the hang is never reported as a clean run."""
     rec = _run_bench(["--gpus", "2", "--points", "2e4", "--centroids", "128", "--backend", "gloo", "--steps", "2",
                       "--warmup", "1", "--sgd", "on", "--sgd-users", "2000", "--sgd-items", "300",
-                      "--sgd-ratings", "20000", "--sgd-rank", "16", "--sgd-timeout", "0.01"])
+                      "--sgd-ratings", "20000", "--sgd-rank", "16", "--sgd-timeout", "0.01"], rc=124)
     assert rec["n_gpus"] == 2 and rec["value"] > 0
     assert "timeout" in rec["sgd"]["error"]
+
+
+_TINY = ["--points", "3e4", "--centroids", "128", "--backend", "gloo", "--steps", "10", "--warmup", "1",
+         "--sgd", "on", "--sgd-users", "3000", "--sgd-items", "400", "--sgd-ratings", "30000", "--sgd-rank", "16",
+         "--sgd-epochs", "10", "--extras", "on", "--pca-n", "6000", "--pca-d", "24", "--pca-steps", "10",
+         "--lda-docs", "600", "--lda-vocab", "900", "--lda-topics", "16", "--lda-len", "20", "--lda-iters", "10"]
+
+
+def _check_full_record(rec, P):
+    assert rec["n_gpus"] == P and rec["config"]["parallelism"] == f"dp{P}"
+    assert rec["steps"] == 10 and rec["value"] > 0 and rec["median_s_per_iter"] > 0
+    assert rec["step_s"]["n"] == 10
+    assert rec["sync_bytes_per_iter"] > 0
+    for name in ("sgd", "pca", "lda"):
+        sub = rec[name]
+        assert "error" not in sub, (name, sub)
+        assert sub["n_gpus"] == P, (name, sub)
+        assert sub["sync_bytes_per_iter"] > 0, (name, sub)
+    s = rec["sgd"]
+    assert s["updates_per_sec"] > 0 and s["epoch_s"]["n"] == 10 and 0 < s["train_rmse"] < 2
+    # ring mode: the two slices rotate on different coprime strides (different xGMI links)
+    if P > 2:
+        assert len(set(s["rotation_strides"])) == 2
+    p = rec["pca"]
+    assert p["pass_s"]["n"] == 10 and p["max_eigenvalue"] > 0.9
+    lda = rec["lda"]
+    assert lda["iter_s"]["n"] == 10 and lda["tokens_per_sec"] > 0 and lda["local_server"] is False
+
+
+@pytest.mark.slow
+def test_bench_full_records_three_ranks():
+    """Every nested record (K-means, MF-SGD rotation with ring strides, PCA, LDA push-pull
+    with the server table remote) runs to completion at P=3 over gloo."""
+    _check_full_record(_run_bench(["--gpus", "3"] + _TINY), 3)
+
+
+@pytest.mark.slow
+def test_bench_full_records_eight_ranks():
+    """Same at the 8-GPU node's world size (8 gloo ranks on the CPU)."""
+    _check_full_record(_run_bench(["--gpus", "8"] + _TINY), 8)
+
+
+def test_bench_single_rank_lda_records_collective_cost():
+    """At P=1 the push-pull record also measures the sweep with pull / delta / push."""
+    rec = _run_bench(["--gpus", "1", "--points", "1e4", "--centroids", "128", "--steps", "2", "--warmup", "1",
+                      "--sgd", "off", "--extras", "on", "--pca-n", "3000", "--pca-d", "16", "--pca-steps", "2",
+                      "--lda-docs", "300", "--lda-vocab", "500", "--lda-topics", "16", "--lda-len", "20",
+                      "--lda-iters", "2"])
+    lda = rec["lda"]
+    assert lda["local_server"] is True and "error" not in lda
+    assert lda["no_local_server"]["tokens_per_sec"] > 0
+    assert rec["pca"]["syrk_tflops"] is not None and rec["pca"]["n_gpus"] == 1
+
+
+class _FakeEvent:
+    def __init__(self, done=True):
+        self.done = done
+
+    def query(self):
+        return self.done
+
+    def elapsed_time(self, other):
+        return 2.0  # ms
+
+
+def test_pending_events_stay_bounded_without_metrics_path(monkeypatch):
+    """Without a metrics path nothing flushes; completed event pairs must still be folded
+    in as they accumulate (unbounded _pending)."""
+    import harp_amd.utils.metrics as M
+
+    m = Metrics()
+    for i in range(5 * M.PENDING_SWEEP):
+        m.collective("allreduce", "c", f"op{i}", 0.0, 8, events=(_FakeEvent(), _FakeEvent()))
+    assert len(m._pending) < M.PENDING_SWEEP
+    assert m.collectives[0]["s"] == pytest.approx(2e-3)
+    # pairs still in flight are kept (in order) until the hard cap forces one sync
+    synced = []
+    monkeypatch.setattr(M.torch.cuda, "synchronize", lambda: synced.append(1))
+    m2 = Metrics()
+    for i in range(M.PENDING_HARD_CAP + 1):
+        m2.collective("allreduce", "c", f"op{i}", 0.0, 8, events=(_FakeEvent(False), _FakeEvent(False)))
+    assert synced and len(m2._pending) < M.PENDING_HARD_CAP
+    t = M.PhaseTimer(use_events=False)
+    for i in range(3 * M.PENDING_SWEEP):
+        t._pending.append(("compute", _FakeEvent(), _FakeEvent()))
+        M._sweep_pending(t._pending, t._fold)
+    assert len(t._pending) < M.PENDING_SWEEP and t.counts["compute"] > 0

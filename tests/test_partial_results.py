@@ -183,3 +183,27 @@ def test_cholesky_qr2_refuses_ill_conditioned_and_auto_falls_back():
     assert ST.cholesky_qr2(X) is None
     out = ST.tsqr(X, method="auto")  # CPU auto = Householder anyway; result must stay exact
     assert torch.allclose(out["Q"] @ out["R"], X, atol=1e-12)
+
+
+def test_cholesky_qr2_refuses_kahan_with_small_diagonal_spread():
+    """A Kahan matrix (cond ~1e14, R diagonal spread ~100) passes the diagonal test; the
+    second-pass factor R2 being far from I must send tsqr to Householder."""
+    import math
+
+    from harp_amd.models import stats as ST
+
+    n, c = 100, 0.3
+    s = math.sqrt(1 - c * c)
+    K = torch.diag(torch.tensor([s ** i for i in range(n)], dtype=torch.float64)) @ (
+        torch.eye(n, dtype=torch.float64) - c * torch.triu(torch.ones(n, n, dtype=torch.float64), 1))
+    g = torch.Generator().manual_seed(0)
+    Q0, _ = torch.linalg.qr(torch.randn(3000, n, generator=g, dtype=torch.float64))
+    X = Q0 @ K
+    dg = torch.diagonal(K)
+    assert float(dg.max() / dg.min()) < ST.CHOLQR_MAX_DIAG_RATIO  # the old test alone accepts it
+    assert ST.cholesky_qr2(X) is None
+    with pytest.raises(ValueError):
+        ST.tsqr(X, method="cholqr2")
+    out = ST.tsqr(X, method="householder")
+    eye = torch.eye(n, dtype=torch.float64)
+    assert (out["Q"].t() @ out["Q"] - eye).abs().max() < 1e-12

@@ -68,3 +68,11 @@ def test_lda_rotation_codec_matches_dense(P):
     sparse = launch(_job, P, args=(LDAConfig(rotate_codec="on", **base), 300, 2000, corpus), timeout=300)
     assert dense[0]["rotate_payload_bytes"] == 0 and sparse[0]["rotate_payload_bytes"] > 0
     assert dense[0]["loglik"] == sparse[0]["loglik"], (dense[0]["loglik"], sparse[0]["loglik"])
+
+
+def test_capacity_beyond_int32_offsets_is_refused():
+    """offsets are int32; a cap past 2^31 would wrap them silently."""
+    with pytest.raises(ValueError):
+        SlabCodec(1 << 20, 4096, 2**31, torch.device("cpu"))
+    c = SlabCodec(1 << 20, 4096, 1000, torch.device("cpu"))  # >= 2^31 cells: int64 row sums
+    assert c.wide and not SlabCodec(64, 64, 100, torch.device("cpu")).wide

@@ -99,3 +99,74 @@ def test_cpu_threaded_block_scheduler_path():
         out[name] = m.trained
     assert out["all"] == 2 * 9000
     assert 0 < out["timer"] < 2 * 9000
+
+
+def _lda_tuned(comm, lo, hi, iters=5):
+    from harp_amd.models.lda import LDACollectiveMapper, LDAConfig, synthetic_corpus
+
+    doc, word = synthetic_corpus(4000, 3000, 20, 60, seed=5)
+    cfg = LDAConfig(num_topics=64, iterations=iters, print_interval=0, time_budget_ms=1000.0, budget_pieces=8,
+                    min_bound=lo, max_bound=hi)
+    m = LDACollectiveMapper(comm, cfg, 4000, 3000, (doc, word))
+    m.init_model(KeyValReader([]))
+    toks = [m.iterate(it) for it in range(iters)]
+    m.rot.wait_all()
+    return {"tokens": toks, "total": m.total_tokens, "budget": list(m.budget_history), "hist": m.tuner.history,
+            "nk": int(m.nk.sum())}
+
+
+def test_lda_budget_tuner_converges_into_band_two_workers():
+    """LDA timer auto-tuning (LDAMPCollectiveMapper.java:295-314, 477-557): starting at the
+    reference's 1 s step (a full sweep here), the all-gathered trained percentage lands in
+    [40, 80] within 3 iterations, and every worker takes the same budget decisions."""
+    res = launch(_lda_tuned, 2, args=(40, 80), timeout=600)
+    for r in res:
+        assert r["budget"][0] == pytest.approx(1.0)
+        assert r["hist"][0]["trained_pct"] == pytest.approx(100.0)  # iteration 0: everything
+        assert r["budget"][1] < 0.5  # one proportional step down
+        tot = [sum(x) for x in zip(*[q["tokens"] for q in res])]
+        pct = [100.0 * t / r["total"] for t in tot]
+        assert any(40 <= p <= 80 for p in pct[1:4]), (pct, r["hist"])
+        assert r["nk"] == r["total"]
+    assert res[0]["budget"] == pytest.approx(res[1]["budget"])  # one all-gathered decision
+
+
+def test_budget_tuner_state_machine():
+    """Halve over the band, double under it, and a break period after an under-train that
+    followed an over-train (the reference's hasOverTrained / lastUnderTrainIte / breakPeriod)."""
+    from harp_amd.runtime.dymoro import BudgetTuner
+
+    class _M:  # one worker: the all-gather returns its own (time, items)
+        device = torch.device("cpu")
+
+        def get_num_workers(self):
+            return 1
+
+        def get_self_id(self):
+            return 0
+
+        def allgather(self, ctx, op, t):
+            return True
+
+    t = BudgetTuner(40, 80, proportional_first=False)
+    m = _M()
+    # full budget used, 100 % trained: over -> halve
+    assert t(m, 1.0, 4.0, 100, 100, 4, it=1) == pytest.approx(0.5)
+    # 10 % trained with the budget fully used: under after an over -> double twice (10->20->40),
+    # and a break period of 1 starts at iteration 2
+    assert t(m, 0.5, 2.0, 10, 100, 4, it=2) == pytest.approx(2.0)
+    assert t.break_period == 1 and t.last_under_train == 2
+    # at iteration 3 (3 - 2 >= 1) tuning resumes; 60 % is inside the band -> unchanged
+    assert t(m, 2.0, 8.0, 60, 100, 4, it=3) == pytest.approx(2.0)
+    assert BudgetTuner(0, 100).enabled is False and BudgetTuner(0, 0).max_bound == 50
+
+
+def test_threaded_cpu_path_with_tuning():
+    """the threaded CPU BlockScheduler path with a budget and tune_ratio used to
+    raise AttributeError after epoch 0 (no StepBudget on that path)."""
+    tr = synthetic_ratings(600, 120, 9000, seed=6)
+    cfg = SGDConfig(rank=8, epochs=2, test_every=0, xcd_blocks=True, cpu_threads=4, time_budget_ms=5.0,
+                    tune_ratio=0.5)
+    m = SGDCollectiveMapper(_cpu(), cfg, 600, 120, tr, None)
+    m.run(KeyValReader([]))
+    assert len(m.budget_history) == 2 and m.budget_history[1] > 0 and m.budget.compute_s > 0
