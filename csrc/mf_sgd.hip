@@ -88,6 +88,16 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&x
   }
 }
 
+// W rows: L1-cached loads, or (persistent flow kernel, where rows written earlier in the
+// same launch by other CUs of the XCD must be seen) loads from L2 like the H rows
+template <int EPL, bool L2>
+__device__ __forceinline__ void load_w(const float* __restrict__ p, float (&x)[EPL]) {
+  if constexpr (L2)
+    load_row_l2<EPL>(p, x);
+  else
+    load_row<EPL>(p, x);
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
@@ -256,7 +266,7 @@ constexpr int XCDS = 8;
 // store waits changed nothing, while ablating the H stores (+66 %) or the H loads (+32 %)
 // and uniform instead of skewed item popularity (+30 %) did: the kernel is bound by L2
 // traffic on hot H rows.
-template <int R>
+template <int R, bool WL2 = false>
 __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, const float* sV, int n, int sl,
                                                float* __restrict__ W, unsigned ldw, float* __restrict__ H,
                                                unsigned ldh, float lr, float lam) {
@@ -270,7 +280,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
   const int i1c = n > 1 ? 1 : 0;
   unsigned row1 = (unsigned)sR[i1c], col1 = (unsigned)sC[i1c];
   float v1 = sV[i1c];
-  load_row<EPL>(W + (cur * ldw + lo), w);
+  load_w<EPL, WL2>(W + (cur * ldw + lo), w);
   load_row_l2<EPL>(H + (col0 * ldh + lo), h);
   load_row_l2<EPL>(H + (col1 * ldh + lo), hB);
 #pragma unroll
@@ -304,7 +314,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     if (!last && row1 != cur) {
       store_row<EPL>(W + (cur * ldw + lo), w);
       cur = row1;
-      load_row<EPL>(W + (cur * ldw + lo), w);
+      load_w<EPL, WL2>(W + (cur * ldw + lo), w);
     }
     const int i2 = i + 2 < n ? i + 2 : n - 1;  // clamped: the last prefetch is a harmless re-read
     const unsigned row2 = (unsigned)sR[i2], col2 = (unsigned)sC[i2];
@@ -379,6 +389,135 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
       sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
                              (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
+}
+
+// Persistent XCD-blocked pass: all `steps` sub-steps of one slice in ONE launch, ordered by
+// point-to-point completion flags instead of kernel boundaries (the reference's dymoro
+// Scheduler hands a block to a thread as soon as its row and column are free,
+// ml/java/.../dymoro/Scheduler.java:95-237; here the unit is an XCD cell).
+//
+// In sub-step s XCD x trains cell (x, (x + s) mod 8): its user block x is private to the
+// XCD in every sub-step, and its item block (x + s) mod 8 was trained in sub-step s - 1 by
+// XCD x + 1 (and in s + 1 by XCD x - 1). So XCD x may start sub-step s as soon as XCD
+// x + 1 has FINISHED sub-step s - 1 -- a dependency on one neighbour, no grid barrier.
+//  * work: rounds of 16 streams x CH ratings are claimed from a per-(XCD, sub-step)
+//    counter by any block of the XCD, so no block ever waits on a specific other block;
+//    the first 8 blocks dispatched cover the 8 XCDs, so every XCD always has a running
+//    block and every wait terminates (the chain of waits ends at sub-step 0);
+//  * completion: a block finishing a round makes its stores visible (workgroup release)
+//    and counts it; the block completing the LAST round of (x, s) writes the XCD's L2 back
+//    (agent release) and raises fin[x][s];
+//  * visibility: XCD x reads item block b only after its producer's write-back, and its
+//    own L2 holds no line of b in this launch (b was not touched by x since the launch
+//    started, and a launch starts with invalidated caches), so no invalidation is needed;
+//    W rows (written by other CUs of the same XCD in earlier sub-steps) are read from L2;
+//  * the last block to leave zeroes the counters for the next launch on this stream;
+//  * a wait gives up after ~1 s and raises the error word (a launch-geometry bug must
+//    never hang the GPU); the host checks it.
+// ws layout (int32): claim[64] | done[64] | fin[64] | exit | error
+constexpr int kFlowWs = 3 * 64 + 2;
+
+// raise a completion flag after writing this XCD's L2 back (agent-scope release), with an
+// explicit wait so the flag cannot overtake the write-back
+__device__ __forceinline__ void publish(int* flag) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_s_waitcnt(0);
+  __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int R, int CH>
+__global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
+                                                              const float* __restrict__ vals,
+                                                              const long* __restrict__ off,
+                                                              const long* __restrict__ win, int steps,
+                                                              float* __restrict__ W, int ldw, float* __restrict__ H,
+                                                              int ldh, float lr, float lam, int* __restrict__ ws) {
+  __shared__ int sR[16 * CH], sC[16 * CH];
+  __shared__ float sV[16 * CH];
+  __shared__ int s_round;
+  int* claim = ws;
+  int* done = ws + 64;
+  int* fin = ws + 128;
+  int* exit_ctr = ws + 192;
+  int* err = ws + 193;
+  const int x = blockIdx.x % XCDS;
+  const int nxt = (x + 1) % XCDS;
+  const int sl = threadIdx.x & 15;
+  const int sub = threadIdx.x >> 4;
+  for (int step = 0; step < steps; ++step) {
+    const int cell = x * XCDS + (x + step) % XCDS;
+    const long a = off[cell];
+    const long ncell = off[cell + 1] - a;
+    const long w0 = win ? win[cell] : 0;
+    const long n = win ? win[XCDS * XCDS + cell] : ncell;
+    const long nst = (n + CH - 1) / CH;
+    const int rounds = (int)((nst + 15) / 16);
+    if (step > 0) {  // item block (x + step) mod 8: XCD x + 1 must have finished step - 1
+      if (threadIdx.x == 0) {
+        long spins = 0;
+        while (__hip_atomic_load(fin + nxt * XCDS + (step - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+          __builtin_amdgcn_s_sleep(8);
+          if (++spins > (1L << 22)) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    if (rounds == 0) {  // empty cell: complete at once (idempotent)
+      if (threadIdx.x == 0) publish(fin + x * XCDS + step);
+      continue;
+    }
+    for (;;) {
+      if (threadIdx.x == 0)
+        s_round = __hip_atomic_fetch_add(claim + x * XCDS + step, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int rd = s_round;
+      if (rd >= rounds) {
+        __syncthreads();  // everyone read s_round before it is rewritten
+        break;
+      }
+      const long r0 = (long)rd * 16 * CH;
+      for (int k = threadIdx.x; k < 16 * CH; k += 256) {
+        if (r0 + k < n) {
+          long q = w0 + r0 + k;
+          if (q >= ncell) q -= ncell;
+          sR[k] = rows[a + q];
+          sC[k] = cols[a + q];
+          sV[k] = vals[a + q];
+        }
+      }
+      __syncthreads();
+      const long mine = n - (r0 + (long)sub * CH);
+      if (mine > 0)
+        sgd_stream_lds<R, true>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
+                                (unsigned)ldw, H, (unsigned)ldh, lr, lam);
+      // every wave's H / W stores are acknowledged by the XCD's L2 before the round counts
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();  // ... and the LDS triples are free
+      if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(done + x * XCDS + step, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == rounds - 1) publish(fin + x * XCDS + step);  // the last round of (x, step)
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(exit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (int)gridDim.x - 1) {  // every block has left: reset for the next launch
+      for (int k = 0; k < 193; ++k) __hip_atomic_store(ws + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int R, int CH>
+int launch_sgd_xcd_flow(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
+                        int steps, int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam,
+                        int* ws, hipStream_t s) {
+  mf_sgd_xcd_flow_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+      rows, cols, vals, off, win, steps, W, ldw, H, ldh, lr, lam, ws);
+  return harp_launch_status();
 }
 
 template <int R>
@@ -705,6 +844,30 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
   MF_DISPATCH(r, SGDX_CALL)
 #undef SGDX_CALL
 #undef SGDX_ARGS
+}
+
+// One launch for all `steps` sub-steps (mf_sgd_xcd_flow_kernel); same arguments as
+// harp_mf_sgd_xcd plus `ws`, a zeroed device int32 workspace of harp_mf_flow_ws_ints()
+// entries private to the stream (left zeroed again by the launch; ws[193] != 0 afterwards
+// means a wait timed out). Ranks <= 256 only.
+HARP_EXPORT int harp_mf_flow_ws_ints() { return kFlowWs; }
+
+HARP_EXPORT int harp_mf_sgd_xcd_flow(const int* rows, const int* cols, const float* vals, const long* off,
+                                     const long* win, int r, int steps, int chunk, int blocks_per_xcd, float* W,
+                                     int ldw, float* H, int ldh, float lr, float lam, int* ws, hipStream_t s) {
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || wide_ok(r) || !ws)
+    return HARP_EBADARG;
+#define SGDF_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, ws, s
+#define SGDF_CALL(RR)                                                                  \
+  (chunk == 8 ? launch_sgd_xcd_flow<RR, 8>(SGDF_ARGS)                                   \
+   : chunk == 16 ? launch_sgd_xcd_flow<RR, 16>(SGDF_ARGS)                               \
+   : chunk == 32 ? launch_sgd_xcd_flow<RR, 32>(SGDF_ARGS)                               \
+   : chunk == 64 ? launch_sgd_xcd_flow<RR, 64>(SGDF_ARGS)                               \
+   : chunk == 128 ? launch_sgd_xcd_flow<RR, 128>(SGDF_ARGS)                             \
+                  : HARP_EBADARG)
+  MF_DISPATCH(r, SGDF_CALL)
+#undef SGDF_CALL
+#undef SGDF_ARGS
 }
 
 HARP_EXPORT int harp_mf_rmse_blocks() { return 1024; }

@@ -1,0 +1,284 @@
+// Device-resident SMO for C-SVC (gfx950): every step of every binary machine runs on the
+// GPU, no host round trip until the machine has converged.
+//
+// Reference: ml/daal/.../daal_svm/MultiClassDenseBatch/SVMDaalCollectiveMapper.java:179
+// (DAAL svm training, boser SMO, inside multi_class_classifier one-against-one) and the
+// libsvm-trained cascade of contrib/.../svm/SVMMapper.java:174-222.
+//
+// Algorithm: SMO with second-order working-set selection (WSS-2, Fan, Chen & Lin 2005),
+// the same arithmetic as the PyTorch solver in harp_amd/models/svm.py (the test oracle):
+//   i = argmax_{t in I_up} -y_t G_t,  stop if m(a) - M(a) < eps
+//   j = argmin_{t in I_low, -y_t G_t < m} -(m + y_t G_t)^2 / max(K_ii + K_tt - 2 K_it, tau)
+//   delta clipped to the box, a_i += y_i delta, a_j -= y_j delta,
+//   G += y (y_i da_i K_i + y_j da_j K_j)
+// Ties resolve to the lowest index (torch argmax / argmin). Products and sums are rounded
+// one by one (no FMA contraction) so the trajectory follows the oracle's.
+//
+// Design: ONE 1024-thread workgroup per binary machine (one-vs-one machines of a
+// multiclass problem run concurrently, one per CU). Thread t owns elements t + 1024 k:
+// their gradient G lives in registers for the whole solve and the box-state bits (a < C,
+// a > 0, y > 0) in three bit masks, so a step touches global memory only for the two
+// kernel rows (gathered through the machine's index list from the shared Gram matrix,
+// L2/HBM) and the diagonal. Three block reductions per step (i; j; the broadcast of the
+// update). n <= 1024 * 32 per machine.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+
+struct ArgMax {
+  double v;
+  int i;
+};
+
+// better(a, b): a larger value, or an equal value at a lower index
+__device__ __forceinline__ bool better_max(double va, int ia, double vb, int ib) {
+  return va > vb || (va == vb && ia < ib);
+}
+__device__ __forceinline__ bool better_min(double va, int ia, double vb, int ib) {
+  return va < vb || (va == vb && ia < ib);
+}
+
+template <bool MAX>
+__device__ __forceinline__ void wave_arg(double& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (MAX ? better_max(ov, oi, v, i) : better_min(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// GREG: the gradient lives in registers (EPT <= 8: <= 110 VGPRs at 1024 threads); else in
+// the machine's slice of g (L2-resident, 8n bytes) -- the 16 / 32-element forms spilled.
+template <int EPT, bool GREG = (EPT <= 8)>
+__global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict__ Kfull, long ldk,
+                                                       const int* __restrict__ ids_all, const long* __restrict__ moff,
+                                                       const double* __restrict__ y_all,
+                                                       const double* __restrict__ kd_all, double* __restrict__ a_all,
+                                                       double* __restrict__ g_all, int* __restrict__ iters, double C,
+                                                       double eps, double tau, int max_iter) {
+  __shared__ double s_v[kWaves], s_w[kWaves];
+  __shared__ int s_i[kWaves];
+  __shared__ double s_bc[8];
+  __shared__ int s_ic[4];
+  const int m = blockIdx.x;
+  const long base = moff[m];
+  const int n = (int)(moff[m + 1] - base);
+  const int* ids = ids_all + base;
+  const double* y = y_all + base;
+  const double* kd = kd_all + base;
+  double* a = a_all + base;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const double NEG = -__builtin_inf(), POS = __builtin_inf();
+
+  double G[GREG ? EPT : 1];
+  double* g = g_all + base;
+  unsigned ypos = 0, ltC = 0, gt0 = 0;  // bit k: element tid + 1024 k
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int t = tid + kThreads * k;
+    if constexpr (GREG) G[k] = -1.0;
+    if (t < n) {
+      const double at = a[t];
+      if (y[t] > 0) ypos |= 1u << k;
+      if (at < C) ltC |= 1u << k;
+      if (at > 0) gt0 |= 1u << k;
+      if constexpr (GREG) G[k] = g[t];
+    }
+  }
+#define GK(k, t) (GREG ? G[GREG ? (k) : 0] : g[t])
+  constexpr int UNR = GREG ? EPT : 4;  // register form: full unroll (static G indices)
+  int it = 0;
+  for (; it < max_iter; ++it) {
+    // ---- i = argmax over I_up of mg = -y G; Mv = min over I_low of mg
+    double bv = NEG, lo = POS;
+    int bi = 0x7fffffff;
+#pragma unroll UNR
+    for (int k = 0; k < EPT; ++k) {
+      const int t = tid + kThreads * k;
+      if (t >= n) continue;
+      const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
+      const double gk = GK(k, t);
+      const double mg = yp ? -gk : gk;
+      const bool up = (yp && lc) || (!yp && g0);
+      const bool low = (yp && g0) || (!yp && lc);
+      if (up && better_max(mg, t, bv, bi)) {
+        bv = mg;
+        bi = t;
+      }
+      if (low) lo = fmin(lo, mg);
+    }
+    wave_arg<true>(bv, bi);
+    lo = wave_min(lo);
+    if (lane == 0) {
+      s_v[wv] = bv;
+      s_i[wv] = bi;
+      s_w[wv] = lo;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      double v = lane < kWaves ? s_v[lane] : NEG, w = lane < kWaves ? s_w[lane] : POS;
+      int i = lane < kWaves ? s_i[lane] : 0x7fffffff;
+      wave_arg<true>(v, i);
+      w = wave_min(w);
+      if (lane == 0) {
+        s_bc[0] = v;
+        s_bc[1] = w;
+        s_ic[0] = i;
+      }
+    }
+    __syncthreads();
+    const double mval = s_bc[0], Mv = s_bc[1];
+    const int i = s_ic[0];
+    if (!(mval - Mv >= eps) || i >= n) break;  // converged (or no candidate: NaN-safe)
+    // ---- j: second-order selection over K row i
+    const double* Ki = Kfull + (long)ids[i] * ldk;
+    const double kii = kd[i];
+    double sv = POS;
+    int sj = 0x7fffffff;
+#pragma unroll UNR
+    for (int k = 0; k < EPT; ++k) {
+      const int t = tid + kThreads * k;
+      if (t >= n) continue;
+      const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
+      const double gk = GK(k, t);
+      const double mg = yp ? -gk : gk;
+      const bool low = (yp && g0) || (!yp && lc);
+      if (!(low && mg < mval)) continue;
+      const double bt = __dsub_rn(mval, mg);
+      double at = __dsub_rn(__dadd_rn(kii, kd[t]), __dmul_rn(2.0, Ki[ids[t]]));
+      if (!(at > 0)) at = tau;
+      const double sc = -__ddiv_rn(__dmul_rn(bt, bt), at);
+      if (better_min(sc, t, sv, sj)) {
+        sv = sc;
+        sj = t;
+      }
+    }
+    wave_arg<false>(sv, sj);
+    if (lane == 0) {
+      s_v[wv] = sv;
+      s_i[wv] = sj;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      double v = lane < kWaves ? s_v[lane] : POS;
+      int j = lane < kWaves ? s_i[lane] : 0x7fffffff;
+      wave_arg<false>(v, j);
+      if (lane == 0) s_ic[1] = j;
+    }
+    __syncthreads();
+    const int j = s_ic[1];
+    if (j >= n) break;  // no admissible j (cannot happen while m - M >= eps)
+    // ---- the two owners publish what the update needs
+    if (tid == (j & (kThreads - 1))) {
+      const int k = j / kThreads;
+      double gj = 0.0;
+      if constexpr (GREG) {
+#pragma unroll
+        for (int q = 0; q < EPT; ++q)
+          if (q == k) gj = G[q];
+      } else {
+        gj = g[j];
+      }
+      const bool yp = (ypos >> k) & 1;
+      const double mg = yp ? -gj : gj;
+      double at = __dsub_rn(__dadd_rn(kii, kd[j]), __dmul_rn(2.0, Ki[ids[j]]));
+      if (!(at > 0)) at = tau;
+      s_bc[2] = __dsub_rn(mval, mg);  // bt_j
+      s_bc[3] = at;                   // at_j
+      s_bc[4] = a[j];
+      s_bc[5] = y[j];
+    }
+    if (tid == (i & (kThreads - 1))) {
+      s_bc[6] = a[i];
+      s_bc[7] = y[i];
+    }
+    __syncthreads();
+    const double btj = s_bc[2], atj = s_bc[3], aj = s_bc[4], yj = s_bc[5], ai = s_bc[6], yi = s_bc[7];
+    double delta = __ddiv_rn(btj, atj);
+    const double lim_i = yi > 0 ? __dsub_rn(C, ai) : ai;
+    const double lim_j = yj > 0 ? aj : __dsub_rn(C, aj);
+    delta = fmax(0.0, fmin(delta, fmin(lim_i, lim_j)));
+    const double dai = __dmul_rn(yi, delta), daj = -__dmul_rn(yj, delta);
+    const double nai = __dadd_rn(ai, dai), naj = __dadd_rn(aj, daj);
+    // owners refresh the box bits (i first, then j: i == j cannot happen, j has mg < m)
+    if (tid == (i & (kThreads - 1))) {
+      const int k = i / kThreads;
+      ltC = nai < C ? ltC | (1u << k) : ltC & ~(1u << k);
+      gt0 = nai > 0 ? gt0 | (1u << k) : gt0 & ~(1u << k);
+      a[i] = nai;
+    }
+    if (tid == (j & (kThreads - 1))) {
+      const int k = j / kThreads;
+      ltC = naj < C ? ltC | (1u << k) : ltC & ~(1u << k);
+      gt0 = naj > 0 ? gt0 | (1u << k) : gt0 & ~(1u << k);
+      a[j] = naj;
+    }
+    // ---- G += y (yi dai K_i + yj daj K_j)
+    const double ci = __dmul_rn(yi, dai), cj = __dmul_rn(yj, daj);
+    const double* Kj = Kfull + (long)ids[j] * ldk;
+#pragma unroll UNR
+    for (int k = 0; k < EPT; ++k) {
+      const int t = tid + kThreads * k;
+      if (t >= n) continue;
+      const int c = ids[t];
+      const double u = __dadd_rn(__dmul_rn(ci, Ki[c]), __dmul_rn(cj, Kj[c]));
+      const double yt = ((ypos >> k) & 1) ? 1.0 : -1.0;
+      if constexpr (GREG)
+        G[k] = __dadd_rn(G[k], __dmul_rn(yt, u));
+      else
+        g[t] = __dadd_rn(g[t], __dmul_rn(yt, u));
+    }
+    __syncthreads();  // s_bc / s_ic are rewritten by the next step
+  }
+  if constexpr (GREG) {
+#pragma unroll UNR
+    for (int k = 0; k < EPT; ++k) {
+      const int t = tid + kThreads * k;
+      if (t < n) g[t] = G[k];
+    }
+  }
+  if (tid == 0) iters[m] = it;
+#undef GK
+}
+
+template <int EPT>
+int launch_smo(const double* K, long ldk, const int* ids, const long* moff, int nm, const double* y, const double* kd,
+               double* a, double* g, int* iters, double C, double eps, double tau, int max_iter, hipStream_t s) {
+  smo_kernel<EPT><<<dim3(nm), dim3(kThreads), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau, max_iter);
+  return harp_launch_status();
+}
+
+}  // namespace
+
+HARP_EXPORT int harp_svm_max_rows() { return kThreads * 32; }
+
+// nm binary machines; machine m owns entries [moff[m], moff[m+1]) of ids (row/col indices
+// into the n x ldk fp64 Gram K), y (+-1), kd (the machine's K diagonal), a (alphas, in/out:
+// usually zeros) and g (gradient, in/out: usually -1). max_n = the largest machine.
+HARP_EXPORT int harp_svm_smo(const double* K, long ldk, const int* ids, const long* moff, int nm, int max_n,
+                             const double* y, const double* kd, double* a, double* g, int* iters, double C, double eps,
+                             double tau, int max_iter, hipStream_t s) {
+  if (nm <= 0 || max_n <= 0 || max_n > kThreads * 32 || !(C > 0) || max_iter < 0) return HARP_EBADARG;
+  const int ept = (max_n + kThreads - 1) / kThreads;
+#define SMO(E) return launch_smo<E>(K, ldk, ids, moff, nm, y, kd, a, g, iters, C, eps, tau, max_iter, s)
+  if (ept <= 1) SMO(1);
+  if (ept <= 2) SMO(2);
+  if (ept <= 4) SMO(4);
+  if (ept <= 8) SMO(8);
+  if (ept <= 16) SMO(16);
+  SMO(32);
+#undef SMO
+}

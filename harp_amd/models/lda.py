@@ -39,8 +39,8 @@ class LDAConfig:
     seed: int = 0
     max_chunk: int = 0        # tokens per word chunk; 0 = 2048 (dense sampler) / 65536 (sparse)
     block_words: int = 4096   # push/pull strategy: words per model partition
-    sparse_comm: str = "off"  # push/pull: "on" moves nonzero counts only (profiles/r2_apps: the torch
-                              # nonzero / index_add compaction costs 0.15-0.26 s per iteration)
+    sparse_comm: str = "auto"  # push/pull: "on" = fixed-layout sparse rows (parallel.sparse_ps, HIP codec),
+                               # "off" = dense word blocks, "auto" = whichever the link/HBM model says is faster
     local_server: bool = True  # push-pull, one worker owning every touched block: sample in the table
     rotate_codec: str = "auto"  # rotation: "on" sends word-topic slabs as sparse payloads (ops/slabcodec),
                                 # "auto" when that payload is at most half the dense slab, "off" dense
@@ -405,8 +405,23 @@ class LDAPushPullMapper(LDACollectiveMapper):
         ldoc = (doc // P).to(torch.int32)
         blocks = torch.unique(word // B)
         self.need = blocks.cpu().tolist()
-        lrow = torch.searchsorted(blocks, word // B) * B + word % B
-        order = torch.argsort(lrow)
+        nblocks = math.ceil(self.vocab / B)
+        owned = list(range(me, nblocks, P))
+        self.sum = ArrCombiner(Operation.SUM)
+        # a single worker that owns every block its tokens touch, in the same order: its
+        # server table IS the sampled slab, so pull (a copy), the before-snapshot, the delta
+        # and push (an add back) are four full-model passes that leave the same counts;
+        # the table aliases the slab and they are skipped (cfg.local_server=False keeps them)
+        self.local_server = P == 1 and cfg.local_server and self.need == owned
+        self.ps = None
+        if not self.local_server:
+            self.ps = self._sparse_plan(word)  # None: the dense block path is cheaper / unsupported
+        if self.ps is not None:
+            # sparse rows: the local table holds exactly the touched words, in id order
+            lrow = torch.searchsorted(self.touched, word)
+        else:
+            lrow = torch.searchsorted(blocks, word // B) * B + word % B
+        order = torch.argsort(lrow, stable=True)  # token order by word id in either layout
         self.tdoc = ldoc[order].contiguous()
         self.tword = lrow[order].to(torch.int32).contiguous()
         self.chunk_idx = L.build_chunks(self.tword, L.max_chunk(cfg.max_chunk, self.sparse))
@@ -415,85 +430,136 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local) if self.sparse else None
         maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
         self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(dev, maxlen), device=dev)
-        slab = torch.zeros((len(self.need) * B, self.Kp), dtype=torch.int32, device=dev)
+        nrows = self.touched.numel() if self.ps is not None else len(self.need) * B
+        slab = torch.zeros((nrows, self.Kp), dtype=torch.int32, device=dev)
         nk = torch.zeros(self.Kp, dtype=torch.int32, device=dev)
         L.count(self.tdoc, self.tword, self.tz, self.ndk, slab, nk)
         if P > 1:
             nk = reduce_partials(self.comm, {"nk": nk}, dtype=torch.float64)["nk"].round().to(torch.int32)
         self.nk = nk
-        self.sum = ArrCombiner(Operation.SUM)
-        nblocks = math.ceil(self.vocab / B)
-        owned = list(range(me, nblocks, P))
         # distributed global table: owned word blocks, one packed [n_owned, B, K_pad] slab
-        # one persistent buffer of the blocks this worker's tokens touch: pulled into, sampled
-        # on in place, turned into the count delta and pushed back (cached comm plans)
         nneed = len(self.need)
-        self.pull_buf = slab.view(nneed, B, self.Kp) if nneed else torch.zeros((0, B, self.Kp), dtype=torch.int32,
-                                                                              device=dev)
-        # a single worker that owns every block its tokens touch, in the same order: its
-        # server table IS the sampled slab, so pull (a copy), the before-snapshot, the delta
-        # and push (an add back) are four full-model passes that leave the same counts;
-        # the table aliases the slab and they are skipped (cfg.local_server=False keeps them)
-        self.local_server = P == 1 and cfg.local_server and self.need == owned
-        gbuf = self.pull_buf if self.local_server else torch.zeros((len(owned), B, self.Kp), dtype=torch.int32,
-                                                                   device=dev)
-        self.glob = PackedTable(owned, gbuf, table_id=1, combiner=self.sum)
-        self.before = None if self.local_server else torch.empty_like(self.pull_buf)
-        self.want_pt = PackedTable(self.need, self.pull_buf, table_id=3, combiner=self.sum)
-        for t in (self.glob, self.want_pt):
-            t.static_layout = True
-        if not self.local_server:
-            self._push_delta()  # initial counts = a delta against an all-zero model
+        if self.ps is not None:
+            self.pull_buf = slab
+            gbuf = torch.zeros((len(owned), B, self.Kp), dtype=torch.int32, device=dev)
+            self.glob = PackedTable(owned, gbuf, table_id=1, combiner=self.sum)
+            self.glob.static_layout = True
+            self.before = self.want_pt = None
+            self.ps.push(self.pull_buf, self._glob_rows(), delta=False)  # initial counts into an empty model
+        else:
+            # one persistent buffer of the blocks this worker's tokens touch: pulled into,
+            # sampled on in place, turned into the count delta and pushed back (cached plans)
+            self.pull_buf = slab.view(nneed, B, self.Kp) if nneed else torch.zeros((0, B, self.Kp), dtype=torch.int32,
+                                                                                  device=dev)
+            gbuf = self.pull_buf if self.local_server else torch.zeros((len(owned), B, self.Kp), dtype=torch.int32,
+                                                                       device=dev)
+            self.glob = PackedTable(owned, gbuf, table_id=1, combiner=self.sum)
+            self.before = None if self.local_server else torch.empty_like(self.pull_buf)
+            self.want_pt = PackedTable(self.need, self.pull_buf, table_id=3, combiner=self.sum)
+            for t in (self.glob, self.want_pt):
+                t.static_layout = True
+            if not self.local_server:
+                self._push_delta()  # initial counts = a delta against an all-zero model
         self.vbeta = self.vocab * cfg.beta
 
-    def _sparse(self) -> bool:
-        """Nonzero-only push / pull: the count scan costs a pass over the slab, so it pays
-        only when the dense rows would cross xGMI and are mostly zero (large K)."""
-        m = self.cfg.sparse_comm
-        if m == "auto":
-            return self.get_num_workers() > 1 and self.Kp >= 4096
-        return m == "on"  # default off: see LDAConfig.sparse_comm
+    # link / HBM model for the auto choice: all-to-all bytes spread over min(P-1, 7) xGMI
+    # links at a practical ~100 GB/s each; HBM passes at ~4 TB/s (read + write streams)
+    A2A_LINK_BPS = 100e9
+    HBM_BPS = 4e12
+
+    def _sparse_plan(self, word: torch.Tensor):
+        """Build the fixed-layout sparse push/pull plan (``parallel.sparse_ps``) unless
+        ``sparse_comm`` is "off", K exceeds the codec's row limit, or (``auto``) the
+        modelled time of the dense block path is lower. Collective; every rank decides
+        from allreduced estimates, so all take the same path."""
+        from ..ops.rowcodec import MAX_K
+        from ..parallel.sparse_ps import SparseRowPS
+
+        cfg = self.cfg
+        mode = cfg.sparse_comm
+        if mode not in ("on", "off", "auto"):
+            raise ValueError(f"sparse_comm={mode!r}: expected on, off or auto")
+        P, B, Kp = self.get_num_workers(), self.B, self.Kp
+        if mode == "off" or Kp > MAX_K or Kp % 4:
+            return None
+        self.touched, tok = torch.unique(word, return_counts=True)
+        ps = SparseRowPS(self.comm, self.touched, tok, lambda i: (i // B) % P, lambda i: (i // B) // P * B + i % B,
+                         Kp, self.device)
+        if mode == "on":
+            return ps
+        pull_b, push_b = ps.bytes_per_call(remote_only=True)
+        row_b = Kp * 4
+        nblk = len(self.need)
+        dense_remote = 2 * nblk * B * row_b * (P - 1) / P
+        links = max(1, min(P - 1, 7))
+        t_dense = dense_remote / (self.A2A_LINK_BPS * links) + 7 * nblk * B * row_b / self.HBM_BPS
+        t_sparse = (pull_b + push_b) / (self.A2A_LINK_BPS * links) + 3 * self.touched.numel() * row_b / self.HBM_BPS
+        est = torch.tensor([t_dense - t_sparse], dtype=torch.float64, device=self.device)
+        if P > 1:
+            self.comm.all_reduce(est)
+        self.comm_model = {"t_dense_s": t_dense, "t_sparse_s": t_sparse, "sparse_bytes": pull_b + push_b,
+                           "dense_bytes": int(dense_remote)}
+        return ps if float(est.item()) > 0 else None
+
+    def _glob_rows(self) -> torch.Tensor:
+        return self.glob.buffer.view(-1, self.Kp)
+
+    @property
+    def comm_mode(self) -> str:
+        return "local" if self.local_server else ("sparse" if self.ps is not None else "dense")
 
     def _push_delta(self) -> None:
-        # sparse: only the nonzero count changes travel (<= 2 per resampled token, 12 B each)
-        if not self.push("lda", "push-model", self.want_pt, self.glob, None, sparse=self._sparse()):
+        if not self.push("lda", "push-model", self.want_pt, self.glob, None):
             raise IOError("push failed")
 
     def _pull(self) -> torch.Tensor:
-        sparse = self._sparse()
-        if sparse:
-            self.pull_buf.zero_()  # a sparse pull combines nonzeros into zeroed rows
-        # dense: every needed block has an owner, so the overwrite pull rewrites all of them
-        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, sparse=sparse, overwrite=not sparse):
+        # every needed block has an owner, so the overwrite pull rewrites all of them
+        if not self.pull("lda", "pull-model", self.want_pt, self.glob, True, overwrite=True):
             raise IOError("pull failed")
         return self.pull_buf.view(-1, self.Kp)
 
+    def _timed_ps(self, kind: str, fn, nbytes: int) -> None:
+        with self.metrics.time_collective(kind, "lda", f"{kind}-model", nbytes if self.get_num_workers() > 1 else 0,
+                                          self.device):
+            fn()
+
     def iterate(self, it: int) -> int:
         cfg = self.cfg
+        seed = (cfg.seed << 40) ^ (it << 20) ^ 0x5A
         if self.local_server:
             n = self.tz.numel()
             if n:
                 d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, self.pull_buf.view(-1, self.Kp),
-                                 self.nk, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
-                                 (cfg.seed << 40) ^ (it << 20) ^ 0x5A, self.doc_index)
+                                 self.nk, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index)
                 self.nk += d
             return n
-        slab = self._pull()
-        self.before.copy_(self.pull_buf)
-        before = self.before.view(-1, self.Kp)
+        if self.ps is not None:
+            pull_b, push_b = self.ps.bytes_per_call(remote_only=True)
+            self._timed_ps("pull", lambda: self.ps.pull(self._glob_rows(), self.pull_buf), pull_b)
+            slab = self.pull_buf
+        else:
+            slab = self._pull()
+            self.before.copy_(self.pull_buf)
         n = self.tz.numel()
         if n:
             d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, slab, self.nk,
-                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, (cfg.seed << 40) ^ (it << 20) ^ 0x5A,
-                             self.doc_index)
+                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index)
         else:
             d = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
-        slab -= before
-        self._push_delta()
+        if self.ps is not None:
+            self._timed_ps("push", lambda: self.ps.push(self.pull_buf, self._glob_rows()), push_b)
+        else:
+            slab -= self.before.view(-1, self.Kp)
+            self._push_delta()
         if self.get_num_workers() > 1:
             d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
         self.nk += d
         return n
+
+    def _after_iteration(self, it: int) -> None:
+        if self.ps is not None:
+            self.ps.check_overflow()
+        super()._after_iteration(it)
 
     def log_likelihood(self, it: int) -> float:
         cfg = self.cfg
@@ -522,7 +588,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
             self._after_iteration(it)
         self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start,
-                       "local_server": self.local_server}
+                       "local_server": self.local_server, "comm_mode": self.comm_mode}
 
     def _state_tables(self, it: int) -> dict:
         from ..utils.checkpoint import blob_table, tensor_table

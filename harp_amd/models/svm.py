@@ -10,9 +10,13 @@ string-concatenating ``HarpStringPlus`` combiner, then de-duplicated in a HashSe
 
 MI355X design: SMO with second-order working-set selection (Fan, Chen & Lin 2005); the
 kernel matrix of the training block is one GEMM (+ fused RBF epilogue) kept resident
-(a 60k-row fp64 Gram is 29 GB — nothing on a 288 GB device), and each SMO step is a few
-vectorised reductions over it. The cascade keeps the reference's wire format: SV lines
-travel through the generic (variable-length Writable) allreduce path.
+(a 60k-row fp64 Gram is 29 GB — nothing on a 288 GB device). On the GPU the whole solve
+runs in ``csrc/svm.hip`` (:func:`smo_device`): one 1024-thread workgroup per binary
+machine with the gradient in registers, no host round trip per SMO step, and the
+K(K-1)/2 one-vs-one machines of a multiclass problem trained concurrently in ONE launch
+over the shared Gram matrix. The PyTorch loop below is the CPU path and the oracle. The
+cascade keeps the reference's wire format: SV lines travel through the generic
+(variable-length Writable) allreduce path.
 """
 from __future__ import annotations
 
@@ -21,6 +25,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..core.combiner import PartitionCombiner, PartitionStatus
+from ..ops import _lib
 from ..core.table import Table
 from ..core.writable import DataInput, DataOutput, Writable
 from ..parallel import collectives as CL
@@ -36,13 +41,58 @@ def kernel_matrix(X, Y, kernel: str = "linear", sigma: float = 1.0, k: float = 1
     raise ValueError(kernel)
 
 
+_lib.register({
+    "harp_svm_max_rows": [],
+    # K, ldk, ids, moff, nm, max_n, y, kd, a, g, iters, C, eps, tau, max_iter, stream
+    "harp_svm_smo": [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p,
+                     _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_double, _lib.c_double,
+                     _lib.c_double, _lib.c_int, _lib.c_void_p],
+})
+
+
+def native_smo_ok(K: torch.Tensor, n: int) -> bool:
+    """The device solver takes fp64 GPU Gram matrices with <= harp_svm_max_rows() rows per machine."""
+    return (K.device.type == "cuda" and K.dtype == torch.float64 and K.dim() == 2 and K.stride(1) == 1
+            and _lib.use_native(K) and 0 < n <= int(_lib.kernels().harp_svm_max_rows()))
+
+
+def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Tensor]], C: float, eps: float,
+               tau: float, max_iter: int) -> List[Tuple[torch.Tensor, torch.Tensor, int]]:
+    """Train every binary machine ``(idx, y)`` (rows / columns ``idx`` of the fp64 Gram
+    ``K``, labels +-1) with the device SMO, all machines in one launch. Returns per
+    machine (alpha, gradient G = Q alpha - e, SMO steps)."""
+    dev = K.device
+    idx = [m[0].to(dev, torch.int32) for m in machines]
+    ys = [m[1].to(dev, torch.float64).reshape(-1) for m in machines]
+    sizes = [int(i.numel()) for i in idx]
+    moff = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0).tolist()), dtype=torch.int64, device=dev)
+    ids = torch.cat(idx).contiguous()
+    y = torch.cat(ys).contiguous()
+    kd = torch.diagonal(K)[ids.long()].contiguous()
+    a = torch.zeros_like(y)
+    g = -torch.ones_like(y)
+    iters = torch.zeros(len(machines), dtype=torch.int32, device=dev)
+    st = _lib.kernels().harp_svm_smo(K.data_ptr(), K.stride(0), ids.data_ptr(), moff.data_ptr(), len(machines),
+                                     max(sizes), y.data_ptr(), kd.data_ptr(), a.data_ptr(), g.data_ptr(),
+                                     iters.data_ptr(), float(C), float(eps), float(tau), int(max_iter),
+                                     _lib.stream_ptr(dev))
+    _lib.check(st, "svm_smo")
+    it = iters.tolist()
+    out, o = [], 0
+    for k, n in enumerate(sizes):
+        out.append((a[o:o + n], g[o:o + n], it[k]))
+        o += n
+    return out
+
+
 class BinarySVM:
     """C-SVC trained by SMO with WSS-2; labels in {-1, +1} (or {0,1} mapped)."""
 
     def __init__(self, C: float = 1.0, kernel: str = "linear", sigma: float = 1.0, accuracy_threshold: float = 1e-3,
-                 tau: float = 1e-6, max_iterations: int = 100000):
+                 tau: float = 1e-6, max_iterations: int = 100000, solver: str = "auto"):
         self.C, self.kernel, self.sigma = C, kernel, sigma
         self.eps, self.tau, self.max_iter = accuracy_threshold, tau, max_iterations
+        self.solver = solver  # "auto": the device SMO for GPU Gram matrices; "torch": the oracle loop
 
     def fit(self, X: torch.Tensor, y: torch.Tensor, K: Optional[torch.Tensor] = None) -> "BinarySVM":
         Xd = X.double() if not (X.is_sparse or X.layout == torch.sparse_csr) else X.double()
@@ -51,6 +101,10 @@ class BinarySVM:
             yv = 2 * yv - 1
         n = yv.numel()
         K = kernel_matrix(Xd, Xd, self.kernel, self.sigma) if K is None else K.double()
+        if self.solver != "torch" and native_smo_ok(K, n):
+            ar = torch.arange(n, device=K.device)
+            a, G, steps = smo_device(K.contiguous(), [(ar, yv)], self.C, self.eps, self.tau, self.max_iter)[0]
+            return self._finish(Xd, yv, a, G, steps)
         Kd = torch.diagonal(K).clone()
         a = torch.zeros(n, dtype=torch.float64, device=K.device)
         G = -torch.ones(n, dtype=torch.float64, device=K.device)
@@ -84,7 +138,14 @@ class BinarySVM:
             a[j] += daj
             # G += Q[:, i] dai + Q[:, j] daj,  Q = y y^T K
             G += yv * (yi * dai * K[i] + yj * daj * K[j])
-        self.n_iterations = it + 1
+        return self._finish(Xd, yv, a, G, it)
+
+    def _finish(self, Xd, yv, a, G, steps: int) -> "BinarySVM":
+        """Bias from the free SVs (or the violating-pair midpoint) and the SV set."""
+        Cc = self.C
+        pos = yv > 0
+        self.n_iterations = steps + 1
+        self.alpha, self.grad = a, G
         free = (a > 1e-12) & (a < Cc - 1e-12)
         yG = yv * G
         if bool(free.any()):
@@ -102,6 +163,10 @@ class BinarySVM:
         self.sv = Xd.to_dense()[sv] if (Xd.is_sparse or Xd.layout == torch.sparse_csr) else Xd[sv]
         self.coef = (a * yv)[sv]
         return self
+
+    def dual_objective(self) -> float:
+        """0.5 a^T Q a - e^T a = 0.5 a^T (G - e) with G = Q a - e."""
+        return float(0.5 * (self.alpha * (self.grad - 1.0)).sum())
 
     def decision(self, X):
         Kx = kernel_matrix(X.double(), self.sv, self.kernel, self.sigma)
@@ -124,13 +189,23 @@ class MultiClassSVM:
         Xd = X.double()
         Kfull = kernel_matrix(Xd, Xd, self.kw.get("kernel", "linear"), self.kw.get("sigma", 1.0))
         Xdense = Xd.to_dense() if (Xd.is_sparse or Xd.layout == torch.sparse_csr) else Xd
+        pairs = []
         for a in range(self.K):
             for b in range(a + 1, self.K):
                 idx = torch.nonzero((yl == a) | (yl == b)).reshape(-1)
                 if idx.numel() == 0:
                     continue
-                yy = torch.where(yl[idx] == a, 1.0, -1.0).double()
-                self.machines[(a, b)] = BinarySVM(**self.kw).fit(Xdense[idx], yy, Kfull[idx][:, idx])
+                pairs.append(((a, b), idx, torch.where(yl[idx] == a, 1.0, -1.0).double()))
+        if pairs and self.kw.get("solver", "auto") != "torch" and native_smo_ok(Kfull, max(p[1].numel() for p in pairs)):
+            # all one-vs-one machines in ONE device launch over the shared Gram matrix
+            proto = BinarySVM(**self.kw)
+            res = smo_device(Kfull.contiguous(), [(idx, yy) for _, idx, yy in pairs], proto.C, proto.eps, proto.tau,
+                             proto.max_iter)
+            for (key, idx, yy), (al, G, steps) in zip(pairs, res):
+                self.machines[key] = BinarySVM(**self.kw)._finish(Xdense[idx], yy.to(al.device), al, G, steps)
+            return self
+        for key, idx, yy in pairs:
+            self.machines[key] = BinarySVM(**self.kw).fit(Xdense[idx], yy, Kfull[idx][:, idx])
         return self
 
     def predict(self, X):

@@ -35,6 +35,11 @@ _lib.register({
     # rows, cols, vals, off, win, r, steps, chunk, blocks_per_xcd, variant, W, ldw, H, ldh, lr, lam, stream
     "harp_mf_sgd_xcd": [_lib.c_void_p] * 5 + [_lib.c_int] * 5 + [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
                                                                  _lib.c_float, _lib.c_float, _lib.c_void_p],
+    # rows, cols, vals, off, win, r, steps, chunk, blocks_per_xcd, W, ldw, H, ldh, lr, lam, ws, stream
+    "harp_mf_sgd_xcd_flow": [_lib.c_void_p] * 5 + [_lib.c_int] * 4 + [_lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                                                                    _lib.c_int, _lib.c_float, _lib.c_float,
+                                                                    _lib.c_void_p, _lib.c_void_p],
+    "harp_mf_flow_ws_ints": [],
     "harp_mf_rmse_blocks": [],
     "harp_mf_rmse": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int,
                      _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
@@ -55,6 +60,32 @@ def _rt():
         rt.harp_mf_sse_cpu.restype = ctypes.c_double
         rt._mf_bound = True
     return rt
+
+
+# variant 1 = one persistent launch per slice pass ordered by neighbour completion flags
+# (mf_sgd_xcd_flow_kernel) instead of one launch per sub-step; ranks <= 256
+FLOW_VARIANT = 1
+_FLOW_WS: dict = {}
+
+
+def _flow_ws(device: torch.device) -> torch.Tensor:
+    """Zeroed int32 workspace of the flow kernel, one per (device, stream): the launch leaves
+    it zeroed again, so launches on one stream reuse it (kernels on a stream serialise)."""
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
+    ws = _FLOW_WS.get(key)
+    if ws is None:
+        n = int(_lib.kernels().harp_mf_flow_ws_ints())
+        ws = _FLOW_WS[key] = torch.zeros(n, dtype=torch.int32, device=device)
+    return ws
+
+
+def check_flow_errors(device: torch.device) -> None:
+    """Raise if a flow launch on ``device`` gave up waiting on a neighbour (host sync)."""
+    for (idx, _), ws in _FLOW_WS.items():
+        if idx == device.index and int(ws[-1].item()):
+            ws[-1].zero_()
+            raise RuntimeError("MF-SGD flow kernel: a cross-XCD wait timed out (results of that pass are invalid)")
 
 
 def _check(rows, cols, vals, W, H):
@@ -134,7 +165,8 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
     ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path).
     ``chunk``: ratings per stream (8, 16, 32, 64 or 128 on the GPU; <= 0 = :func:`auto_chunk`);
-    ``variant``: must be 0 (the measured alternatives are no longer built; csrc/mf_sgd.hip).
+    ``variant``: 0 = one launch per sub-step; 1 (:data:`FLOW_VARIANT`, ranks <= 256) = the
+    whole pass in one persistent launch ordered by per-XCD completion flags.
     ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
     ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
     CPU only: ``threads > 1`` or a ``time_budget`` (s) run the cells through the 2-D
@@ -158,11 +190,17 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
         if chunk <= 0:  # wide ranks (one wave per stream) take 32 / 64 / 128 only
             chunk = auto_chunk(trained, blocks_per_xcd) if r <= 256 else max(32, auto_chunk(trained, blocks_per_xcd))
         lib = _lib.kernels()
-        st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
-                                 _lib.ptr(win), r, nb, chunk,
-                                 blocks_per_xcd, variant, W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr),
-                                 float(lam), _lib.stream_ptr(W.device))
-        _lib.check(st, "mf_sgd_xcd")
+        if variant == FLOW_VARIANT and r <= 256:
+            st = lib.harp_mf_sgd_xcd_flow(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
+                                          _lib.ptr(win), r, nb, chunk, blocks_per_xcd, W.data_ptr(), W.stride(0),
+                                          H.data_ptr(), H.stride(0), float(lr), float(lam),
+                                          _flow_ws(W.device).data_ptr(), _lib.stream_ptr(W.device))
+            _lib.check(st, "mf_sgd_xcd_flow")
+        else:
+            st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
+                                     _lib.ptr(win), r, nb, chunk, blocks_per_xcd, 0, W.data_ptr(), W.stride(0),
+                                     H.data_ptr(), H.stride(0), float(lr), float(lam), _lib.stream_ptr(W.device))
+            _lib.check(st, "mf_sgd_xcd")
         if win is not None:
             win.record_stream(torch.cuda.current_stream(W.device))
         return trained

@@ -1,0 +1,163 @@
+"""Sparse row codec for parameter-server push / pull (``csrc/rowcodec.hip``).
+
+Count-table rows (LDA word-topic) travel as fixed-size per-row SLOTS whose capacity is a
+token bound that never changes while sampling, so sender and receiver derive the same
+layout once and every call is a fixed-size all-to-all with no size exchange (no host
+sync). A slot is ``[int32 nnz][int32 counts cap][uint16 topics cap]`` or, when that is
+not smaller, the dense row (``cap = -1``); every slot starts 16-byte aligned.
+
+Reference: contrib/src/main/java/edu/iu/lda/LDAMapperDyn.java (push :380, pull :429)
+moving sparse ``TopicCountList`` rows (ml/java/src/main/java/edu/iu/lda/LDAUtil.java:159-213).
+
+GPU tensors use the HIP kernels (mandatory on a GPU); CPU tensors use the PyTorch
+implementation below, which is also the oracle of the GPU tests.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+_lib.register({
+    "harp_rowcodec_encode": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                             _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                             _lib.c_void_p],
+    "harp_rowcodec_decode": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                             _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p],
+})
+
+ALIGN = 16
+MAX_K = 16384  # LDS row limit of the kernels (one 64 KB workgroup row)
+
+
+def slot_caps(bound: torch.Tensor, K: int) -> torch.Tensor:
+    """Per-row slot capacity from a nonzero bound: min(K, bound), or -1 (dense slot) when
+    the sparse slot would not be smaller than the dense row."""
+    c = bound.clamp(min=0, max=K).to(torch.int64)
+    return torch.where(4 + 6 * c >= 4 * K, torch.full_like(c, -1), c)
+
+
+def slot_sizes(caps: torch.Tensor, K: int) -> torch.Tensor:
+    """Bytes of each slot (16-aligned)."""
+    raw = torch.where(caps < 0, torch.full_like(caps, 4 * K), 4 + 6 * caps.clamp_min(0))
+    return (raw + ALIGN - 1) // ALIGN * ALIGN
+
+
+def layout(caps: torch.Tensor, K: int, base: int = 0) -> Tuple[torch.Tensor, int]:
+    """(slot byte offsets from ``base``, total bytes) of consecutive slots."""
+    sz = slot_sizes(caps, K)
+    off = torch.cumsum(sz, 0) - sz + base
+    return off, int(sz.sum().item())
+
+
+def _check_args(t: torch.Tensor, K: int) -> None:
+    if t.dtype != torch.int32 or t.dim() != 2 or t.shape[1] < K or t.stride(1) != 1:
+        raise ValueError(f"rowcodec needs an int32 [rows, >=K] table, got {tuple(t.shape)} {t.dtype}")
+    if K <= 0 or K % 4 or K > MAX_K:
+        raise ValueError(f"rowcodec needs 0 < K <= {MAX_K}, K % 4 == 0 (got {K})")
+
+
+def _dense_rows(buf: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, K: int) -> torch.Tensor:
+    """Decode every slot into dense rows [n, K] (CPU oracle)."""
+    n = off.numel()
+    out = torch.zeros((n, K), dtype=torch.int32, device=buf.device)
+    if n == 0:
+        return out
+    w32 = buf.view(torch.int32)
+    w16 = buf.view(torch.int16)
+    dense = cap < 0
+    if bool(dense.any()):
+        d = torch.nonzero(dense).flatten()
+        idx = (off[d] // 4)[:, None] + torch.arange(K, device=buf.device)[None, :]
+        out[d] = w32[idx]
+    sp = torch.nonzero(~dense).flatten()
+    if sp.numel():
+        o, c = off[sp], cap[sp]
+        nnz = w32[o // 4].to(torch.int64).clamp(min=0)
+        nnz = torch.minimum(nnz, c)
+        rows = torch.repeat_interleave(sp, nnz)
+        first = torch.cumsum(nnz, 0) - nnz
+        e = torch.arange(int(nnz.sum()), device=buf.device) - torch.repeat_interleave(first, nnz)
+        ro, rc = torch.repeat_interleave(o, nnz), torch.repeat_interleave(c, nnz)
+        cnt = w32[(ro + 4 + 4 * e) // 4]
+        top = w16[(ro + 4 + 4 * rc + 2 * e) // 2].to(torch.int64) & 0xFFFF
+        ok = top < K
+        out[rows[ok], top[ok]] = cnt[ok]
+    return out
+
+
+def encode(src: torch.Tensor, K: int, rows: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, out: torch.Tensor,
+           overflow: torch.Tensor, before: Optional[torch.Tensor] = None, b_off: Optional[torch.Tensor] = None,
+           b_cap: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Slot j of ``out`` := row ``src[rows[j], :K]`` (minus the row decoded from slot j of
+    ``before`` when given: a count delta against the pulled snapshot). Entries past a
+    slot's capacity are dropped and flag ``overflow``. ``rows`` int32, ``off`` int64
+    byte offsets, ``cap`` int32 (-1 = dense slot)."""
+    _check_args(src, K)
+    n = rows.numel()
+    if n == 0:
+        return out
+    if _lib.use_native(src):
+        for t in (rows, off, cap, out, overflow) + ((before, b_off, b_cap) if before is not None else ()):
+            assert t.device == src.device and t.is_contiguous()
+        assert rows.dtype == torch.int32 and off.dtype == torch.int64 and cap.dtype == torch.int32
+        st = _lib.kernels().harp_rowcodec_encode(
+            src.data_ptr(), src.stride(0), K, rows.data_ptr(), n, off.data_ptr(), cap.data_ptr(), out.data_ptr(),
+            _lib.ptr(before), _lib.ptr(b_off), _lib.ptr(b_cap), overflow.data_ptr(), _lib.stream_ptr(src.device))
+        _lib.check(st, "rowcodec_encode")
+        return out
+    vals = src[rows.long(), :K]
+    if before is not None:
+        vals = vals - _dense_rows(before, b_off.long(), b_cap.long(), K)
+    off, cap = off.long(), cap.long()
+    w32, w16 = out.view(torch.int32), out.view(torch.int16)
+    dense = cap < 0
+    if bool(dense.any()):
+        d = torch.nonzero(dense).flatten()
+        w32[(off[d] // 4)[:, None] + torch.arange(K)[None, :]] = vals[d]
+    sp = torch.nonzero(~dense).flatten()
+    if sp.numel():
+        v = vals[sp]
+        nz = v != 0
+        nnz = nz.sum(1)
+        pos = torch.cumsum(nz.to(torch.int64), 1) - 1
+        r, t = torch.nonzero(nz, as_tuple=True)
+        p = pos[r, t]
+        c = cap[sp][r]
+        keep = p < c
+        if not bool(keep.all()):
+            overflow.fill_(1)
+        r, t, p, c = r[keep], t[keep], p[keep], c[keep]
+        o = off[sp][r]
+        w32[(o + 4 + 4 * p) // 4] = v[r, t]
+        w16[(o + 4 + 4 * c + 2 * p) // 2] = t.to(torch.int16)
+        w32[off[sp] // 4] = torch.minimum(nnz, cap[sp]).to(torch.int32)
+    return out
+
+
+def decode(dst: torch.Tensor, K: int, rows: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, inp: torch.Tensor,
+           add: bool = False) -> torch.Tensor:
+    """Row ``dst[rows[j], :K]`` := slot j of ``inp`` (``add``: += instead; rows may repeat
+    and then all add)."""
+    _check_args(dst, K)
+    n = rows.numel()
+    if n == 0:
+        return dst
+    if _lib.use_native(dst):
+        for t in (rows, off, cap, inp):
+            assert t.device == dst.device and t.is_contiguous()
+        assert rows.dtype == torch.int32 and off.dtype == torch.int64 and cap.dtype == torch.int32
+        st = _lib.kernels().harp_rowcodec_decode(dst.data_ptr(), dst.stride(0), K, rows.data_ptr(), n, off.data_ptr(),
+                                                 cap.data_ptr(), inp.data_ptr(), 1 if add else 0,
+                                                 _lib.stream_ptr(dst.device))
+        _lib.check(st, "rowcodec_decode")
+        return dst
+    vals = _dense_rows(inp, off.long(), cap.long(), K)
+    r = rows.long()
+    if add:
+        dst[:, :K].index_add_(0, r, vals)
+    else:
+        dst[r, :K] = vals
+    return dst

@@ -23,7 +23,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-chunk", type=int, default=0, help="tokens per word chunk (0: LDAConfig default)")
     ap.add_argument("--strategy", default="rotation", choices=["rotation", "push_pull"])
-    ap.add_argument("--sparse-comm", default="off", choices=["auto", "on", "off"])
+    ap.add_argument("--sparse-comm", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--local-server", default="on", choices=["on", "off"],
+                    help="push_pull at P=1: off runs the pull / push collectives even on one rank")
     a = ap.parse_args()
     import torch
 
@@ -38,7 +40,7 @@ def main():
     toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
     gen = time.perf_counter() - t0
     cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters,
-                    sparse_comm=a.sparse_comm)
+                    sparse_comm=a.sparse_comm, local_server=a.local_server == "on")
     if a.max_chunk:
         cfg.max_chunk = a.max_chunk
     cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper
@@ -64,6 +66,24 @@ def main():
     comm.barrier()
     dt = time.perf_counter() - t0
     ll = m.log_likelihood(a.warmup + a.iters)
+    extra = {"comm_mode": getattr(m, "comm_mode", "rotation")}
+    if getattr(m, "ps", None) is not None:  # sparse push/pull: codec + exchange time per call
+        ps = m.ps
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        reps = 10
+        ev[0].record()
+        for _ in range(reps):
+            ps.pull(m._glob_rows(), m.pull_buf)
+        ev[1].record()
+        for _ in range(reps):
+            ps.push(m.pull_buf, m._glob_rows())  # zero deltas: same payload work as a real push
+        ev[2].record()
+        ev[2].synchronize()
+        pb, qb = ps.bytes_per_call(remote_only=False)
+        extra.update({"pull_ms": ev[0].elapsed_time(ev[1]) / reps, "push_ms": ev[1].elapsed_time(ev[2]) / reps,
+                      "pull_payload_bytes": pb, "push_payload_bytes": qb, "rows": ps.n_rows,
+                      "dense_rows_bytes": ps.n_rows * m.Kp * 4})
+        ps.check_overflow()
     tot = torch.tensor([float(n)], dtype=torch.float64, device=comm.device)
     if comm.world_size > 1:
         comm.all_reduce(tot)
@@ -73,7 +93,7 @@ def main():
                           "docs": nd, "vocab": V, "topics": a.topics, "tokens": int(tot.item()) // a.iters,
                           "sampler": "sparse" if m.doc_index is not None else "dense",
                           "sparse_waves": L.SPARSE_WAVES, "max_chunk": L.max_chunk(cfg.max_chunk, m.sparse),
-                          "chunk_order": os.environ.get("HARP_LDA_ORDER", "lpt"), "loglik_init": ll0, "loglik_end": ll, "init_s": init_s, "gen_s": gen}), flush=True)
+                          "chunk_order": os.environ.get("HARP_LDA_ORDER", "lpt"), "loglik_init": ll0, "loglik_end": ll, "init_s": init_s, "gen_s": gen, **extra}), flush=True)
     shutdown()
 
 

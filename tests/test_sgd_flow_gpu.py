@@ -1,0 +1,60 @@
+"""MF-SGD persistent flow kernel (one launch per slice pass, cross-XCD completion flags,
+csrc/mf_sgd.hip mf_sgd_xcd_flow_kernel) vs the one-launch-per-sub-step kernel."""
+import pytest
+import torch
+
+from harp_amd.models.sgd_mf import SGDConfig, SGDCollectiveMapper, synthetic_ratings
+from harp_amd.ops import mf as MF
+from harp_amd.parallel.comm import Communicator
+from harp_amd.runtime.mapper import KeyValReader
+
+pytestmark = pytest.mark.gpu
+
+
+def _train(cuda, variant, epochs=6, slices=4, fraction=1.0, n=600000):
+    nu, ni = 20000, 3000
+    u, i, v = synthetic_ratings(nu, ni, n, seed=5)
+    cfg = SGDConfig(rank=128, epochs=epochs, test_every=0, num_slices=slices, kernel_variant=variant, chunk=0,
+                    train_fraction=fraction, lr=0.005)
+    m = SGDCollectiveMapper(Communicator(None, cuda), cfg, nu, ni, (u, i, v), None)
+    m.init_model(KeyValReader([]))
+    trained = sum(m.train_epoch(ep) for ep in range(epochs))
+    m.rot.wait_all()
+    torch.cuda.synchronize()
+    MF.check_flow_errors(cuda)
+    rmse, _ = m._eval_ring(epochs - 1)
+    return trained, rmse
+
+
+def test_flow_matches_per_substep_launches(cuda):
+    t0, r0 = _train(cuda, 0)
+    t1, r1 = _train(cuda, MF.FLOW_VARIANT)
+    assert t0 == t1
+    assert abs(r1 - r0) / r0 < 0.005, (r0, r1)
+
+
+def test_flow_windows_and_workspace_reuse(cuda):
+    """Fixed-fraction windows take the same path; many launches on one stream reuse the
+    self-resetting workspace."""
+    t0, r0 = _train(cuda, 0, epochs=8, fraction=0.5)
+    t1, r1 = _train(cuda, MF.FLOW_VARIANT, epochs=8, fraction=0.5)
+    assert t0 == t1
+    assert abs(r1 - r0) / r0 < 0.01, (r0, r1)
+    ws = [w for (d, _), w in MF._FLOW_WS.items() if d == cuda.index]
+    assert ws and all(int(w.abs().sum()) == 0 for w in ws)
+
+
+def test_flow_empty_cells(cuda):
+    """Cells with no ratings complete at once (no wait on them can hang)."""
+    W = torch.rand(64, 128, device=cuda)
+    H = torch.rand(64, 128, device=cuda)
+    rows = torch.arange(32, dtype=torch.int32, device=cuda)
+    cols = torch.arange(32, dtype=torch.int32, device=cuda)
+    vals = torch.full((32,), 3.0, device=cuda)
+    off = torch.zeros(65, dtype=torch.int64)
+    off[1:] = 32  # all ratings in cell 0, the other 63 cells empty
+    n = MF.sgd_update_blocked(rows, cols, vals, off.to(cuda), W, H, 0.01, 0.05, chunk=8, blocks_per_xcd=4,
+                              host_off=off.tolist(), variant=MF.FLOW_VARIANT)
+    torch.cuda.synchronize()
+    MF.check_flow_errors(cuda)
+    assert n == 32
