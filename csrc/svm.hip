@@ -20,7 +20,9 @@
 // a > 0, y > 0) in three bit masks, so a step touches global memory only for the two
 // kernel rows (gathered through the machine's index list from the shared Gram matrix,
 // L2/HBM) and the diagonal. Three block reductions per step (i; j; the broadcast of the
-// update). n <= 1024 * 32 per machine.
+// update). n <= 1024 * 32 per machine. Measured (profiles/r3_svm): the first form, with the
+// gradient in global memory and one element's gathers in flight at a time, spent ~44 us per
+// step at n = 20k in serialized memory round trips.
 #include "common.h"
 
 namespace {
@@ -60,9 +62,14 @@ __device__ __forceinline__ double wave_min(double v) {
   return v;
 }
 
-// GREG: the gradient lives in registers (EPT <= 8: <= 110 VGPRs at 1024 threads); else in
-// the machine's slice of g (L2-resident, 8n bytes) -- the 16 / 32-element forms spilled.
-template <int EPT, bool GREG = (EPT <= 8)>
+// Thread t owns elements t + 1024 k (k < EPT): gradient G, the machine-local column index
+// (IDENT: the machine is the whole matrix, column = element) and three box-state bit masks
+// in registers. Loops over k are fully unrolled so every gather of a phase is in flight at
+// once (one memory round trip per phase, not one per element); a scheduling barrier every
+// GRP elements bounds how many are in flight, and with them the register use.
+constexpr int GRP = 8;
+
+template <int EPT, bool IDENT>
 __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict__ Kfull, long ldk,
                                                        const int* __restrict__ ids_all, const long* __restrict__ moff,
                                                        const double* __restrict__ y_all,
@@ -80,45 +87,51 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
   const double* y = y_all + base;
   const double* kd = kd_all + base;
   double* a = a_all + base;
+  double* g = g_all + base;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const double NEG = -__builtin_inf(), POS = __builtin_inf();
 
-  double G[GREG ? EPT : 1];
-  double* g = g_all + base;
+  double G[EPT];
+  int col[IDENT ? 1 : EPT];
   unsigned ypos = 0, ltC = 0, gt0 = 0;  // bit k: element tid + 1024 k
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int t = tid + kThreads * k;
-    if constexpr (GREG) G[k] = -1.0;
+    G[k] = -1.0;
+    if constexpr (!IDENT) col[k] = 0;
     if (t < n) {
       const double at = a[t];
       if (y[t] > 0) ypos |= 1u << k;
       if (at < C) ltC |= 1u << k;
       if (at > 0) gt0 |= 1u << k;
-      if constexpr (GREG) G[k] = g[t];
+      G[k] = g[t];
+      if constexpr (!IDENT) col[k] = ids[t];
     }
   }
-#define GK(k, t) (GREG ? G[GREG ? (k) : 0] : g[t])
-  constexpr int UNR = GREG ? EPT : 4;  // register form: full unroll (static G indices)
+#define COL(k, t) (IDENT ? (t) : col[IDENT ? 0 : (k)])
   int it = 0;
   for (; it < max_iter; ++it) {
-    // ---- i = argmax over I_up of mg = -y G; Mv = min over I_low of mg
+    // an opaque copy of the thread id: keeps the per-element addresses from being hoisted
+    // out of the step loop (EPT x 64-bit registers each) -- they are cheap to recompute
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    // ---- i = argmax over I_up of mg = -y G; Mv = min over I_low of mg (registers only)
     double bv = NEG, lo = POS;
     int bi = 0x7fffffff;
-#pragma unroll UNR
+#pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int t = tid + kThreads * k;
-      if (t >= n) continue;
-      const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
-      const double gk = GK(k, t);
-      const double mg = yp ? -gk : gk;
-      const bool up = (yp && lc) || (!yp && g0);
-      const bool low = (yp && g0) || (!yp && lc);
-      if (up && better_max(mg, t, bv, bi)) {
-        bv = mg;
-        bi = t;
+      if (t < n) {
+        const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
+        const double mg = yp ? -G[k] : G[k];
+        const bool up = (yp && lc) || (!yp && g0);
+        const bool low = (yp && g0) || (!yp && lc);
+        if (up && better_max(mg, t, bv, bi)) {
+          bv = mg;
+          bi = t;
+        }
+        if (low) lo = fmin(lo, mg);
       }
-      if (low) lo = fmin(lo, mg);
     }
     wave_arg<true>(bv, bi);
     lo = wave_min(lo);
@@ -144,26 +157,29 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     const int i = s_ic[0];
     if (!(mval - Mv >= eps) || i >= n) break;  // converged (or no candidate: NaN-safe)
     // ---- j: second-order selection over K row i
-    const double* Ki = Kfull + (long)ids[i] * ldk;
+    const double* Ki = Kfull + (long)(IDENT ? i : ids[i]) * ldk;
     const double kii = kd[i];
     double sv = POS;
     int sj = 0x7fffffff;
-#pragma unroll UNR
+#pragma unroll
     for (int k = 0; k < EPT; ++k) {
+      if (k && k % GRP == 0) __builtin_amdgcn_sched_barrier(0);
       const int t = tid + kThreads * k;
-      if (t >= n) continue;
-      const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
-      const double gk = GK(k, t);
-      const double mg = yp ? -gk : gk;
-      const bool low = (yp && g0) || (!yp && lc);
-      if (!(low && mg < mval)) continue;
-      const double bt = __dsub_rn(mval, mg);
-      double at = __dsub_rn(__dadd_rn(kii, kd[t]), __dmul_rn(2.0, Ki[ids[t]]));
-      if (!(at > 0)) at = tau;
-      const double sc = -__ddiv_rn(__dmul_rn(bt, bt), at);
-      if (better_min(sc, t, sv, sj)) {
-        sv = sc;
-        sj = t;
+      if (t < n) {
+        const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
+        const double mg = yp ? -G[k] : G[k];
+        const bool low = (yp && g0) || (!yp && lc);
+        const double kit = Ki[COL(k, t)], kdt = kd[t];
+        if (low && mg < mval) {
+          const double bt = __dsub_rn(mval, mg);
+          double at = __dsub_rn(__dadd_rn(kii, kdt), __dmul_rn(2.0, kit));
+          if (!(at > 0)) at = tau;
+          const double sc = -__ddiv_rn(__dmul_rn(bt, bt), at);
+          if (better_min(sc, t, sv, sj)) {
+            sv = sc;
+            sj = t;
+          }
+        }
       }
     }
     wave_arg<false>(sv, sj);
@@ -183,18 +199,14 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     if (j >= n) break;  // no admissible j (cannot happen while m - M >= eps)
     // ---- the two owners publish what the update needs
     if (tid == (j & (kThreads - 1))) {
-      const int k = j / kThreads;
+      const int kj = j / kThreads;
       double gj = 0.0;
-      if constexpr (GREG) {
 #pragma unroll
-        for (int q = 0; q < EPT; ++q)
-          if (q == k) gj = G[q];
-      } else {
-        gj = g[j];
-      }
-      const bool yp = (ypos >> k) & 1;
+      for (int q = 0; q < EPT; ++q)
+        if (q == kj) gj = G[q];
+      const bool yp = (ypos >> kj) & 1;
       const double mg = yp ? -gj : gj;
-      double at = __dsub_rn(__dadd_rn(kii, kd[j]), __dmul_rn(2.0, Ki[ids[j]]));
+      double at = __dsub_rn(__dadd_rn(kii, kd[j]), __dmul_rn(2.0, Ki[IDENT ? j : ids[j]]));
       if (!(at > 0)) at = tau;
       s_bc[2] = __dsub_rn(mval, mg);  // bt_j
       s_bc[3] = at;                   // at_j
@@ -213,7 +225,7 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     delta = fmax(0.0, fmin(delta, fmin(lim_i, lim_j)));
     const double dai = __dmul_rn(yi, delta), daj = -__dmul_rn(yj, delta);
     const double nai = __dadd_rn(ai, dai), naj = __dadd_rn(aj, daj);
-    // owners refresh the box bits (i first, then j: i == j cannot happen, j has mg < m)
+    // owners refresh the box bits (i != j: j has mg < m = mg_i)
     if (tid == (i & (kThreads - 1))) {
       const int k = i / kThreads;
       ltC = nai < C ? ltC | (1u << k) : ltC & ~(1u << k);
@@ -228,36 +240,39 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     }
     // ---- G += y (yi dai K_i + yj daj K_j)
     const double ci = __dmul_rn(yi, dai), cj = __dmul_rn(yj, daj);
-    const double* Kj = Kfull + (long)ids[j] * ldk;
-#pragma unroll UNR
+    const double* Kj = Kfull + (long)(IDENT ? j : ids[j]) * ldk;
+#pragma unroll
     for (int k = 0; k < EPT; ++k) {
+      if (k && k % GRP == 0) __builtin_amdgcn_sched_barrier(0);
       const int t = tid + kThreads * k;
-      if (t >= n) continue;
-      const int c = ids[t];
-      const double u = __dadd_rn(__dmul_rn(ci, Ki[c]), __dmul_rn(cj, Kj[c]));
-      const double yt = ((ypos >> k) & 1) ? 1.0 : -1.0;
-      if constexpr (GREG)
+      if (t < n) {
+        const int c = COL(k, t);
+        const double u = __dadd_rn(__dmul_rn(ci, Ki[c]), __dmul_rn(cj, Kj[c]));
+        const double yt = ((ypos >> k) & 1) ? 1.0 : -1.0;
         G[k] = __dadd_rn(G[k], __dmul_rn(yt, u));
-      else
-        g[t] = __dadd_rn(g[t], __dmul_rn(yt, u));
+      }
     }
     __syncthreads();  // s_bc / s_ic are rewritten by the next step
   }
-  if constexpr (GREG) {
-#pragma unroll UNR
-    for (int k = 0; k < EPT; ++k) {
-      const int t = tid + kThreads * k;
-      if (t < n) g[t] = G[k];
-    }
+#undef COL
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int t = tid + kThreads * k;
+    if (t < n) g[t] = G[k];
   }
   if (tid == 0) iters[m] = it;
-#undef GK
 }
 
 template <int EPT>
 int launch_smo(const double* K, long ldk, const int* ids, const long* moff, int nm, const double* y, const double* kd,
-               double* a, double* g, int* iters, double C, double eps, double tau, int max_iter, hipStream_t s) {
-  smo_kernel<EPT><<<dim3(nm), dim3(kThreads), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau, max_iter);
+               double* a, double* g, int* iters, double C, double eps, double tau, int max_iter, bool ident,
+               hipStream_t s) {
+  if (ident)
+    smo_kernel<EPT, true><<<dim3(nm), dim3(kThreads), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau,
+                                                              max_iter);
+  else
+    smo_kernel<EPT, false><<<dim3(nm), dim3(kThreads), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau,
+                                                               max_iter);
   return harp_launch_status();
 }
 
@@ -268,17 +283,20 @@ HARP_EXPORT int harp_svm_max_rows() { return kThreads * 32; }
 // nm binary machines; machine m owns entries [moff[m], moff[m+1]) of ids (row/col indices
 // into the n x ldk fp64 Gram K), y (+-1), kd (the machine's K diagonal), a (alphas, in/out:
 // usually zeros) and g (gradient, in/out: usually -1). max_n = the largest machine.
+// `ident`: one machine whose ids are 0..n-1 (columns need no indirection).
 HARP_EXPORT int harp_svm_smo(const double* K, long ldk, const int* ids, const long* moff, int nm, int max_n,
                              const double* y, const double* kd, double* a, double* g, int* iters, double C, double eps,
-                             double tau, int max_iter, hipStream_t s) {
+                             double tau, int max_iter, int ident, hipStream_t s) {
   if (nm <= 0 || max_n <= 0 || max_n > kThreads * 32 || !(C > 0) || max_iter < 0) return HARP_EBADARG;
+  if (ident && nm != 1) return HARP_EBADARG;
   const int ept = (max_n + kThreads - 1) / kThreads;
-#define SMO(E) return launch_smo<E>(K, ldk, ids, moff, nm, y, kd, a, g, iters, C, eps, tau, max_iter, s)
+#define SMO(E) return launch_smo<E>(K, ldk, ids, moff, nm, y, kd, a, g, iters, C, eps, tau, max_iter, ident != 0, s)
   if (ept <= 1) SMO(1);
   if (ept <= 2) SMO(2);
   if (ept <= 4) SMO(4);
   if (ept <= 8) SMO(8);
   if (ept <= 16) SMO(16);
+  if (ept <= 24) SMO(24);
   SMO(32);
 #undef SMO
 }

@@ -10,9 +10,12 @@ row blocks (hipBLASLt) with the norm terms fused into its epilogue (``addmm`` of
 -2 X Y^T product onto the broadcast norms), so the N x M distance matrix is produced in
 one pass; kNN tiles the query set and keeps a running top-k per tile (no N x M
 materialisation for large M); distributed kNN selects the local top-k on each
-training shard and merges the P candidates with one all-gather. EM's E-step is one
-batched triangular solve per component; sufficient statistics (N_k, sum x, sum x x^T)
-are ONE allreduce per iteration.
+training shard and merges the P candidates with one all-gather. EM on the GPU runs the
+fused HIP E-step (``ops.gmm``: whitened Mahalanobis for all components in registers +
+LDS, log-sum-exp responsibilities in the same kernel) and one GEMM-shaped statistics pass
+(N_k, sum r x, sum r x x^T from the augmented point); on the CPU the E-step is one
+batched triangular solve per component. Either way the sufficient statistics are ONE
+allreduce per iteration.
 """
 from __future__ import annotations
 
@@ -141,10 +144,11 @@ def _max():
 # ---------------------------------------------------------------- EM-GMM
 def em_gmm(X: torch.Tensor, K: int, comm: Optional[Communicator] = None, n_iterations: int = 100,
            accuracy_threshold: float = 1e-6, reg: float = 1e-6, covariance: str = "full",
-           init: Optional[Dict[str, torch.Tensor]] = None, seed: int = 0) -> Dict[str, torch.Tensor]:
+           init: Optional[Dict[str, torch.Tensor]] = None, seed: int = 0, estep: str = "auto") -> Dict[str, torch.Tensor]:
     """EM for a K-component Gaussian mixture (full or diagonal covariance).
     Distributed: each worker holds a row shard; sufficient statistics are allreduced.
-    Stops when the log-likelihood improves by less than ``accuracy_threshold``."""
+    Stops when the log-likelihood improves by less than ``accuracy_threshold``.
+    ``estep``: "auto" (HIP kernels for fp64 GPU data, d <= 64) or "torch"."""
     from ..parallel.partition_util import broadcast_objects
 
     Xd = _dense(X).double()
@@ -166,18 +170,26 @@ def em_gmm(X: torch.Tensor, K: int, comm: Optional[Communicator] = None, n_itera
     prev = -math.inf
     ll = prev
     it = 0
+    from ..ops import gmm as GM
+
+    native = GM.usable(Xd) and estep != "torch"
     for it in range(n_iterations):
-        logp = _log_gauss(Xd, mu, cov, covariance) + torch.log(w)[None, :]
-        lse = torch.logsumexp(logp, 1)
-        R = torch.exp(logp - lse[:, None])  # [n, K]
-        Nk = R.sum(0)
-        S1 = LA.atb(R, Xd)
-        if covariance == "full":
-            S2 = torch.einsum("nk,ni,nj->kij", R, Xd, Xd)
+        if native:
+            R, llsum = GM.estep(Xd, w, mu, cov, covariance)
+            Nk, S1, S2 = GM.stats(Xd, R, covariance)
         else:
-            S2 = LA.atb(R, Xd * Xd)
+            logp = _log_gauss(Xd, mu, cov, covariance) + torch.log(w)[None, :]
+            lse = torch.logsumexp(logp, 1)
+            R = torch.exp(logp - lse[:, None])  # [n, K]
+            llsum = lse.sum()
+            Nk = R.sum(0)
+            S1 = LA.atb(R, Xd)
+            if covariance == "full":
+                S2 = torch.einsum("nk,ni,nj->kij", R, Xd, Xd)
+            else:
+                S2 = LA.atb(R, Xd * Xd)
         st = reduce_partials(comm or _one(), {"Nk": Nk.cpu(), "S1": S1.cpu(), "S2": S2.cpu(),
-                                              "ll": lse.sum().reshape(1).cpu(),
+                                              "ll": llsum.reshape(1).cpu(),
                                               "n": torch.tensor([float(n)])})
         Nk, S1, S2 = st["Nk"].to(dev), st["S1"].to(dev), st["S2"].to(dev)
         ll = float(st["ll"][0]) / float(st["n"][0])

@@ -43,10 +43,10 @@ def kernel_matrix(X, Y, kernel: str = "linear", sigma: float = 1.0, k: float = 1
 
 _lib.register({
     "harp_svm_max_rows": [],
-    # K, ldk, ids, moff, nm, max_n, y, kd, a, g, iters, C, eps, tau, max_iter, stream
+    # K, ldk, ids, moff, nm, max_n, y, kd, a, g, iters, C, eps, tau, max_iter, ident, stream
     "harp_svm_smo": [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p,
                      _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_double, _lib.c_double,
-                     _lib.c_double, _lib.c_int, _lib.c_void_p],
+                     _lib.c_double, _lib.c_int, _lib.c_int, _lib.c_void_p],
 })
 
 
@@ -57,10 +57,11 @@ def native_smo_ok(K: torch.Tensor, n: int) -> bool:
 
 
 def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Tensor]], C: float, eps: float,
-               tau: float, max_iter: int) -> List[Tuple[torch.Tensor, torch.Tensor, int]]:
+               tau: float, max_iter: int, ident: bool = False) -> List[Tuple[torch.Tensor, torch.Tensor, int]]:
     """Train every binary machine ``(idx, y)`` (rows / columns ``idx`` of the fp64 Gram
-    ``K``, labels +-1) with the device SMO, all machines in one launch. Returns per
-    machine (alpha, gradient G = Q alpha - e, SMO steps)."""
+    ``K``, labels +-1) with the device SMO, all machines in one launch. ``ident``: one
+    machine over all of K (idx = 0..n-1, no index indirection). Returns per machine
+    (alpha, gradient G = Q alpha - e, SMO steps)."""
     dev = K.device
     idx = [m[0].to(dev, torch.int32) for m in machines]
     ys = [m[1].to(dev, torch.float64).reshape(-1) for m in machines]
@@ -75,7 +76,7 @@ def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Ten
     st = _lib.kernels().harp_svm_smo(K.data_ptr(), K.stride(0), ids.data_ptr(), moff.data_ptr(), len(machines),
                                      max(sizes), y.data_ptr(), kd.data_ptr(), a.data_ptr(), g.data_ptr(),
                                      iters.data_ptr(), float(C), float(eps), float(tau), int(max_iter),
-                                     _lib.stream_ptr(dev))
+                                     1 if ident else 0, _lib.stream_ptr(dev))
     _lib.check(st, "svm_smo")
     it = iters.tolist()
     out, o = [], 0
@@ -103,7 +104,8 @@ class BinarySVM:
         K = kernel_matrix(Xd, Xd, self.kernel, self.sigma) if K is None else K.double()
         if self.solver != "torch" and native_smo_ok(K, n):
             ar = torch.arange(n, device=K.device)
-            a, G, steps = smo_device(K.contiguous(), [(ar, yv)], self.C, self.eps, self.tau, self.max_iter)[0]
+            a, G, steps = smo_device(K.contiguous(), [(ar, yv)], self.C, self.eps, self.tau, self.max_iter,
+                                     ident=K.shape[0] == n)[0]
             return self._finish(Xd, yv, a, G, steps)
         Kd = torch.diagonal(K).clone()
         a = torch.zeros(n, dtype=torch.float64, device=K.device)

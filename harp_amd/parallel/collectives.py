@@ -368,7 +368,12 @@ def _apply(table: Table, function) -> None:
         table._rebuild_parts()
 
 
+# call counters of the expensive plan-building exchanges (tests assert cached plans skip them)
+STATS: Dict[str, int] = {"id_set_allgather": 0, "join_plans_built": 0, "rotate_header_roundtrips": 0}
+
+
 def _id_sets(comm: Communicator, table: Table) -> List[List[int]]:
+    STATS["id_set_allgather"] += 1
     ids = torch.tensor(sorted(table.get_partition_ids()), dtype=torch.int64)
     msgs = comm.all_gather_bytes(ids.view(torch.uint8).to(comm.device))
     return [m.cpu().view(torch.int64).tolist() if m.numel() else [] for m in msgs]
@@ -514,20 +519,26 @@ class RotateHandle:
 
 
 def _rotate_packed(comm: Communicator, table: PackedTable, dst: int, src: int, async_op: bool):
+    """Packed rotate: ONE blocking header round trip (the incoming row count), then the
+    incoming ids and rows in one asynchronous grouped send/recv (they used to be two
+    blocking round trips before the payload). ``async_op``: the handle is returned once
+    the payload is in flight; :meth:`RotateHandle.wait` installs it."""
     dev = comm.device
     n_out = torch.tensor([len(table)], dtype=torch.int64, device=dev)
     n_in = torch.empty(1, dtype=torch.int64, device=dev)
     comm.sendrecv({dst: n_out}, {src: n_in})
+    STATS["rotate_header_roundtrips"] += 1
     rows = int(n_in.item())
     ids_out = torch.tensor(table.ids, dtype=torch.int64, device=dev)
     ids_in = torch.empty(rows, dtype=torch.int64, device=dev)
     buf_out = table.buffer if table.buffer.device == dev else table.buffer.to(dev)
     buf_in = torch.empty((rows,) + table.part_shape, dtype=buf_out.dtype, device=dev)
-    sends = {dst: ids_out} if ids_out.numel() else {}
-    recvs = {src: ids_in} if rows else {}
-    comm.sendrecv(sends, recvs)
-    works = comm.sendrecv({dst: buf_out} if buf_out.numel() else {}, {src: buf_in} if buf_in.numel() else {},
-                          async_op=True)
+    sends, recvs = {}, {}
+    if ids_out.numel():
+        sends[dst] = [ids_out] + ([buf_out] if buf_out.numel() else [])
+    if rows:
+        recvs[src] = [ids_in] + ([buf_in] if buf_in.numel() else [])
+    works = comm.sendrecv_multi(sends, recvs, async_op=True)
     home = table.buffer.device
 
     def finish():
@@ -543,33 +554,32 @@ def _rotate_packed(comm: Communicator, table: PackedTable, dst: int, src: int, a
 def join(comm: Communicator, dynamic: Table, partitioner: Optional[Partitioner], static: Table) -> bool:
     """Graph join: every dynamic partition goes to each worker whose static table holds
     the same id (else to the partitioner owner). Dynamic partitions not needed locally
-    are removed; received ones are combined into the dynamic table."""
+    are removed; received ones are combined into the dynamic table.
+
+    The reference builds a master ``Join`` plan per call (GraphCollective.java:313-441:
+    gather both id sets at the master, broadcast the plan, then bcast or dispatch). Here
+    the routing is a cached plan (:class:`_JoinPlan`) keyed on every rank's (static,
+    dynamic) layout: a repeated join with unchanged layouts skips the id-set all-gather
+    entirely (no exchange at all when both tables are ``static_layout`` PackedTables,
+    else one small all-gather of layout hashes), and a packed dynamic table with a dense
+    combiner moves as ONE fixed-split all-to-all of rows (no size exchange, no
+    per-partition objects)."""
     P = comm.world_size
     if P == 1:
         return True
-    holders: Dict[int, List[int]] = {}
-    for r, ids in enumerate(_id_sets(comm, static)):
-        for i in ids:
-            holders.setdefault(i, []).append(r)
+    plan = _join_plan(comm, dynamic, partitioner, static)
+    if plan.packed:
+        return _join_packed(comm, dynamic, plan)
     send: List[List[Partition]] = [[] for _ in range(P)]
-    remove: List[int] = []
     for p in dynamic.get_partitions():
-        dests = holders.get(p.id())
-        if dests is None and partitioner is not None:
-            w = partitioner.get_worker_id(p.id())
-            dests = [w] if w != UNKNOWN_WORKER_ID else None
-        if dests is None:
-            continue  # nobody needs it: stays local
-        for w in dests:
+        for w in plan.dests.get(p.id(), ()):
             if w != comm.rank:
                 send[w].append(p)
-        if comm.rank not in dests:
-            remove.append(p.id())
     home = _home(dynamic, comm)
     msgs = [(_encode(send[r], comm) if r != comm.rank else torch.empty(0, dtype=torch.uint8, device=comm.device))
             for r in range(P)]
     recv = comm.all_to_all_bytes(msgs)
-    for i in remove:
+    for i in plan.remove:
         dynamic.remove_partition(i)
     target = dynamic.to_table() if isinstance(dynamic, PackedTable) else dynamic
     for r in range(P):
@@ -577,6 +587,114 @@ def join(comm: Communicator, dynamic: Table, partitioner: Optional[Partitioner],
             _add_all(target, _decode(recv[r], home))
     if target is not dynamic:
         _replace(dynamic, target)
+    return True
+
+
+class _JoinPlan:
+    """Routing of one join: per local dynamic id its destination ranks, the ids removed
+    locally, and (packed fast path) the row routing of the all-to-all. Cached on the
+    STATIC table (the long-lived side, e.g. a vertex table), keyed on the layouts."""
+
+    packed = False
+
+
+def _ids_sig(t: Table) -> tuple:
+    if isinstance(t, PackedTable):
+        return (t.ids_hash(), len(t))
+    ids = sorted(t.get_partition_ids())
+    return (zlib.crc32(torch.tensor(ids, dtype=torch.int64).numpy().tobytes()) if ids else 0, len(ids))
+
+
+def _join_plan(comm: Communicator, dynamic: Table, partitioner: Optional[Partitioner], static: Table) -> _JoinPlan:
+    P, me = comm.world_size, comm.rank
+    mine = (_ids_sig(static), _ids_sig(dynamic))
+    pkey = plans._part_key(partitioner) if partitioner is not None else None
+    cache = getattr(static, "_join_plans", None)
+    if cache is None:
+        cache = static._join_plans = {}
+    stat = (getattr(dynamic, "static_layout", False) and getattr(static, "static_layout", False)
+            and isinstance(dynamic, PackedTable) and isinstance(static, PackedTable))
+    if stat:
+        for k, pl in cache.items():
+            if k[0] == mine and k[2] == pkey:
+                return pl
+        key = (mine, None, pkey)
+    else:
+        allv = comm.all_gather_ints([mine[0][0], mine[0][1], mine[1][0], mine[1][1]])
+        key = (mine, tuple(tuple(r) for r in allv.tolist()), pkey)
+        pl = cache.get(key)
+        if pl is not None:
+            return pl
+    STATS["join_plans_built"] += 1
+    holders: Dict[int, List[int]] = {}
+    for r, ids in enumerate(_id_sets(comm, static)):
+        for i in ids:
+            holders.setdefault(i, []).append(r)
+    pl = _JoinPlan()
+    pl.dests, pl.remove = {}, []
+    for i in dynamic.get_partition_ids():
+        dests = holders.get(i)
+        if dests is None and partitioner is not None:
+            w = partitioner.get_worker_id(i)
+            dests = [w] if w != UNKNOWN_WORKER_ID else None
+        if dests is None:
+            continue  # nobody needs it: stays local
+        pl.dests[i] = dests
+        if me not in dests:
+            pl.remove.append(i)
+    # packed fast path only if EVERY rank's dynamic table is packed alike (agreed collectively)
+    cand = isinstance(dynamic, PackedTable) and _is_dense_combiner(dynamic.combiner)
+    sig = zlib.crc32(repr((dynamic.part_shape, str(dynamic.buffer.dtype))).encode()) & 0x7FFFFFFF if cand else 0
+    got = comm.all_gather_ints([sig, int(cand)])
+    if cand and bool((got[:, 0] == sig).all()) and bool((got[:, 1] == 1).all()):
+        _build_packed_join(comm, dynamic, pl)
+    if len(cache) > 8:
+        cache.clear()
+    cache[key] = pl
+    return pl
+
+
+def _build_packed_join(comm: Communicator, dynamic: PackedTable, pl: _JoinPlan) -> None:
+    """Row routing of a packed join: rows sorted by destination (a row needed by several
+    ranks is sent to each), the received ids per source, and the post-join layout."""
+    P, me = comm.world_size, comm.rank
+    ids = dynamic.ids
+    per_dest: List[List[int]] = [[] for _ in range(P)]
+    for row, i in enumerate(ids):
+        for w in pl.dests.get(i, ()):
+            if w != me:
+                per_dest[w].append(row)
+    send_rows = [r for d in per_dest for r in d]
+    send_counts = [len(d) for d in per_dest]
+    got = plans._exchange_ids(comm, [torch.tensor([ids[r] for r in d], dtype=torch.int64) for d in per_dest])
+    recv_ids = [x.tolist() for x in got]
+    removed = set(pl.remove)
+    keep_rows = [row for row, i in enumerate(ids) if i not in removed]
+    new_ids = sorted(set(ids[r] for r in keep_rows) | set(i for x in recv_ids for i in x))
+    pos = {i: k for k, i in enumerate(new_ids)}
+    dev = dynamic.buffer.device
+    t = lambda x: torch.tensor(x, dtype=torch.int64, device=dev)  # noqa: E731
+    pl.packed = True
+    pl.send_idx = t(send_rows)
+    pl.send_counts = send_counts
+    pl.recv_counts = [len(x) for x in recv_ids]
+    pl.keep_idx = t(keep_rows)
+    pl.keep_pos = t([pos[ids[r]] for r in keep_rows])
+    pl.recv_pos = t([pos[i] for x in recv_ids for i in x])
+    pl.new_ids = new_ids
+
+
+def _join_packed(comm: Communicator, dynamic: PackedTable, pl: _JoinPlan) -> bool:
+    op = plans._op_name(dynamic)
+    buf = dynamic.buffer
+    send = buf.index_select(0, pl.send_idx) if pl.send_idx.numel() else buf[:0]
+    recv = plans._alltoall_rows(comm, send, pl.send_counts, pl.recv_counts, buf)
+    out = torch.full((len(pl.new_ids),) + dynamic.part_shape, plans.identity_value(op, buf.dtype), dtype=buf.dtype,
+                     device=buf.device)
+    if pl.keep_idx.numel():
+        out.index_copy_(0, pl.keep_pos, buf.index_select(0, pl.keep_idx))
+    plans.combine_rows(out, pl.recv_pos, recv, op)
+    dynamic.set_contents(pl.new_ids, out)
     return True
 
 

@@ -242,6 +242,26 @@ class Communicator:
             w.wait()
         return []
 
+    def sendrecv_multi(self, sends: dict, recvs: dict, async_op: bool = False):
+        """Like :meth:`sendrecv` with a LIST of tensors per peer, all in one grouped call
+        (per peer, the tensors are matched in list order)."""
+        self._hook("sendrecv")
+        ops = []
+        for dst, ts in sends.items():
+            for t in ts:
+                ops.append(dist.P2POp(dist.isend, t, self.global_rank(dst), self.group))
+        for src, ts in recvs.items():
+            for t in ts:
+                ops.append(dist.P2POp(dist.irecv, t, self.global_rank(src), self.group))
+        if not ops:
+            return []
+        works = dist.batch_isend_irecv(ops)
+        if async_op:
+            return works
+        for w in works:
+            w.wait()
+        return []
+
     # -- helpers built on the primitives ----------------------------------------------
     def all_gather_ints(self, values: Sequence[int]) -> torch.Tensor:
         """All-gather a small int64 vector; returns a CPU tensor [P, len(values)]."""
