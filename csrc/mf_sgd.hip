@@ -404,9 +404,9 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
 //    counter by any block of the XCD, so no block ever waits on a specific other block;
 //    the first 8 blocks dispatched cover the 8 XCDs, so every XCD always has a running
 //    block and every wait terminates (the chain of waits ends at sub-step 0);
-//  * completion: a block finishing a round makes its stores visible (workgroup release)
-//    and counts it; the block completing the LAST round of (x, s) writes the XCD's L2 back
-//    (agent release) and raises fin[x][s];
+//  * completion: a block that finds no more rounds of (x, s) waits for its own stores
+//    (once) and adds the rounds it trained; the block whose add completes the count writes
+//    the XCD's L2 back (agent release) and raises fin[x][s];
 //  * visibility: XCD x reads item block b only after its producer's write-back, and its
 //    own L2 holds no line of b in this launch (b was not touched by x since the launch
 //    started, and a launch starts with invalidated caches), so no invalidation is needed;
@@ -456,8 +456,8 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
       if (threadIdx.x == 0) {
         long spins = 0;
         while (__hip_atomic_load(fin + nxt * XCDS + (step - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-          __builtin_amdgcn_s_sleep(8);
-          if (++spins > (1L << 22)) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1L << 24)) {
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
@@ -470,15 +470,14 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
       if (threadIdx.x == 0) publish(fin + x * XCDS + step);
       continue;
     }
+    int mine = 0;  // rounds of (x, step) this block trained
     for (;;) {
       if (threadIdx.x == 0)
         s_round = __hip_atomic_fetch_add(claim + x * XCDS + step, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       const int rd = s_round;
-      if (rd >= rounds) {
-        __syncthreads();  // everyone read s_round before it is rewritten
-        break;
-      }
+      __syncthreads();  // everyone read s_round before it is rewritten
+      if (rd >= rounds) break;
       const long r0 = (long)rd * 16 * CH;
       for (int k = threadIdx.x; k < 16 * CH; k += 256) {
         if (r0 + k < n) {
@@ -490,16 +489,21 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
         }
       }
       __syncthreads();
-      const long mine = n - (r0 + (long)sub * CH);
-      if (mine > 0)
-        sgd_stream_lds<R, true>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
+      const long left = n - (r0 + (long)sub * CH);
+      if (left > 0)
+        sgd_stream_lds<R, true>(sR + sub * CH, sC + sub * CH, sV + sub * CH, left < CH ? (int)left : CH, sl, W,
                                 (unsigned)ldw, H, (unsigned)ldh, lr, lam);
-      // every wave's H / W stores are acknowledged by the XCD's L2 before the round counts
+      __syncthreads();  // the LDS triples are free
+      ++mine;
+    }
+    if (mine) {
+      // every wave's H / W stores of this block's rounds are acknowledged by the XCD's L2
+      // before they count (once per block and sub-step, not per round)
       __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();  // ... and the LDS triples are free
+      __syncthreads();
       if (threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(done + x * XCDS + step, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == rounds - 1) publish(fin + x * XCDS + step);  // the last round of (x, step)
+        const int prev = __hip_atomic_fetch_add(done + x * XCDS + step, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + mine == rounds) publish(fin + x * XCDS + step);  // the last rounds of (x, step)
       }
     }
   }

@@ -24,7 +24,7 @@ import torch
 from ..core.combiner import Operation
 from ..ops import linalg as LA
 from ..parallel.comm import Communicator
-from .common import gather_rows, reduce_partials
+from .common import broadcast_tensor, gather_rows, reduce_partials
 
 
 def _local(comm: Optional[Communicator]) -> Communicator:
@@ -87,7 +87,17 @@ def pca(X: torch.Tensor, comm: Optional[Communicator] = None, method: str = "cor
     comm = _local(comm)
     if method == "correlation":
         r = correlation(X, comm)
-        evals, evecs = torch.linalg.eigh(r["correlation"])
+        # step 2 on the master only (PCADaalCollectiveMapper.java:121-147), then broadcast:
+        # the d x d fp64 eigensolve is not repeated on every worker
+        d = r["correlation"].shape[0]
+        dev = r["correlation"].device
+        if comm.rank == 0:
+            evals, evecs = torch.linalg.eigh(r["correlation"])
+            packed = torch.cat([evals.reshape(1, d), evecs]).contiguous()
+        else:
+            packed = None
+        packed = broadcast_tensor(comm, packed, (d + 1, d), torch.float64).to(dev)
+        evals, evecs = packed[0], packed[1:]
         order = torch.argsort(evals, descending=True)
         evals, evecs = evals[order], evecs[:, order].t()
     elif method == "svd":

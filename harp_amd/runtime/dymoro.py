@@ -315,16 +315,20 @@ class BudgetTuner:
     trained per iteration lands in ``[min_bound, max_bound]`` percent (the reference's LDA
     ``adjustMiniBatch``, LDAMPCollectiveMapper.java:295-314, 477-557).
 
-    Each iteration every worker's (compute time, items trained) is all-gathered; the
-    trained percentage is scaled by (predicted / actual) compute time, where predicted =
-    budget x P x slices x P (every step of every worker running exactly to the budget), so
-    steps that overran or finished early are normalised out. Over ``max_bound``: halve the
-    budget. Under ``min_bound``: double it (and keep doubling while the projection stays
-    under); an under-train after an over-train starts a ``break_period`` (1, 2, 4, ...
-    iterations) during which the budget is left alone, which damps oscillation.
+    Each iteration every worker's (compute time, items trained) is all-gathered. Over
+    ``max_bound``: halve the budget. Under ``min_bound``: double it (and keep doubling
+    while the projection stays under); an under-train after an over-train starts a
+    ``break_period`` (1, 2, 4, ... iterations) during which the budget is left alone,
+    which damps oscillation.
 
-    The first tuning (``proportional_first``) instead sets the budget in one proportional
-    step toward the band's midpoint (the SGD ``adjustMiniBatch`` rule,
+    Deviation, measured on MI355X: the reference decides on the trained percentage scaled
+    by (predicted / actual) compute time, predicted = budget x P x slices x P, which
+    divides out steps that overran their timer. On the GPU a step's pieces are issued one
+    ahead (:class:`StepBudget`), so every step overruns by up to two pieces and that
+    projection stayed inside the band while 87 % of the tokens were trained. The
+    halve / double rule here therefore uses the TRAINED percentage; the projection is
+    used once, for the first tuning (``proportional_first``), which sets the budget in one
+    proportional step toward the band's midpoint (the SGD ``adjustMiniBatch`` rule,
     SGDCollectiveMapper.java:623-668): the reference starts LDA at a 1 s CPU step, and a
     GPU step is milliseconds, so plain halving would need ~10 iterations to get there.
     Returns the new budget in seconds. Bounds outside (0, 100] fall back to 50/50 and
@@ -355,23 +359,23 @@ class BudgetTuner:
         tot_time, tot_items = t.buffer.sum(0).cpu().tolist()
         real = 100.0 * tot_items / max(float(total_items), 1.0)
         predicted = budget_s * P * steps
-        pct = real * predicted / max(tot_time, 1e-12)
+        proj = real * predicted / max(tot_time, 1e-12)
         new = budget_s
-        rec = {"iter": it, "trained_pct": round(real, 3), "projected_pct": round(pct, 3), "budget_s": budget_s}
+        rec = {"iter": it, "trained_pct": round(real, 3), "projected_pct": round(proj, 3), "budget_s": budget_s}
         if self.tuned == 0 and self.proportional_first:
-            if pct > self.max_bound or pct < self.min_bound:
+            if proj > self.max_bound or proj < self.min_bound:
                 target = 0.5 * (self.min_bound + self.max_bound)
-                new = budget_s * target / max(pct, 1e-9)
+                new = budget_s * target / max(proj, 1e-9)
         elif self.last_under_train == 0 or it - self.last_under_train >= self.break_period:
-            if pct > self.max_bound:
+            if real > self.max_bound:
                 self.has_over_trained = True
                 new = budget_s / 2
-            elif pct < self.min_bound:
+            elif real < self.min_bound:
                 if self.has_over_trained:
                     self.last_under_train = it
                     self.break_period = 1 if self.break_period == 0 else 2 * self.break_period
                 new = budget_s * 2
-                potential = 2 * pct
+                potential = 2 * real
                 while potential < self.min_bound and potential > 0:
                     potential *= 2
                     new *= 2

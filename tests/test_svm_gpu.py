@@ -9,9 +9,9 @@ from harp_amd.models.svm import BinarySVM, MultiClassSVM
 pytestmark = pytest.mark.gpu
 
 
-def _data(n, d, seed, classes=2):
+def _data(n, d, seed, classes=2, spread=1.5):
     g = torch.Generator().manual_seed(seed)
-    centers = torch.randn(classes, d, generator=g) * 1.5
+    centers = torch.randn(classes, d, generator=g) * spread
     y = torch.randint(0, classes, (n,), generator=g)
     X = centers[y] + torch.randn(n, d, generator=g)
     return X.double(), y
@@ -43,9 +43,10 @@ def test_device_multiclass_one_launch(cuda):
 
 
 def test_device_smo_speed_20k(cuda):
-    """n = 20k RBF: the device solver is >= 20x the host-synchronised loop (timed on a
-    step-capped run of the loop, scaled per step)."""
-    X, y = _data(20000, 16, 3)
+    """n = 20k RBF, overlapping classes (thousands of SMO steps): the device solver is
+    >= 20x the host-synchronised loop (timed on a step-capped run of the loop, scaled per
+    step; the device time includes its setup and the bias / SV extraction)."""
+    X, y = _data(20000, 16, 3, spread=0.25)
     Xg, yg = X.to(cuda), y.to(cuda)
     from harp_amd.models.svm import kernel_matrix
 
