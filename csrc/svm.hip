@@ -14,21 +14,20 @@
 // Ties resolve to the lowest index (torch argmax / argmin). Products and sums are rounded
 // one by one (no FMA contraction) so the trajectory follows the oracle's.
 //
-// Design: ONE 1024-thread workgroup per binary machine (one-vs-one machines of a
-// multiclass problem run concurrently, one per CU). Thread t owns elements t + 1024 k:
-// their gradient G lives in registers for the whole solve and the box-state bits (a < C,
-// a > 0, y > 0) in three bit masks, so a step touches global memory only for the two
-// kernel rows (gathered through the machine's index list from the shared Gram matrix,
-// L2/HBM) and the diagonal. Three block reductions per step (i; j; the broadcast of the
-// update). n <= 1024 * 32 per machine. Measured (profiles/r3_svm): the first form, with the
+// Design: ONE workgroup per binary machine (one-vs-one machines of a multiclass problem run
+// concurrently, one per CU): 1024 threads x <= 8 elements up to 8192 rows, else 512
+// threads x <= 64 elements (n <= 32768). Thread t owns elements t + T k: their gradient G
+// lives in registers for the whole solve and the box-state bits (a < C, a > 0, y > 0) in
+// three bit masks; a machine's column list (multiclass) sits in LDS. A step touches
+// global memory only for the two kernel rows (gathered from the shared Gram matrix,
+// L2/HBM, 8 elements' loads in flight at a time) and the diagonal. Three block
+// reductions per step (i; j; the broadcast of the update). Measured (profiles/r3_svm): the first form, with the
 // gradient in global memory and one element's gathers in flight at a time, spent ~44 us per
 // step at n = 20k in serialized memory round trips.
 #include "common.h"
 
 namespace {
 
-constexpr int kThreads = 1024;
-constexpr int kWaves = kThreads / 64;
 
 struct ArgMax {
   double v;
@@ -62,22 +61,22 @@ __device__ __forceinline__ double wave_min(double v) {
   return v;
 }
 
-// Thread t owns elements t + 1024 k (k < EPT): gradient G, the machine-local column index
-// (IDENT: the machine is the whole matrix, column = element) and three box-state bit masks
-// in registers. Loops over k are fully unrolled so every gather of a phase is in flight at
-// once (one memory round trip per phase, not one per element); a scheduling barrier every
-// GRP elements bounds how many are in flight, and with them the register use.
+// Thread t owns elements t + T k (k < EPT): gradient G and three box-state bit masks in
+// registers (IDENT: the machine is the whole matrix, column = element; else the columns in
+// LDS). Gathers are issued GRP elements at a time, unconditionally, so a phase costs a few
+// memory round trips, not one per element (the first form waited on every element's
+// loads: ~28 us per step at n = 20k).
 constexpr int GRP = 8;
 
-template <int EPT, bool IDENT>
-__global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict__ Kfull, long ldk,
+template <int EPT, bool IDENT, int T>
+__global__ __launch_bounds__(T) void smo_kernel(const double* __restrict__ Kfull, long ldk,
                                                        const int* __restrict__ ids_all, const long* __restrict__ moff,
                                                        const double* __restrict__ y_all,
                                                        const double* __restrict__ kd_all, double* __restrict__ a_all,
                                                        double* __restrict__ g_all, int* __restrict__ iters, double C,
                                                        double eps, double tau, int max_iter) {
-  __shared__ double s_v[kWaves], s_w[kWaves];
-  __shared__ int s_i[kWaves];
+  __shared__ double s_v[16], s_w[16];
+  __shared__ int s_i[16];
   __shared__ double s_bc[8];
   __shared__ int s_ic[4];
   const int m = blockIdx.x;
@@ -92,23 +91,24 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
   const double NEG = -__builtin_inf(), POS = __builtin_inf();
 
   double G[EPT];
-  int col[IDENT ? 1 : EPT];
+  // machine-local column indices (not IDENT): staged once in LDS, read per phase
+  extern __shared__ int s_col[];
   unsigned ypos = 0, ltC = 0, gt0 = 0;  // bit k: element tid + 1024 k
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
-    const int t = tid + kThreads * k;
+    const int t = tid + T * k;
     G[k] = -1.0;
-    if constexpr (!IDENT) col[k] = 0;
     if (t < n) {
       const double at = a[t];
       if (y[t] > 0) ypos |= 1u << k;
       if (at < C) ltC |= 1u << k;
       if (at > 0) gt0 |= 1u << k;
       G[k] = g[t];
-      if constexpr (!IDENT) col[k] = ids[t];
+      if constexpr (!IDENT) s_col[t] = ids[t];
     }
   }
-#define COL(k, t) (IDENT ? (t) : col[IDENT ? 0 : (k)])
+  __syncthreads();
+#define COL(k, t) (IDENT ? (t) : s_col[t])
   int it = 0;
   for (; it < max_iter; ++it) {
     // an opaque copy of the thread id: keeps the per-element addresses from being hoisted
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     int bi = 0x7fffffff;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-      const int t = tid + kThreads * k;
+      const int t = tid + T * k;
       if (t < n) {
         const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
         const double mg = yp ? -G[k] : G[k];
@@ -142,8 +142,8 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     }
     __syncthreads();
     if (wv == 0) {
-      double v = lane < kWaves ? s_v[lane] : NEG, w = lane < kWaves ? s_w[lane] : POS;
-      int i = lane < kWaves ? s_i[lane] : 0x7fffffff;
+      double v = lane < (T / 64) ? s_v[lane] : NEG, w = lane < (T / 64) ? s_w[lane] : POS;
+      int i = lane < (T / 64) ? s_i[lane] : 0x7fffffff;
       wave_arg<true>(v, i);
       w = wave_min(w);
       if (lane == 0) {
@@ -161,18 +161,32 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     const double kii = kd[i];
     double sv = POS;
     int sj = 0x7fffffff;
+    // gathers issued GRP elements at a time, unconditionally (clamped index), so they are
+    // in flight together; the selection is predicated afterwards
+    asm volatile("" : "+v"(tid));  // per-phase address recomputation (not kept live across phases)
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      if (k && k % GRP == 0) __builtin_amdgcn_sched_barrier(0);
-      const int t = tid + kThreads * k;
-      if (t < n) {
+    for (int k0 = 0; k0 < EPT; k0 += GRP) {
+      double kit[GRP], kdt[GRP];
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int k = k0 + u;
+        if (k < EPT) {
+          const int t = tid + T * k, tc = t < n ? t : n - 1;
+          kit[u] = Ki[COL(k, tc)];
+          kdt[u] = kd[tc];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int k = k0 + u;
+        const int t = tid + T * k;
+        if (k >= EPT || t >= n) continue;
         const bool yp = (ypos >> k) & 1, lc = (ltC >> k) & 1, g0 = (gt0 >> k) & 1;
         const double mg = yp ? -G[k] : G[k];
         const bool low = (yp && g0) || (!yp && lc);
-        const double kit = Ki[COL(k, t)], kdt = kd[t];
         if (low && mg < mval) {
           const double bt = __dsub_rn(mval, mg);
-          double at = __dsub_rn(__dadd_rn(kii, kdt), __dmul_rn(2.0, kit));
+          double at = __dsub_rn(__dadd_rn(kii, kdt[u]), __dmul_rn(2.0, kit[u]));
           if (!(at > 0)) at = tau;
           const double sc = -__ddiv_rn(__dmul_rn(bt, bt), at);
           if (better_min(sc, t, sv, sj)) {
@@ -189,8 +203,8 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     }
     __syncthreads();
     if (wv == 0) {
-      double v = lane < kWaves ? s_v[lane] : POS;
-      int j = lane < kWaves ? s_i[lane] : 0x7fffffff;
+      double v = lane < (T / 64) ? s_v[lane] : POS;
+      int j = lane < (T / 64) ? s_i[lane] : 0x7fffffff;
       wave_arg<false>(v, j);
       if (lane == 0) s_ic[1] = j;
     }
@@ -198,8 +212,8 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     const int j = s_ic[1];
     if (j >= n) break;  // no admissible j (cannot happen while m - M >= eps)
     // ---- the two owners publish what the update needs
-    if (tid == (j & (kThreads - 1))) {
-      const int kj = j / kThreads;
+    if (tid == (j & (T - 1))) {
+      const int kj = j / T;
       double gj = 0.0;
 #pragma unroll
       for (int q = 0; q < EPT; ++q)
@@ -213,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
       s_bc[4] = a[j];
       s_bc[5] = y[j];
     }
-    if (tid == (i & (kThreads - 1))) {
+    if (tid == (i & (T - 1))) {
       s_bc[6] = a[i];
       s_bc[7] = y[i];
     }
@@ -226,14 +240,14 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     const double dai = __dmul_rn(yi, delta), daj = -__dmul_rn(yj, delta);
     const double nai = __dadd_rn(ai, dai), naj = __dadd_rn(aj, daj);
     // owners refresh the box bits (i != j: j has mg < m = mg_i)
-    if (tid == (i & (kThreads - 1))) {
-      const int k = i / kThreads;
+    if (tid == (i & (T - 1))) {
+      const int k = i / T;
       ltC = nai < C ? ltC | (1u << k) : ltC & ~(1u << k);
       gt0 = nai > 0 ? gt0 | (1u << k) : gt0 & ~(1u << k);
       a[i] = nai;
     }
-    if (tid == (j & (kThreads - 1))) {
-      const int k = j / kThreads;
+    if (tid == (j & (T - 1))) {
+      const int k = j / T;
       ltC = naj < C ? ltC | (1u << k) : ltC & ~(1u << k);
       gt0 = naj > 0 ? gt0 | (1u << k) : gt0 & ~(1u << k);
       a[j] = naj;
@@ -241,15 +255,28 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
     // ---- G += y (yi dai K_i + yj daj K_j)
     const double ci = __dmul_rn(yi, dai), cj = __dmul_rn(yj, daj);
     const double* Kj = Kfull + (long)(IDENT ? j : ids[j]) * ldk;
+    asm volatile("" : "+v"(tid));
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      if (k && k % GRP == 0) __builtin_amdgcn_sched_barrier(0);
-      const int t = tid + kThreads * k;
-      if (t < n) {
-        const int c = COL(k, t);
-        const double u = __dadd_rn(__dmul_rn(ci, Ki[c]), __dmul_rn(cj, Kj[c]));
+    for (int k0 = 0; k0 < EPT; k0 += GRP) {
+      double ki[GRP], kj[GRP];
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int k = k0 + u;
+        if (k < EPT) {
+          const int t = tid + T * k, tc = t < n ? t : n - 1;
+          const int c = COL(k, tc);
+          ki[u] = Ki[c];
+          kj[u] = Kj[c];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int k = k0 + u;
+        const int t = tid + T * k;
+        if (k >= EPT || t >= n) continue;
+        const double v = __dadd_rn(__dmul_rn(ci, ki[u]), __dmul_rn(cj, kj[u]));
         const double yt = ((ypos >> k) & 1) ? 1.0 : -1.0;
-        G[k] = __dadd_rn(G[k], __dmul_rn(yt, u));
+        G[k] = __dadd_rn(G[k], __dmul_rn(yt, v));
       }
     }
     __syncthreads();  // s_bc / s_ic are rewritten by the next step
@@ -257,28 +284,38 @@ __global__ __launch_bounds__(kThreads) void smo_kernel(const double* __restrict_
 #undef COL
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
-    const int t = tid + kThreads * k;
+    const int t = tid + T * k;
     if (t < n) g[t] = G[k];
   }
   if (tid == 0) iters[m] = it;
 }
 
-template <int EPT>
+template <int EPT, int T>
+int launch_smo_attr() {
+  const int bytes = (int)sizeof(int) * EPT * T;
+  if (bytes <= 64 * 1024) return HARP_OK;
+  return hipFuncSetAttribute((const void*)smo_kernel<EPT, false, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             bytes) == hipSuccess ? HARP_OK : HARP_ELAUNCH;
+}
+
+template <int EPT, int T>
 int launch_smo(const double* K, long ldk, const int* ids, const long* moff, int nm, const double* y, const double* kd,
                double* a, double* g, int* iters, double C, double eps, double tau, int max_iter, bool ident,
                hipStream_t s) {
   if (ident)
-    smo_kernel<EPT, true><<<dim3(nm), dim3(kThreads), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau,
-                                                              max_iter);
-  else
-    smo_kernel<EPT, false><<<dim3(nm), dim3(kThreads), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau,
-                                                               max_iter);
+    smo_kernel<EPT, true, T><<<dim3(nm), dim3(T), 0, s>>>(K, ldk, ids, moff, y, kd, a, g, iters, C, eps, tau,
+                                                          max_iter);
+  else if (launch_smo_attr<EPT, T>() != HARP_OK)
+    return HARP_ELAUNCH;
+  else  // the machines' column lists live in LDS: EPT * T ints (<= 128 KB)
+    smo_kernel<EPT, false, T><<<dim3(nm), dim3(T), sizeof(int) * EPT * T, s>>>(K, ldk, ids, moff, y, kd, a, g,
+                                                                               iters, C, eps, tau, max_iter);
   return harp_launch_status();
 }
 
 }  // namespace
 
-HARP_EXPORT int harp_svm_max_rows() { return kThreads * 32; }
+HARP_EXPORT int harp_svm_max_rows() { return 512 * 64; }
 
 // nm binary machines; machine m owns entries [moff[m], moff[m+1]) of ids (row/col indices
 // into the n x ldk fp64 Gram K), y (+-1), kd (the machine's K diagonal), a (alphas, in/out:
@@ -287,16 +324,21 @@ HARP_EXPORT int harp_svm_max_rows() { return kThreads * 32; }
 HARP_EXPORT int harp_svm_smo(const double* K, long ldk, const int* ids, const long* moff, int nm, int max_n,
                              const double* y, const double* kd, double* a, double* g, int* iters, double C, double eps,
                              double tau, int max_iter, int ident, hipStream_t s) {
-  if (nm <= 0 || max_n <= 0 || max_n > kThreads * 32 || !(C > 0) || max_iter < 0) return HARP_EBADARG;
+  if (nm <= 0 || max_n <= 0 || max_n > 512 * 64 || !(C > 0) || max_iter < 0) return HARP_EBADARG;
   if (ident && nm != 1) return HARP_EBADARG;
-  const int ept = (max_n + kThreads - 1) / kThreads;
-#define SMO(E) return launch_smo<E>(K, ldk, ids, moff, nm, y, kd, a, g, iters, C, eps, tau, max_iter, ident != 0, s)
-  if (ept <= 1) SMO(1);
-  if (ept <= 2) SMO(2);
-  if (ept <= 4) SMO(4);
-  if (ept <= 8) SMO(8);
-  if (ept <= 16) SMO(16);
-  if (ept <= 24) SMO(24);
-  SMO(32);
+  // up to 8192 rows: 1024 threads x <= 8 elements (<= 128 registers); beyond: 512 threads
+  // with up to 64 elements each (256 registers per lane, the gradient still in registers)
+#define SMO(E, TT) return launch_smo<E, TT>(K, ldk, ids, moff, nm, y, kd, a, g, iters, C, eps, tau, max_iter, ident != 0, s)
+  const int e1 = (max_n + 1023) / 1024;
+  if (e1 <= 1) SMO(1, 1024);
+  if (e1 <= 2) SMO(2, 1024);
+  if (e1 <= 4) SMO(4, 1024);
+  if (e1 <= 8) SMO(8, 1024);
+  const int e2 = (max_n + 511) / 512;
+  if (e2 <= 24) SMO(24, 512);
+  if (e2 <= 32) SMO(32, 512);
+  if (e2 <= 40) SMO(40, 512);
+  if (e2 <= 48) SMO(48, 512);
+  SMO(64, 512);
 #undef SMO
 }

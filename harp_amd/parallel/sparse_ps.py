@@ -108,6 +108,12 @@ class SparseRowPS:
         self.pull_recv = _Side(per_lrow, pull_caps_in, self.K, dev)     # requester: -> local rows
         self.push_send = _Side(per_lrow, push_caps_out, self.K, dev)    # requester: deltas of local rows
         self.push_recv = _Side(orows, push_caps_in, self.K, dev)        # owner: += into glob rows
+        if P == 1:
+            # one rank: both ends derive the same layout from the same caps, so the receive
+            # side reads the send payload in place (no loopback copy)
+            assert self.pull_recv.nbytes == self.pull_send.nbytes and self.push_recv.nbytes == self.push_send.nbytes
+            self.pull_recv.buf = self.pull_send.buf
+            self.push_recv.buf = self.push_send.buf
         self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.n_rows = int(ids.numel())
         self._pulled = False
@@ -122,7 +128,7 @@ class SparseRowPS:
     # -- collectives ---------------------------------------------------------------------
     def _exchange(self, send: _Side, recv: _Side) -> None:
         if self.comm.world_size == 1:
-            if send.nbytes:
+            if send.nbytes and recv.buf.data_ptr() != send.buf.data_ptr():
                 recv.buf[:send.nbytes].copy_(send.buf[:send.nbytes])
             return
         self.comm.all_to_all_single(recv.buf[:recv.nbytes], send.buf[:send.nbytes], recv.splits, send.splits)
