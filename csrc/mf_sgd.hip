@@ -402,8 +402,10 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
 // x + 1 has FINISHED sub-step s - 1 -- a dependency on one neighbour, no grid barrier.
 //  * work: rounds of 16 streams x CH ratings are claimed from a per-(XCD, sub-step)
 //    counter by any block of the XCD, so no block ever waits on a specific other block;
-//    the first 8 blocks dispatched cover the 8 XCDs, so every XCD always has a running
-//    block and every wait terminates (the chain of waits ends at sub-step 0);
+//    a block waits for the neighbour only after it has claimed a round (blocks left
+//    without work move on, so few blocks poll); the first 8 blocks dispatched cover the
+//    8 XCDs, so every XCD always has a running block and every wait terminates (the chain
+//    of waits ends at sub-step 0);
 //  * completion: a block that finds no more rounds of (x, s) waits for its own stores
 //    (once) and adds the rounds it trained; the block whose add completes the count writes
 //    the XCD's L2 back (agent release) and raises fin[x][s];
@@ -452,20 +454,6 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
     const long n = win ? win[XCDS * XCDS + cell] : ncell;
     const long nst = (n + CH - 1) / CH;
     const int rounds = (int)((nst + 15) / 16);
-    if (step > 0) {  // item block (x + step) mod 8: XCD x + 1 must have finished step - 1
-      if (threadIdx.x == 0) {
-        long spins = 0;
-        while (__hip_atomic_load(fin + nxt * XCDS + (step - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1L << 24)) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-      __syncthreads();
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
     if (rounds == 0) {  // empty cell: complete at once (idempotent)
       if (threadIdx.x == 0) publish(fin + x * XCDS + step);
       continue;
@@ -478,6 +466,23 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
       const int rd = s_round;
       __syncthreads();  // everyone read s_round before it is rewritten
       if (rd >= rounds) break;
+      if (mine == 0 && step > 0) {
+        // claimed work in (x, step): item block (x + step) mod 8 must be released by XCD
+        // x + 1 (its sub-step step - 1). Blocks without work never wait, so only the
+        // blocks that train poll the flag.
+        if (threadIdx.x == 0) {
+          long spins = 0;
+          while (__hip_atomic_load(fin + nxt * XCDS + (step - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1L << 24)) {
+              __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+        __syncthreads();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      }
       const long r0 = (long)rd * 16 * CH;
       for (int k = threadIdx.x; k < 16 * CH; k += 256) {
         if (r0 + k < n) {
