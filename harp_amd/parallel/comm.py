@@ -137,6 +137,10 @@ class Communicator:
                 device = torch.device("cpu")
         self.device = torch.device(device)
         self.workers = Workers(self.rank, self.world_size)
+        # gloo moves only host tensors for point-to-point / all-to-all: when gloo ranks keep
+        # their buffers on a GPU (the multi-rank rehearsal on a one-GPU box, where RCCL
+        # refuses two ranks per device), those ops stage through host memory
+        self.stage = self.backend == "gloo" and self.device.type == "cuda" and self.world_size > 1
         self._channels: dict = {}
         self._lock = threading.Lock()
         # Optional fault injection hook (tests): called before every collective with the
@@ -185,26 +189,43 @@ class Communicator:
             else:
                 dist.barrier(group=self.group)
 
+    def _host(self, t: torch.Tensor, fn) -> None:
+        """Run a collective on a host copy of ``t`` and copy the result back (staging)."""
+        h = t.detach().cpu().contiguous()
+        fn(h)
+        t.copy_(h)
+
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
         self._hook("all_reduce")
         if self.world_size > 1:
+            if self.stage and t.device.type != "cpu":
+                return self._host(t, lambda h: dist.all_reduce(h, op=op, group=self.group))
             return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
         return None
 
     def broadcast(self, t: torch.Tensor, root: int, async_op: bool = False):
         self._hook("broadcast")
         if self.world_size > 1:
+            if self.stage and t.device.type != "cpu":
+                return self._host(t, lambda h: dist.broadcast(h, src=self.global_rank(root), group=self.group))
             return dist.broadcast(t, src=self.global_rank(root), group=self.group, async_op=async_op)
         return None
 
     def reduce(self, t: torch.Tensor, root: int, op=dist.ReduceOp.SUM):
         self._hook("reduce")
         if self.world_size > 1:
+            if self.stage and t.device.type != "cpu":
+                return self._host(t, lambda h: dist.reduce(h, dst=self.global_rank(root), op=op, group=self.group))
             dist.reduce(t, dst=self.global_rank(root), op=op, group=self.group)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         self._hook("all_gather")
         if self.world_size > 1:
+            if self.stage and out.device.type != "cpu":
+                ho = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_gather_into_tensor(ho, inp.cpu(), group=self.group)
+                out.copy_(ho)
+                return None
             return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
         out.copy_(inp.reshape(out.shape))
         return None
@@ -213,6 +234,11 @@ class Communicator:
                        async_op: bool = False):
         self._hook("reduce_scatter")
         if self.world_size > 1:
+            if self.stage and out.device.type != "cpu":
+                ho = torch.empty(out.shape, dtype=out.dtype)
+                dist.reduce_scatter_tensor(ho, inp.cpu(), op=op, group=self.group)
+                out.copy_(ho)
+                return None
             return dist.reduce_scatter_tensor(out, inp, op=op, group=self.group, async_op=async_op)
         out.copy_(inp.reshape(out.shape))
         return None
@@ -221,6 +247,11 @@ class Communicator:
                           out_splits: Sequence[int] | None = None, in_splits: Sequence[int] | None = None):
         self._hook("all_to_all")
         if self.world_size > 1:
+            if self.stage and out.device.type != "cpu":
+                ho = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=self.group)
+                out.copy_(ho)
+                return
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
         else:
             out.copy_(inp)
@@ -228,6 +259,8 @@ class Communicator:
     def sendrecv(self, sends: dict, recvs: dict, async_op: bool = False):
         """Grouped point-to-point: ``sends`` maps dest -> tensor, ``recvs`` src -> tensor."""
         self._hook("sendrecv")
+        if self.stage:
+            return self._staged_p2p({d: [t] for d, t in sends.items()}, {s: [t] for s, t in recvs.items()})
         ops = []
         for dst, t in sends.items():
             ops.append(dist.P2POp(dist.isend, t, self.global_rank(dst), self.group))
@@ -242,10 +275,31 @@ class Communicator:
             w.wait()
         return []
 
+    def _staged_p2p(self, sends: dict, recvs: dict):
+        """Host-staged grouped send/recv (gloo ranks with device buffers); completes before
+        returning (no works to wait on)."""
+        ops, host_recv = [], []
+        for dst, ts in sends.items():
+            for t in ts:
+                ops.append(dist.P2POp(dist.isend, t.detach().cpu().contiguous(), self.global_rank(dst), self.group))
+        for src, ts in recvs.items():
+            for t in ts:
+                h = torch.empty(t.shape, dtype=t.dtype)
+                host_recv.append((t, h))
+                ops.append(dist.P2POp(dist.irecv, h, self.global_rank(src), self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for t, h in host_recv:
+            t.copy_(h)
+        return []
+
     def sendrecv_multi(self, sends: dict, recvs: dict, async_op: bool = False):
         """Like :meth:`sendrecv` with a LIST of tensors per peer, all in one grouped call
         (per peer, the tensors are matched in list order)."""
         self._hook("sendrecv")
+        if self.stage:
+            return self._staged_p2p(sends, recvs)
         ops = []
         for dst, ts in sends.items():
             for t in ts:
