@@ -230,3 +230,19 @@ def test_pending_events_stay_bounded_without_metrics_path(monkeypatch):
         t._pending.append(("compute", _FakeEvent(), _FakeEvent()))
         M._sweep_pending(t._pending, t._fold)
     assert len(t._pending) < M.PENDING_SWEEP and t.counts["compute"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu_all_records(cuda):
+    """Every nested record at P = 2 with both ranks' kernels on the GPU (gloo with host
+    staging: RCCL refuses two ranks per device): the multi-rank device paths (rotation
+    rings, sparse push / pull rows, PCA broadcast) run before an 8-GPU node sees them."""
+    rec = _run_bench(["--gpus", "2", "--backend", "gloo", "--points", "2e5", "--centroids", "256", "--steps", "3",
+                      "--warmup", "1", "--sgd", "on", "--sgd-users", "20000", "--sgd-items", "3000",
+                      "--sgd-ratings", "400000", "--sgd-epochs", "3", "--extras", "on", "--pca-n", "2e5",
+                      "--pca-d", "200", "--pca-steps", "3", "--lda-docs", "5000", "--lda-vocab", "8000",
+                      "--lda-topics", "256", "--lda-len", "40", "--lda-iters", "3"])
+    assert rec["n_gpus"] == 2 and rec["dtype"] == "bf16"
+    for name in ("sgd", "pca", "lda"):
+        assert "error" not in rec[name], (name, rec[name])
+        assert rec[name]["n_gpus"] == 2 and rec[name]["sync_bytes_per_iter"] > 0
