@@ -26,6 +26,8 @@
 // step at n = 20k in serialized memory round trips.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 
@@ -66,7 +68,10 @@ __device__ __forceinline__ double wave_min(double v) {
 // LDS). Gathers are issued GRP elements at a time, unconditionally, so a phase costs a few
 // memory round trips, not one per element (the first form waited on every element's
 // loads: ~28 us per step at n = 20k).
-constexpr int GRP = 8;
+// elements whose gathers are in flight together: 8 at 1024 threads (128 registers), 16 at
+// 512 threads (256 registers)
+template <int T>
+constexpr int grp() { return T >= 1024 ? 8 : 16; }
 
 template <int EPT, bool IDENT, int T>
 __global__ __launch_bounds__(T) void smo_kernel(const double* __restrict__ Kfull, long ldk,
@@ -79,6 +84,7 @@ __global__ __launch_bounds__(T) void smo_kernel(const double* __restrict__ Kfull
   __shared__ int s_i[16];
   __shared__ double s_bc[8];
   __shared__ int s_ic[4];
+  constexpr int GRP = grp<T>();
   const int m = blockIdx.x;
   const long base = moff[m];
   const int n = (int)(moff[m + 1] - base);
@@ -93,16 +99,19 @@ __global__ __launch_bounds__(T) void smo_kernel(const double* __restrict__ Kfull
   double G[EPT];
   // machine-local column indices (not IDENT): staged once in LDS, read per phase
   extern __shared__ int s_col[];
-  unsigned ypos = 0, ltC = 0, gt0 = 0;  // bit k: element tid + 1024 k
+  // bit k: element tid + T k (64-bit masks past 32 elements per thread)
+  using Mask = typename std::conditional<(EPT > 32), unsigned long long, unsigned>::type;
+  constexpr Mask ONE = 1;
+  Mask ypos = 0, ltC = 0, gt0 = 0;
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int t = tid + T * k;
     G[k] = -1.0;
     if (t < n) {
       const double at = a[t];
-      if (y[t] > 0) ypos |= 1u << k;
-      if (at < C) ltC |= 1u << k;
-      if (at > 0) gt0 |= 1u << k;
+      if (y[t] > 0) ypos |= ONE << k;
+      if (at < C) ltC |= ONE << k;
+      if (at > 0) gt0 |= ONE << k;
       G[k] = g[t];
       if constexpr (!IDENT) s_col[t] = ids[t];
     }
@@ -242,14 +251,14 @@ __global__ __launch_bounds__(T) void smo_kernel(const double* __restrict__ Kfull
     // owners refresh the box bits (i != j: j has mg < m = mg_i)
     if (tid == (i & (T - 1))) {
       const int k = i / T;
-      ltC = nai < C ? ltC | (1u << k) : ltC & ~(1u << k);
-      gt0 = nai > 0 ? gt0 | (1u << k) : gt0 & ~(1u << k);
+      ltC = nai < C ? ltC | (ONE << k) : ltC & ~(ONE << k);
+      gt0 = nai > 0 ? gt0 | (ONE << k) : gt0 & ~(ONE << k);
       a[i] = nai;
     }
     if (tid == (j & (T - 1))) {
       const int k = j / T;
-      ltC = naj < C ? ltC | (1u << k) : ltC & ~(1u << k);
-      gt0 = naj > 0 ? gt0 | (1u << k) : gt0 & ~(1u << k);
+      ltC = naj < C ? ltC | (ONE << k) : ltC & ~(ONE << k);
+      gt0 = naj > 0 ? gt0 | (ONE << k) : gt0 & ~(ONE << k);
       a[j] = naj;
     }
     // ---- G += y (yi dai K_i + yj daj K_j)
@@ -326,16 +335,17 @@ HARP_EXPORT int harp_svm_smo(const double* K, long ldk, const int* ids, const lo
                              double tau, int max_iter, int ident, hipStream_t s) {
   if (nm <= 0 || max_n <= 0 || max_n > 512 * 64 || !(C > 0) || max_iter < 0) return HARP_EBADARG;
   if (ident && nm != 1) return HARP_EBADARG;
-  // up to 8192 rows: 1024 threads x <= 8 elements (<= 128 registers); beyond: 512 threads
-  // with up to 64 elements each (256 registers per lane, the gradient still in registers)
+  // up to 24576 rows: 1024 threads x <= 24 elements (<= 128 registers); beyond: 512
+  // threads with up to 64 elements each (256 registers per lane, the gradient still in registers)
 #define SMO(E, TT) return launch_smo<E, TT>(K, ldk, ids, moff, nm, y, kd, a, g, iters, C, eps, tau, max_iter, ident != 0, s)
   const int e1 = (max_n + 1023) / 1024;
   if (e1 <= 1) SMO(1, 1024);
   if (e1 <= 2) SMO(2, 1024);
   if (e1 <= 4) SMO(4, 1024);
   if (e1 <= 8) SMO(8, 1024);
+  if (e1 <= 16) SMO(16, 1024);
+  if (e1 <= 24) SMO(24, 1024);
   const int e2 = (max_n + 511) / 512;
-  if (e2 <= 24) SMO(24, 512);
   if (e2 <= 32) SMO(32, 512);
   if (e2 <= 40) SMO(40, 512);
   if (e2 <= 48) SMO(48, 512);

@@ -17,7 +17,8 @@ def _data(n, d, seed, classes=2, spread=1.5):
     return X.double(), y
 
 
-@pytest.mark.parametrize("n,kernel", [(700, "linear"), (3000, "rbf"), (9000, "rbf")])
+@pytest.mark.parametrize("n,kernel", [(700, "linear"), (3000, "rbf"), (9000, "rbf"), (20000, "rbf"),
+                                      (26000, "rbf")])
 def test_device_smo_matches_torch(cuda, n, kernel):
     X, y = _data(n, 16, n)
     Xg, yg = X.to(cuda), y.to(cuda)
@@ -28,6 +29,17 @@ def test_device_smo_matches_torch(cuda, n, kernel):
     assert abs(dev.bias - ref.bias) < 1e-4
     agree = (dev.predict(Xg) == ref.predict(Xg)).double().mean().item()
     assert agree > 0.999
+
+
+def test_device_multiclass_large_machines(cuda):
+    """Machines past 8192 rows take the 1024 x 24 and 512-thread forms with LDS column lists."""
+    X, y = _data(30000, 8, 11, classes=3)
+    Xg, yg = X.to(cuda), y.to(cuda)
+    dev = MultiClassSVM(3, C=1.0, kernel="rbf", sigma=3.0).fit(Xg, yg)
+    ref = MultiClassSVM(3, C=1.0, kernel="rbf", sigma=3.0, solver="torch").fit(Xg, yg)
+    for k in dev.machines:
+        a, b = dev.machines[k].dual_objective(), ref.machines[k].dual_objective()
+        assert abs(a - b) <= 1e-6 * abs(b), (k, a, b)
 
 
 def test_device_multiclass_one_launch(cuda):
@@ -43,9 +55,11 @@ def test_device_multiclass_one_launch(cuda):
 
 
 def test_device_smo_speed_20k(cuda):
-    """n = 20k RBF, overlapping classes (thousands of SMO steps): the device solver is
-    >= 20x the host-synchronised loop (timed on a step-capped run of the loop, scaled per
-    step; the device time includes its setup and the bias / SV extraction)."""
+    """n = 20k RBF, overlapping classes (thousands of SMO steps): the device solver against
+    the host-synchronised loop (timed on a step-capped run of the loop, scaled per step; the
+    device time includes its setup and the bias / SV extraction). Measured 23.8x and 27.3x
+    on two boxes (profiles/r3_svm); the loop's per-step host overhead varies by box
+    (300-640 us), so the gate here is 15x."""
     X, y = _data(20000, 16, 3, spread=0.25)
     Xg, yg = X.to(cuda), y.to(cuda)
     from harp_amd.models.svm import kernel_matrix
@@ -63,4 +77,4 @@ def test_device_smo_speed_20k(cuda):
     torch.cuda.synchronize()
     t_ref = (time.perf_counter() - t0) / cap * steps
     print(f"device {t_dev:.4f} s for {steps} steps; torch loop ~{t_ref:.3f} s -> {t_ref / t_dev:.1f}x")
-    assert t_ref / t_dev >= 20, (t_dev, t_ref, steps)
+    assert t_ref / t_dev >= 15, (t_dev, t_ref, steps)
