@@ -11,15 +11,19 @@ string-concatenating ``HarpStringPlus`` combiner, then de-duplicated in a HashSe
 MI355X design: SMO with second-order working-set selection (Fan, Chen & Lin 2005); the
 kernel matrix of the training block is one GEMM (+ fused RBF epilogue) kept resident
 (a 60k-row fp64 Gram is 29 GB — nothing on a 288 GB device). On the GPU the whole solve
-runs in ``csrc/svm.hip`` (:func:`smo_device`): one 1024-thread workgroup per binary
-machine with the gradient in registers, no host round trip per SMO step, and the
-K(K-1)/2 one-vs-one machines of a multiclass problem trained concurrently in ONE launch
-over the shared Gram matrix. The PyTorch loop below is the CPU path and the oracle. The
+runs in ``csrc/svm.hip`` (:func:`smo_device`), no host round trip per SMO step: a large
+machine is split over 16 CUs of one XCD (gradient, alphas and its slice of kernel row i
+in registers, two cross-workgroup reductions per step through the XCD's L2; up to 8
+machines at once, one per XCD), many small ones run one 1024-thread workgroup each, and
+the K(K-1)/2 one-vs-one machines of a multiclass problem train concurrently in ONE
+launch over the shared Gram matrix. The PyTorch loop below is the CPU path and the oracle. The
 cascade keeps the reference's wire format: SV lines travel through the generic
 (variable-length Writable) allreduce path.
 """
 from __future__ import annotations
 
+import os
+import warnings
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -43,6 +47,14 @@ def kernel_matrix(X, Y, kernel: str = "linear", sigma: float = 1.0, k: float = 1
 
 _lib.register({
     "harp_svm_max_rows": [],
+    "harp_svm_coop_ws_ints": [],
+    "harp_svm_coop_xcd_ints": [],
+    "harp_svm_coop_max_rows": [_lib.c_int],
+    # K, ldk, ids, moff, nm, max_n, y, kd, a, g, iters, C, eps, tau, max_iter, NB, ident, ws, stream
+    "harp_svm_smo_coop": [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int,
+                          _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_double,
+                          _lib.c_double, _lib.c_double, _lib.c_int, _lib.c_int, _lib.c_int, _lib.c_void_p,
+                          _lib.c_void_p],
     # K, ldk, ids, moff, nm, max_n, y, kd, a, g, iters, C, eps, tau, max_iter, ident, stream
     "harp_svm_smo": [_lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p,
                      _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_double, _lib.c_double,
@@ -50,10 +62,63 @@ _lib.register({
 })
 
 
-def native_smo_ok(K: torch.Tensor, n: int) -> bool:
-    """The device solver takes fp64 GPU Gram matrices with <= harp_svm_max_rows() rows per machine."""
+# machines of at least COOP_MIN_ROWS rows are split over several CUs of one XCD each (XCD x
+# trains machines x, x + 8, ...; csrc/svm.hip smo_coop_kernel) when there are at most
+# COOP_MAX_MACHINES of them (more small machines fill the chip better one CU each);
+# HARP_SVM_COOP_NB overrides the CU count per machine (0 = off)
+COOP_MIN_ROWS = 4096
+COOP_MAX_NB = 16
+COOP_MAX_MACHINES = 16
+
+
+def coop_workgroups(max_n: int, machines: int = 1) -> int:
+    """CUs per machine for the cooperative kernel (<= 4 elements per thread, <= 16 CUs), or
+    0 for the one-CU-per-machine kernel."""
+    one_cu_max = int(_lib.kernels().harp_svm_max_rows())
+    env = os.environ.get("HARP_SVM_COOP_NB")
+    if env is not None:
+        nb = int(env)
+    elif max_n < COOP_MIN_ROWS or (machines > COOP_MAX_MACHINES and max_n <= one_cu_max):
+        return 0
+    else:
+        nb = COOP_MAX_NB
+    if nb <= 0 or max_n > 4096 * nb:
+        return 0
+    return nb
+
+
+def _max_rows() -> int:
+    k = _lib.kernels()
+    return max(int(k.harp_svm_max_rows()), int(k.harp_svm_coop_max_rows(COOP_MAX_NB)))
+
+
+def native_smo_ok(K: torch.Tensor, n: int, machines: int = 1) -> bool:
+    """The device solver takes fp64 GPU Gram matrices with machines of <= 65536 rows (the
+    cooperative kernel at 16 CUs; the one-CU kernel takes <= 32768)."""
     return (K.device.type == "cuda" and K.dtype == torch.float64 and K.dim() == 2 and K.stride(1) == 1
-            and _lib.use_native(K) and 0 < n <= int(_lib.kernels().harp_svm_max_rows()))
+            and _lib.use_native(K) and 0 < n <= _max_rows())
+
+
+def _smo_coop(K, ids, moff, nm, max_n, y, kd, C, eps, tau, max_iter, ident, nb):
+    """All machines over ``nb`` CUs each; None if some XCD could not run its machines
+    cooperatively (fewer than nb workgroups there, or a wait gave up)."""
+    dev = K.device
+    k = _lib.kernels()
+    ws = torch.zeros(int(k.harp_svm_coop_ws_ints()), dtype=torch.int32, device=dev)
+    a = torch.zeros_like(y)
+    g = -torch.ones_like(y)
+    iters = torch.zeros(nm, dtype=torch.int32, device=dev)
+    st = k.harp_svm_smo_coop(K.data_ptr(), K.stride(0), ids.data_ptr(), moff.data_ptr(), nm, max_n, y.data_ptr(),
+                             kd.data_ptr(), a.data_ptr(), g.data_ptr(), iters.data_ptr(), float(C), float(eps),
+                             float(tau), int(max_iter), nb, 1 if ident else 0, ws.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(st, "svm_smo_coop")
+    w = ws.view(8, int(k.harp_svm_coop_xcd_ints()))[:, :4].tolist()
+    bad = [x for x in range(min(nm, 8)) if w[x][0] < nb or w[x][3] != 0]
+    if bad:
+        warnings.warn(f"cooperative SMO did not run on {nb} CUs of XCDs {bad} (claims / errors "
+                      f"{[(w[x][0], w[x][3]) for x in bad]}); using the one-CU kernel")
+        return None
+    return a, g, iters.tolist()
 
 
 def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Tensor]], C: float, eps: float,
@@ -72,6 +137,17 @@ def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Ten
     kd = torch.diagonal(K)[ids.long()].contiguous()
     a = torch.zeros_like(y)
     g = -torch.ones_like(y)
+    nb = coop_workgroups(max(sizes), len(machines))
+    r = _smo_coop(K, ids, moff, len(machines), max(sizes), y, kd, C, eps, tau, max_iter, ident, nb) if nb else None
+    if r is not None:
+        a, g, it = r
+        out, o = [], 0
+        for k, n in enumerate(sizes):
+            out.append((a[o:o + n], g[o:o + n], it[k]))
+            o += n
+        return out
+    if max(sizes) > int(_lib.kernels().harp_svm_max_rows()):
+        raise ValueError(f"device SMO: {max(sizes)} rows per machine exceed {int(_lib.kernels().harp_svm_max_rows())}")
     iters = torch.zeros(len(machines), dtype=torch.int32, device=dev)
     st = _lib.kernels().harp_svm_smo(K.data_ptr(), K.stride(0), ids.data_ptr(), moff.data_ptr(), len(machines),
                                      max(sizes), y.data_ptr(), kd.data_ptr(), a.data_ptr(), g.data_ptr(),
@@ -198,7 +274,8 @@ class MultiClassSVM:
                 if idx.numel() == 0:
                     continue
                 pairs.append(((a, b), idx, torch.where(yl[idx] == a, 1.0, -1.0).double()))
-        if pairs and self.kw.get("solver", "auto") != "torch" and native_smo_ok(Kfull, max(p[1].numel() for p in pairs)):
+        if pairs and self.kw.get("solver", "auto") != "torch" and native_smo_ok(Kfull, max(p[1].numel() for p in pairs),
+                                                                                     machines=len(pairs)):
             # all one-vs-one machines in ONE device launch over the shared Gram matrix
             proto = BinarySVM(**self.kw)
             res = smo_device(Kfull.contiguous(), [(idx, yy) for _, idx, yy in pairs], proto.C, proto.eps, proto.tau,

@@ -31,6 +31,49 @@ def test_device_smo_matches_torch(cuda, n, kernel):
     assert agree > 0.999
 
 
+@pytest.mark.parametrize("n", [5000, 20000, 40000])
+def test_coop_smo_matches_one_cu_kernel(cuda, n, monkeypatch):
+    """One machine split over 4 / 8 / 16 CUs of one XCD follows the one-CU kernel's exact
+    trajectory (same steps, same alphas), and past the one-CU limit (40k rows) the torch
+    oracle's objective."""
+    from harp_amd.models import svm as S
+
+    X, y = _data(n, 16, n + 1, spread=0.5)
+    Xg, yg = X.to(cuda), y.to(cuda)
+    K = S.kernel_matrix(Xg, Xg, "rbf", 4.0)
+    runs = {}
+    for nb in ([0] if n <= 32768 else []) + [4, 8, 16]:
+        if nb and n > 4096 * nb:
+            continue
+        monkeypatch.setenv("HARP_SVM_COOP_NB", str(nb))
+        m = BinarySVM(C=1.0, kernel="rbf", sigma=4.0).fit(Xg, yg, K)
+        runs[nb] = (m.n_iterations, m.alpha.clone(), m.dual_objective())
+    base = runs.get(0, next(iter(runs.values())))
+    for nb, (it, al, ob) in runs.items():
+        assert it == base[0], (nb, it, base[0])
+        assert torch.equal(al, base[1]), nb
+    if n > 32768:
+        ref = BinarySVM(C=1.0, kernel="rbf", sigma=4.0, solver="torch", max_iterations=200000).fit(Xg, yg, K)
+        assert abs(base[2] - ref.dual_objective()) <= 1e-6 * abs(ref.dual_objective())
+
+
+@pytest.mark.parametrize("n,classes", [(20000, 3), (12000, 5)])
+def test_coop_multiclass_matches_one_cu_kernel(cuda, n, classes, monkeypatch):
+    """Multiclass machines on the cooperative kernel, one XCD each (3 machines), and two
+    after one another on the first XCDs (10 machines), equal the one-CU kernel exactly."""
+    X, y = _data(n, 8, 5 + classes, classes=classes, spread=1.0)
+    Xg, yg = X.to(cuda), y.to(cuda)
+    res = {}
+    for nb in (0, 16):
+        monkeypatch.setenv("HARP_SVM_COOP_NB", str(nb))
+        m = MultiClassSVM(classes, C=1.0, kernel="rbf", sigma=3.0).fit(Xg, yg)
+        res[nb] = {k: (v.n_iterations, v.alpha) for k, v in m.machines.items()}
+    assert res[0].keys() == res[16].keys() and len(res[0]) == classes * (classes - 1) // 2
+    for k in res[0]:
+        assert res[0][k][0] == res[16][k][0], k
+        assert torch.equal(res[0][k][1], res[16][k][1]), k
+
+
 def test_device_multiclass_large_machines(cuda):
     """Machines past 8192 rows take the 1024 x 24 and 512-thread forms with LDS column lists."""
     X, y = _data(30000, 8, 11, classes=3)
@@ -57,9 +100,9 @@ def test_device_multiclass_one_launch(cuda):
 def test_device_smo_speed_20k(cuda):
     """n = 20k RBF, overlapping classes (thousands of SMO steps): the device solver against
     the host-synchronised loop (timed on a step-capped run of the loop, scaled per step; the
-    device time includes its setup and the bias / SV extraction). Measured 23.8x and 27.3x
-    on two boxes (profiles/r3_svm); the loop's per-step host overhead varies by box
-    (300-640 us), so the gate here is 15x."""
+    device time includes its setup and the bias / SV extraction). The machine runs on 16 CUs
+    (8.2 us per step, 47.9x; the one-CU kernel: 21 us, 19-27x, profiles/r3_svm); the loop's
+    per-step host overhead varies by box (300-640 us)."""
     X, y = _data(20000, 16, 3, spread=0.25)
     Xg, yg = X.to(cuda), y.to(cuda)
     from harp_amd.models.svm import kernel_matrix
@@ -77,4 +120,4 @@ def test_device_smo_speed_20k(cuda):
     torch.cuda.synchronize()
     t_ref = (time.perf_counter() - t0) / cap * steps
     print(f"device {t_dev:.4f} s for {steps} steps; torch loop ~{t_ref:.3f} s -> {t_ref / t_dev:.1f}x")
-    assert t_ref / t_dev >= 15, (t_dev, t_ref, steps)
+    assert t_ref / t_dev >= 25, (t_dev, t_ref, steps)
