@@ -141,6 +141,9 @@ class Communicator:
         # their buffers on a GPU (the multi-rank rehearsal on a one-GPU box, where RCCL
         # refuses two ranks per device), those ops stage through host memory
         self.stage = self.backend == "gloo" and self.device.type == "cuda" and self.world_size > 1
+        # the reverse: RCCL moves only device tensors, so a host tensor handed to a primitive
+        # under nccl runs on a device copy (a path the gloo tests would not catch)
+        self.dev_stage = self.backend == "nccl" and self.world_size > 1
         self._channels: dict = {}
         self._lock = threading.Lock()
         # Optional fault injection hook (tests): called before every collective with the
@@ -195,11 +198,23 @@ class Communicator:
         fn(h)
         t.copy_(h)
 
+    def _on_host(self, *ts: torch.Tensor) -> bool:
+        """nccl with a host tensor among ``ts``: the op must run on device copies."""
+        return self.dev_stage and any(t.device.type == "cpu" for t in ts)
+
+    def _dev(self, t: torch.Tensor, fn) -> None:
+        """Run a collective on a device copy of host tensor ``t``, copying the result back."""
+        d = t.detach().to(self.device).contiguous()
+        fn(d)
+        t.copy_(d.cpu())
+
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
         self._hook("all_reduce")
         if self.world_size > 1:
             if self.stage and t.device.type != "cpu":
                 return self._host(t, lambda h: dist.all_reduce(h, op=op, group=self.group))
+            if self._on_host(t):
+                return self._dev(t, lambda d: dist.all_reduce(d, op=op, group=self.group))
             return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
         return None
 
@@ -208,6 +223,8 @@ class Communicator:
         if self.world_size > 1:
             if self.stage and t.device.type != "cpu":
                 return self._host(t, lambda h: dist.broadcast(h, src=self.global_rank(root), group=self.group))
+            if self._on_host(t):
+                return self._dev(t, lambda d: dist.broadcast(d, src=self.global_rank(root), group=self.group))
             return dist.broadcast(t, src=self.global_rank(root), group=self.group, async_op=async_op)
         return None
 
@@ -216,6 +233,8 @@ class Communicator:
         if self.world_size > 1:
             if self.stage and t.device.type != "cpu":
                 return self._host(t, lambda h: dist.reduce(h, dst=self.global_rank(root), op=op, group=self.group))
+            if self._on_host(t):
+                return self._dev(t, lambda d: dist.reduce(d, dst=self.global_rank(root), op=op, group=self.group))
             dist.reduce(t, dst=self.global_rank(root), op=op, group=self.group)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
@@ -225,6 +244,11 @@ class Communicator:
                 ho = torch.empty(out.shape, dtype=out.dtype)
                 dist.all_gather_into_tensor(ho, inp.cpu(), group=self.group)
                 out.copy_(ho)
+                return None
+            if self._on_host(out, inp):
+                do = torch.empty(out.shape, dtype=out.dtype, device=self.device)
+                dist.all_gather_into_tensor(do, inp.to(self.device), group=self.group)
+                out.copy_(do)
                 return None
             return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
         out.copy_(inp.reshape(out.shape))
@@ -239,6 +263,11 @@ class Communicator:
                 dist.reduce_scatter_tensor(ho, inp.cpu(), op=op, group=self.group)
                 out.copy_(ho)
                 return None
+            if self._on_host(out, inp):
+                do = torch.empty(out.shape, dtype=out.dtype, device=self.device)
+                dist.reduce_scatter_tensor(do, inp.to(self.device), op=op, group=self.group)
+                out.copy_(do)
+                return None
             return dist.reduce_scatter_tensor(out, inp, op=op, group=self.group, async_op=async_op)
         out.copy_(inp.reshape(out.shape))
         return None
@@ -252,6 +281,11 @@ class Communicator:
                 dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=self.group)
                 out.copy_(ho)
                 return
+            if self._on_host(out, inp):
+                do = torch.empty(out.shape, dtype=out.dtype, device=self.device)
+                dist.all_to_all_single(do, inp.to(self.device), out_splits, in_splits, group=self.group)
+                out.copy_(do)
+                return
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
         else:
             out.copy_(inp)
@@ -261,6 +295,8 @@ class Communicator:
         self._hook("sendrecv")
         if self.stage:
             return self._staged_p2p({d: [t] for d, t in sends.items()}, {s: [t] for s, t in recvs.items()})
+        if self._on_host(*sends.values(), *recvs.values()):
+            return self._device_p2p({d: [t] for d, t in sends.items()}, {s: [t] for s, t in recvs.items()})
         ops = []
         for dst, t in sends.items():
             ops.append(dist.P2POp(dist.isend, t, self.global_rank(dst), self.group))
@@ -294,12 +330,34 @@ class Communicator:
             t.copy_(h)
         return []
 
+    def _device_p2p(self, sends: dict, recvs: dict):
+        """Grouped send/recv of host tensors under nccl through device copies; completes
+        before returning."""
+        ops, dev_recv = [], []
+        for dst, ts in sends.items():
+            for t in ts:
+                ops.append(dist.P2POp(dist.isend, t.detach().to(self.device).contiguous(), self.global_rank(dst),
+                                      self.group))
+        for src, ts in recvs.items():
+            for t in ts:
+                d = torch.empty(t.shape, dtype=t.dtype, device=self.device)
+                dev_recv.append((t, d))
+                ops.append(dist.P2POp(dist.irecv, d, self.global_rank(src), self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for t, d in dev_recv:
+            t.copy_(d)
+        return []
+
     def sendrecv_multi(self, sends: dict, recvs: dict, async_op: bool = False):
         """Like :meth:`sendrecv` with a LIST of tensors per peer, all in one grouped call
         (per peer, the tensors are matched in list order)."""
         self._hook("sendrecv")
         if self.stage:
             return self._staged_p2p(sends, recvs)
+        if self._on_host(*(t for ts in sends.values() for t in ts), *(t for ts in recvs.values() for t in ts)):
+            return self._device_p2p(sends, recvs)
         ops = []
         for dst, ts in sends.items():
             for t in ts:

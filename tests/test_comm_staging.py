@@ -27,3 +27,43 @@ def _worker(comm):
 def test_staged_p2p_matches_direct():
     for o in launch(_worker, 3, timeout=300):
         assert o[False] == o[True]
+
+
+def _dev_stage_worker(comm):
+    """The nccl host-tensor path (device copies) forced on gloo CPU ranks, where the
+    'device' is the host: every primitive must give the direct path's results."""
+    out = {}
+    P, r = comm.world_size, comm.rank
+    for ds in (False, True):
+        comm.dev_stage = ds
+        res = []
+        t = torch.arange(6, dtype=torch.float64) + r
+        comm.all_reduce(t)
+        res.append(t.tolist())
+        b = torch.full((3,), float(r))
+        comm.broadcast(b, 1)
+        res.append(b.tolist())
+        rd = torch.full((2,), float(r + 1))
+        comm.reduce(rd, 0)
+        res.append(rd.tolist() if r == 0 else None)
+        ag = torch.empty(P * 2, dtype=torch.int64)
+        comm.all_gather_into(ag, torch.tensor([r, 10 * r]))
+        res.append(ag.tolist())
+        a2a = torch.empty(P * 2, dtype=torch.int64)
+        comm.all_to_all_single(a2a, torch.arange(P * 2, dtype=torch.int64) + 100 * r)
+        res.append(a2a.tolist())
+        nxt, prv = (r + 1) % P, (r - 1) % P
+        got = torch.empty(4)
+        comm.sendrecv({nxt: torch.full((4,), float(r))}, {prv: got})
+        res.append(got.tolist())
+        g1, g2 = torch.empty(2), torch.empty(3, dtype=torch.int64)
+        comm.sendrecv_multi({nxt: [torch.full((2,), 7.0 + r), torch.arange(3) + r]}, {prv: [g1, g2]})
+        res.append((g1.tolist(), g2.tolist()))
+        out[ds] = res
+    comm.dev_stage = False
+    return out
+
+
+def test_nccl_host_tensor_staging_matches_direct():
+    for o in launch(_dev_stage_worker, 3, timeout=300):
+        assert o[False] == o[True]
