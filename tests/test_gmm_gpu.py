@@ -30,7 +30,7 @@ def _torch_estep(X, w, mu, cov, covariance):
     return torch.exp(logp - lse[:, None]), lse.sum()
 
 
-@pytest.mark.parametrize("d,K,cov_kind", [(5, 3, "full"), (16, 10, "full"), (32, 64, "full"), (40, 7, "full"),
+@pytest.mark.parametrize("d,K,cov_kind", [(5, 3, "full"), (16, 10, "full"), (32, 64, "full"), (40, 7, "full"), (64, 5, "full"),
                                           (12, 9, "diag")])
 def test_estep_and_stats_match_torch(cuda, d, K, cov_kind):
     X, w, mu, cov = _mixture(20000, d, K, d * 100 + K)
@@ -46,6 +46,8 @@ def test_estep_and_stats_match_torch(cuda, d, K, cov_kind):
     assert torch.allclose(S1, Rt.t() @ Xg, rtol=1e-9, atol=1e-6)
     S2t = torch.einsum("nk,ni,nj->kij", Rt, Xg, Xg) if cov_kind == "full" else Rt.t() @ (Xg * Xg)
     assert torch.allclose(S2, S2t, rtol=1e-9, atol=1e-5)
+    Nk2, _, S22 = GM.stats(Xg, Rt.contiguous(), cov_kind)  # a row-major R is accepted too
+    assert torch.allclose(Nk2, Nk, rtol=1e-9, atol=1e-6) and torch.allclose(S22, S2t, rtol=1e-9, atol=1e-5)
 
 
 def test_em_gmm_native_matches_torch_path(cuda):
