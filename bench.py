@@ -268,6 +268,7 @@ def bench_pca(args, comm, torch):
     (PCADaalCollectiveMapper.java:121-147: step 2 runs on the master only). CPU ranks
     (gloo rehearsal) form the same G with an fp32 matmul."""
     from harp_amd.models.common import reduce_partials
+    from harp_amd.ops.eig import eigvalsh
 
     P, r = comm.world_size, comm.rank
     N, d = int(args.pca_n), args.pca_d
@@ -291,7 +292,7 @@ def bench_pca(args, comm, torch):
         cov = (Gs[:d, :d] - cnt * torch.outer(mean, mean)) / (cnt - 1)
         sd = torch.diagonal(cov).sqrt()
         if r == 0:
-            ev = torch.linalg.eigvalsh(cov / torch.outer(sd, sd))
+            ev = eigvalsh(cov / torch.outer(sd, sd))  # one-XCD tridiagonalisation (csrc/eig.hip) on GPUs
         else:
             ev = torch.empty(d, dtype=torch.float64, device=dev)
         if P > 1:
