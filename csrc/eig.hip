@@ -25,8 +25,6 @@
 // precision instead of ~53 bisections).
 #include "common.h"
 
-#include <cstdlib>
-
 namespace {
 
 constexpr int kT = 1024, kW = kT / 64;
@@ -80,21 +78,6 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 
 // A: n x n symmetric, column-major (lda), overwritten. d[n], e[n-1]: the tridiagonal.
 // wsd (doubles, zeroed): p[2][n], then pv[2], sigma[2].
-// tile loads: 0 non-temporal, 1 plain, 2 workgroup-scope (sc0), 3 agent-scope (sc1),
-// 4 plain after invalidating the CU's vector L1 at every arrival
-template <int LF>
-__device__ __forceinline__ void inv_l1() {
-  if constexpr (LF == 4) asm volatile("buffer_inv sc0" ::: "memory");
-}
-template <int LF>
-__device__ __forceinline__ double ld_tile(const double* p) {
-  if constexpr (LF == 0) return __builtin_nontemporal_load(p);
-  if constexpr (LF == 1 || LF == 4) return *p;
-  if constexpr (LF == 2) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int LF>
 __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, long lda, int n,
                                                         double* __restrict__ dout, double* __restrict__ eout, int NB,
                                                         int* __restrict__ ws, double* __restrict__ wsd,
@@ -162,10 +145,13 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
     STAMP(0)
     // super tiles: 64 rows x cps columns of the trailing block per workgroup, each wave
     // cpw of those columns (re-cut every step, so the work stays balanced as m shrinks; the
-    // matrix is therefore read past the CU's L1, where other workgroups' writes of the last
-    // step are not seen). The 16 waves' partial p are summed in LDS, so p takes one fp64
-    // atomic per row and workgroup (one per row and wave contended on the same lines).
-    // A fixed element-to-workgroup ownership (plain L1 loads) balanced badly: 27.6 ms.
+    // matrix is therefore read with agent-scope loads, past the CU's L1, which does not see
+    // other workgroups' writes of the last step -- plain, workgroup-scope and plain after
+    // `buffer_inv sc0` loads all returned stale lines). The 16 waves' partial p are summed in
+    // LDS, so p takes one fp64 atomic per row and workgroup. Measured alternatives
+    // (profiles/r3_eig): non-temporal loads 15.7 ms; a fixed element-to-workgroup ownership
+    // with plain loads (64-row groups: 27.6 ms; cyclic 16-row chunks: 24.3 ms) balanced or
+    // issued worse. What remains is latency: a batch of loads takes ~2.7 us past L1.
     const int RG = (m + 63) / 64;
     const int CSG = NB / RG > 0 ? NB / RG : 1;
     const int cps = (m + CSG - 1) / CSG;
@@ -184,14 +170,14 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
           for (; c + kU <= c1; c += kU, col += kU * lda) {  // kU columns' loads in flight
             double x[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) x[u] = ld_tile<LF>(col + u * lda);
+            for (int u = 0; u < kU; ++u) x[u] = ld_agent(col + u * lda);
 #pragma unroll
             for (int u = 0; u < kU; u += 2) {
               a0 = fma(x[u], sv[c + u], a0);
               a1 = fma(x[u + 1], sv[c + u + 1], a1);
             }
           }
-          for (; c < c1; ++c, col += lda) a0 = fma(ld_tile<LF>(col), sv[c], a0);
+          for (; c < c1; ++c, col += lda) a0 = fma(ld_agent(col), sv[c], a0);
         }
         STAMP(6)
         spart[wv][lane] = a0 + a1;
@@ -215,7 +201,6 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
     }
     STAMP(1)
     if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
-    inv_l1<LF>();
     STAMP(2)
     if (tau != 0.0) {
       const double K = -0.5 * tau * ld_agent(scal + par);
@@ -237,7 +222,7 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
         for (; c + kU <= c1; c += kU, col += kU * lda) {
           double x[kU];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) x[u] = ld_tile<LF>(col + u * lda);
+          for (int u = 0; u < kU; ++u) x[u] = ld_agent(col + u * lda);
 #pragma unroll
           for (int u = 0; u < kU; ++u) {
             const double a = x[u] - (vr * sw[c + u] + wr * sv[c + u]);
@@ -246,12 +231,12 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
           }
         }
         for (; c < c1; ++c, col += lda) {
-          const double a = ld_tile<LF>(col) - (vr * sw[c] + wr * sv[c]);
+          const double a = ld_agent(col) - (vr * sw[c] + wr * sv[c]);
           *col = a;
           if (c == 0 && r >= 2) sp = fma(a, a, sp);
         }
       } else if (c0 == 0 && r >= 2) {
-        const double a = ld_tile<LF>(A + off + r + (long)off * lda);
+        const double a = ld_agent(A + off + r + (long)off * lda);
         sp = fma(a, a, sp);
       }
     }
@@ -259,7 +244,6 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
     if (lane == 0 && sp != 0.0) atomicAdd(scal + 2 + (par ^ 1), sp);
     STAMP(4)
     if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
-    inv_l1<LF>();
     STAMP(5)
   }
   if (stamp)
@@ -366,23 +350,11 @@ HARP_EXPORT int harp_eig_sym(double* A, long lda, int n, double* d, double* e, d
   const int NB = harp_eig_workgroups(n, nb_max);
   if (NB < 1) return HARP_EUNSUPPORTED;
   const size_t lds1 = sizeof(double) * 2 * (size_t)n;
-  const char* lfe = getenv("HARP_EIG_LOAD");
-  const int lf = lfe ? atoi(lfe) : 3;  // agent-scope loads: correct and fastest (profiles/r3_eig)
-  const dim3 grid((unsigned)(NB * 8)), blk(kT);
-  const void* fns[5] = {(const void*)sytrd_coop_kernel<0>, (const void*)sytrd_coop_kernel<1>,
-                        (const void*)sytrd_coop_kernel<2>, (const void*)sytrd_coop_kernel<3>,
-                        (const void*)sytrd_coop_kernel<4>};
-  if (lf < 0 || lf > 4) return HARP_EBADARG;
   if (lds1 > 32 * 1024 &&
-      hipFuncSetAttribute(fns[lf], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess)
+      hipFuncSetAttribute((const void*)sytrd_coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) !=
+          hipSuccess)
     return HARP_ELAUNCH;
-  switch (lf) {
-    case 4: sytrd_coop_kernel<4><<<grid, blk, lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, stamps); break;
-    case 0: sytrd_coop_kernel<0><<<grid, blk, lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, stamps); break;
-    case 1: sytrd_coop_kernel<1><<<grid, blk, lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, stamps); break;
-    case 2: sytrd_coop_kernel<2><<<grid, blk, lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, stamps); break;
-    default: sytrd_coop_kernel<3><<<grid, blk, lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, stamps); break;
-  }
+  sytrd_coop_kernel<<<dim3((unsigned)(NB * 8)), dim3(kT), lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, stamps);
   int st = harp_launch_status();
   if (st != HARP_OK) return st;
   const size_t lds2 = sizeof(double) * 2 * (size_t)n;
