@@ -214,8 +214,11 @@ class GraphShard:
         self.own = torch.arange(me, n_vertices, P, device=dev)
         self.n_local = self.own.numel()
         src, dst = src.to(dev), dst.to(dev)
-        keep = (src % P) == me
-        self.s_loc, self.d_glob = src[keep] // P, dst[keep]
+        if P == 1:  # every edge is local (no boolean mask: masks past 2^31 elements break nonzero)
+            self.s_loc, self.d_glob = src, dst
+        else:
+            keep = (src % P) == me
+            self.s_loc, self.d_glob = src[keep] // P, dst[keep]
         self.csr = None
         if P == 1 or strategy == "allgather":
             if P == 1:

@@ -28,13 +28,35 @@ class CSR:
     n: int
 
 
+SORT_CHUNK = 1 << 30  # torch sorts at most INT_MAX elements per call
+
+
 def build_csr(rows: torch.Tensor, cols: torch.Tensor, n: int) -> CSR:
     """CSR of the (row, col) pairs (rows in [0, n)); neighbour order within a row is the
-    input order (stable sort)."""
-    order = torch.sort(rows.long(), stable=True).indices
-    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=rows.device)
-    rowptr[1:] = torch.cumsum(torch.bincount(rows.long(), minlength=n)[:n], 0)
-    return CSR(rowptr, cols[order].to(torch.int32).contiguous(), n)
+    input order (stable sort). Past 2^30 pairs (a Twitter-size graph has 2.4e9 directed
+    edges) the pairs are stable-sorted in input-order chunks and each chunk's row segments
+    are placed after the earlier chunks' segments of the same row: the same result."""
+    rows = rows.long()
+    dev = rows.device
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    E = rows.numel()
+    if E <= SORT_CHUNK:
+        order = torch.sort(rows, stable=True).indices
+        rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n)[:n], 0)
+        return CSR(rowptr, cols[order].to(torch.int32).contiguous(), n)
+    bounds = list(range(0, E, SORT_CHUNK)) + [E]
+    counts = [torch.bincount(rows[a:b], minlength=n)[:n] for a, b in zip(bounds[:-1], bounds[1:])]
+    rowptr[1:] = torch.cumsum(torch.stack(counts).sum(0), 0)
+    col = torch.empty(E, dtype=torch.int32, device=dev)
+    before = torch.zeros(n, dtype=torch.int64, device=dev)  # this row's pairs in earlier chunks
+    for (a, b), cnt in zip(zip(bounds[:-1], bounds[1:]), counts):
+        r_sorted, order = torch.sort(rows[a:b], stable=True)
+        seg = torch.cumsum(cnt, 0) - cnt  # each row's first position in the sorted chunk
+        rank = torch.arange(b - a, device=dev) - seg[r_sorted]
+        col[rowptr[r_sorted] + before[r_sorted] + rank] = cols[a:b][order].to(torch.int32)
+        before += cnt
+        del r_sorted, order, rank
+    return CSR(rowptr, col, n)
 
 
 def spmm(csr: CSR, M: torch.Tensor) -> torch.Tensor:
