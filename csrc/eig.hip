@@ -258,6 +258,210 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused form (look-ahead): ONE pass over the trailing block and ONE arrival per column.
+// After step k's p_k = tau_k A_k v_k is complete, every workgroup forms w_k and -- from the
+// column k+1 of A_k, updated on the fly (a_i = A_k[i][k+1] - v_i w_0 - w_i v_0) -- the next
+// Householder vector v_{k+1} and tau_{k+1} itself (redundantly, ~2 m loads + two block
+// sums), so the rank-2 update of the trailing block can fold in the next product:
+// a = x - (v_r w_c + w_r v_c) is stored AND multiplied by v_{k+1}[c] in the same pass, and
+// p_{k+1} is complete at the step's single arrival. Same arithmetic as dsytd2; the column
+// update is done once per workgroup instead of read back from memory.
+
+// Householder vector of the column held in c[0..L): c[0] = alpha, sigma = sum c[1..]^2;
+// c becomes v (v[0] = 1). Returns tau; beta in *beta. Every thread of the block calls it.
+__device__ __forceinline__ double house_lds(double* c, int L, double* red, double* beta) {
+  __syncthreads();  // c[] was written by other threads
+  double s = 0.0;
+  for (int i = 1 + (int)threadIdx.x; i < L; i += kT) s = fma(c[i], c[i], s);
+  const double sig = block_sum(s, red);  // its barriers also order the c[] writes before this read
+  const double alpha = c[0];
+  double b = alpha, tau = 0.0, scl = 0.0;
+  if (sig != 0.0) {
+    b = -copysign(sqrt(alpha * alpha + sig), alpha);
+    tau = (b - alpha) / b;
+    scl = 1.0 / (alpha - b);
+  }
+  for (int i = 1 + (int)threadIdx.x; i < L; i += kT) c[i] *= scl;
+  __syncthreads();  // everyone has read c[0] (alpha) before it becomes 1
+  if (threadIdx.x == 0) c[0] = 1.0;
+  __syncthreads();
+  *beta = b;
+  return tau;
+}
+
+// One pass over the mm x mm block at (base, base): if upd, x -= vu[r] wu[c] + wu[r] vu[c]
+// (vu, wu indexed from the block's first row) and stored; if tn != 0, pn[r] += tn * sum_c
+// x * vn[c]. Super tiles of 64 rows x cps columns, re-cut every step (see sytrd_coop_kernel).
+template <int KU>
+__device__ __forceinline__ void fused_pass(double* __restrict__ A, long lda, int base, int mm, int b, int NB,
+                                           bool upd, const double* vu, const double* wu, double tn,
+                                           const double* vn, double* __restrict__ pn, double (*spart)[64]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int RG = (mm + 63) / 64;
+  const int CSG = NB / RG > 0 ? NB / RG : 1;
+  const int cps = (mm + CSG - 1) / CSG;
+  const int cpw = (cps + kW - 1) / kW;
+  const int ST = RG * CSG;
+  const bool mv = tn != 0.0;
+  if (!upd && !mv) return;
+  for (int st = b; st < ST; st += NB) {
+    const int r = (st % RG) * 64 + lane;
+    const int cs0 = (st / RG) * cps, cs1 = cs0 + cps < mm ? cs0 + cps : mm;
+    const int c0 = cs0 + wv * cpw, c1 = c0 + cpw < cs1 ? c0 + cpw : cs1;
+    double a0 = 0.0, a1 = 0.0;
+    if (r < mm && c0 < c1) {
+      const double vr = upd ? vu[r] : 0.0, wr = upd ? wu[r] : 0.0;
+      double* col = A + base + r + (long)(base + c0) * lda;
+      int c = c0;
+      for (; c + KU <= c1; c += KU, col += KU * lda) {  // KU columns' loads in flight
+        double x[KU];
+#pragma unroll
+        for (int u = 0; u < KU; ++u) x[u] = ld_agent(col + u * lda);
+        if (upd) {
+#pragma unroll
+          for (int u = 0; u < KU; ++u) {
+            x[u] -= vr * wu[c + u] + wr * vu[c + u];
+            col[u * lda] = x[u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < KU; u += 2) {
+          a0 = fma(x[u], vn[c + u], a0);
+          a1 = fma(x[u + 1], vn[c + u + 1], a1);
+        }
+      }
+      for (; c < c1; ++c, col += lda) {
+        double x = ld_agent(col);
+        if (upd) {
+          x -= vr * wu[c] + wr * vu[c];
+          *col = x;
+        }
+        a0 = fma(x, vn[c], a0);
+      }
+    }
+    if (mv) {
+      spart[wv][lane] = a0 + a1;
+      __syncthreads();
+      if (wv == 0 && r < mm) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < kW; ++q) acc += spart[q][lane];
+        if (acc != 0.0) atomicAdd(pn + r, tn * acc);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// A: n x n symmetric, column-major (lda), overwritten. d[n], e[n-1]: the tridiagonal.
+// wsd (doubles, zeroed): p[3][n] (p_k, p_{k+1}, and the buffer zeroed for p_{k+2}).
+template <int KU>
+__global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A, long lda, int n,
+                                                         double* __restrict__ dout, double* __restrict__ eout, int NB,
+                                                         int* __restrict__ ws, double* __restrict__ wsd) {
+  extern __shared__ double smem[];
+  double* sv = smem;          // v_k
+  double* sw = smem + n;      // w_k
+  double* sn = smem + 2 * n;  // v_{k+1}
+  __shared__ double red[kW];
+  __shared__ double spart[kW][64];
+  __shared__ int s_b, s_ok;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int b = -1;
+    if ((__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf) == 0) b = atomicAdd(ws, 1);  // HW_REG_XCC_ID
+    s_b = b;
+  }
+  __syncthreads();
+  const int b = s_b;
+  if (b < 0 || b >= NB) return;
+  int* err = ws + 2;
+  const bool lead = b == 0 && tid == 0;
+  if (n < 3) {
+    if (lead) {
+      dout[0] = A[0];
+      if (n == 2) {
+        eout[0] = A[1];
+        dout[1] = A[1 + lda];
+      }
+    }
+    return;
+  }
+  int syncs = 0;
+  // prologue: v_0 from column 0 (rows 1..n-1), p_0 = tau_0 A[1.., 1..] v_0
+  for (int i = tid; i < n - 1; i += kT) sn[i] = A[1 + i];
+  double beta;
+  double tn = house_lds(sn, n - 1, red, &beta);
+  if (lead) {
+    dout[0] = A[0];
+    eout[0] = beta;
+  }
+  fused_pass<KU>(A, lda, 1, n - 1, b, NB, false, nullptr, nullptr, tn, sn, wsd, spart);
+  if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
+  for (int k = 0; k + 2 < n; ++k) {
+    const int off = k + 1, m = n - off;
+    const double tk = tn;
+    double* t = sv;  // v_k <- the look-ahead vector; the old v_{k-1} buffer takes v_{k+1}
+    sv = sn;
+    sn = t;
+    double* pk = wsd + (long)(k % 3) * n;
+    double* pn = wsd + (long)((k + 1) % 3) * n;
+    double* pz = wsd + (long)((k + 2) % 3) * n;
+    // w_k = p_k - (tau_k p_k.v_k / 2) v_k (every workgroup; w = 0 when tau_k = 0)
+    // p_k and column off of A_k are loaded together (one latency); m <= kMaxN = 4 kT
+    constexpr int R = kMaxN / kT;
+    double pr[R], cr[R];
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = tid + q * kT;
+      pr[q] = i < m && tk != 0.0 ? ld_agent(pk + i) : 0.0;
+      cr[q] = i < m ? ld_agent(A + off + i + (long)off * lda) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = tid + q * kT;
+      if (i < m) s = fma(pr[q], sv[i], s);
+    }
+    const double K = -0.5 * tk * block_sum(s, red);
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = tid + q * kT;
+      if (i < m) sw[i] = fma(K, sv[i], pr[q]);
+    }
+    if (b == 0)  // p_{k-1}'s buffer: read by every workgroup before the last arrival
+      for (int i = tid; i < n; i += kT) pz[i] = 0.0;
+    __syncthreads();
+    // column off of A_{k+1}: rows off.. updated on the fly; its diagonal is d[k+1], the
+    // rest gives v_{k+1} (or, at the last step, the final subdiagonal entry)
+    const double v0 = sv[0], w0 = sw[0];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = tid + q * kT;
+      if (i >= m) break;
+      const double a = cr[q] - (sv[i] * w0 + sw[i] * v0);
+      if (i == 0) {
+        if (lead) dout[k + 1] = a;
+      } else {
+        sn[i - 1] = a;
+      }
+    }
+    __syncthreads();
+    if (k + 3 < n) {
+      tn = house_lds(sn, m - 1, red, &beta);
+      if (lead) eout[k + 1] = beta;
+    } else {
+      tn = 0.0;
+      if (lead) eout[k + 1] = sn[0];
+    }
+    // trailing block of the next step: update by (v_k, w_k) and p_{k+1} in one pass
+    fused_pass<KU>(A, lda, off + 1, m - 1, b, NB, tk != 0.0, sv + 1, sw + 1, tn, sn, pn, spart);
+    if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
+  }
+  if (lead) dout[n - 1] = ld_agent(A + (n - 1) + (long)(n - 1) * lda);
+}
+
 // number of eigenvalues of the tridiagonal (d, e^2) below x (Sturm sequence)
 __device__ __forceinline__ int sturm_count(const double* d, const double* e2, int n, double x, double pivmin) {
   double q = d[0] - x;
@@ -332,6 +536,35 @@ __global__ __launch_bounds__(256) void tridiag_multisect_kernel(const double* __
 }
 
 }  // namespace
+
+// Fused look-ahead reduction (sytrd_fused_kernel) + multisection; wsd: zeroed 3 n doubles.
+template <int KU>
+static int launch_fused(double* A, long lda, int n, double* d, double* e, int NB, int* ws, double* wsd, hipStream_t s) {
+  const size_t lds1 = sizeof(double) * 3 * (size_t)n;
+  if (lds1 > 32 * 1024 && hipFuncSetAttribute((const void*)sytrd_fused_kernel<KU>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess)
+    return HARP_ELAUNCH;
+  sytrd_fused_kernel<KU><<<dim3((unsigned)(NB * 8)), dim3(kT), lds1, s>>>(A, lda, n, d, e, NB, ws, wsd);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_eig_sym_fused(double* A, long lda, int n, double* d, double* e, double* w, int nb_max, int* ws,
+                                   double* wsd, int ku, hipStream_t s) {
+  if (n < 1 || n > kMaxN || lda < n || nb_max < 1 || nb_max > kMaxNB || !ws || !wsd) return HARP_EBADARG;
+  const int NB = nb_max;
+  int st = ku == 8 ? launch_fused<8>(A, lda, n, d, e, NB, ws, wsd, s)
+           : ku == 16 ? launch_fused<16>(A, lda, n, d, e, NB, ws, wsd, s)
+           : ku == 32 ? launch_fused<32>(A, lda, n, d, e, NB, ws, wsd, s)
+                      : HARP_EBADARG;
+  if (st != HARP_OK) return st;
+  const size_t lds2 = sizeof(double) * 2 * (size_t)n;
+  if (lds2 > 32 * 1024 &&
+      hipFuncSetAttribute((const void*)tridiag_multisect_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds2) != hipSuccess)
+    return HARP_ELAUNCH;
+  tridiag_multisect_kernel<<<dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), lds2, s>>>(d, e, n, w);
+  return harp_launch_status();
+}
 
 HARP_EXPORT int harp_eig_ws_ints() { return kWsInts; }
 HARP_EXPORT int harp_eig_max_n() { return kMaxN; }

@@ -20,9 +20,16 @@ _lib.register({
     # A, lda, n, d, e, w, nb_max, ws, wsd, stamps, stream
     "harp_eig_sym": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
                      _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    # A, lda, n, d, e, w, nb_max, ws, wsd, ku, stream
+    "harp_eig_sym_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p],
 })
 
 NB_DEFAULT = 32  # workgroups (CUs) of XCD 0
+# reduction form: "fused" (one pass over the trailing block and one arrival per column,
+# look-ahead Householder vector) or "twopass" (matrix-vector pass + rank-2 update pass)
+VARIANT = os.environ.get("HARP_EIG_VARIANT", "fused")
+KU = int(os.environ.get("HARP_EIG_KU", "8"))  # fused form: columns per batch of loads in flight
 
 
 def usable(C: torch.Tensor) -> bool:
@@ -45,12 +52,16 @@ def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None) -> torch.Tenso
         return torch.linalg.eigvalsh(C)
     A = C.contiguous().clone()  # symmetric: row-major storage is the column-major matrix
     ws = torch.zeros(int(k.harp_eig_ws_ints()), dtype=torch.int32, device=dev)
-    wsd = torch.zeros(2 * n + 4, dtype=torch.float64, device=dev)
+    wsd = torch.zeros(3 * n + 4, dtype=torch.float64, device=dev)
     d = torch.empty(n, dtype=torch.float64, device=dev)
     e = torch.empty(n, dtype=torch.float64, device=dev)
     w = torch.empty(n, dtype=torch.float64, device=dev)
-    st = k.harp_eig_sym(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb_max, ws.data_ptr(),
-                        wsd.data_ptr(), _lib.ptr(stamps), _lib.stream_ptr(dev))
+    if VARIANT == "fused" and stamps is None:
+        st = k.harp_eig_sym_fused(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb, ws.data_ptr(),
+                                  wsd.data_ptr(), KU, _lib.stream_ptr(dev))
+    else:
+        st = k.harp_eig_sym(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb_max, ws.data_ptr(),
+                            wsd.data_ptr(), _lib.ptr(stamps), _lib.stream_ptr(dev))
     _lib.check(st, "eig_sym")
     claims, _, err = ws[:3].tolist()
     if claims < nb or err:
