@@ -20,6 +20,9 @@
 //    update of the tile, which also accumulates the next column's squared norm (the next
 //    Householder step needs no extra pass);
 //  * the matrix is read past the CU's L1 (other CUs wrote it one step earlier).
+// The default reduction is the fused look-ahead form (sytrd_fused_kernel below: one pass over
+// the trailing block and ONE arrival per column, 14.4 -> ~11 ms at n = 1000,
+// profiles/r3_eig_fused); the two-pass form above keeps the per-phase cycle stamps.
 // Multisection (tridiag_multisect_kernel): 16 lanes per eigenvalue evaluate Sturm counts at
 // 16 points of its interval, so each round narrows it 17-fold (~13 rounds to machine
 // precision instead of ~53 bisections).
@@ -65,13 +68,14 @@ __device__ __forceinline__ bool arrive(int* cnt, int target, int* err, int* s_ok
 }
 
 // block-wide sum, the result in every thread
+template <int T = kT>
 __device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum_d(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   double s = 0.0;
 #pragma unroll
-  for (int w = 0; w < kW; ++w) s += red[w];
+  for (int w = 0; w < T / 64; ++w) s += red[w];
   __syncthreads();
   return s;
 }
@@ -270,11 +274,12 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
 
 // Householder vector of the column held in c[0..L): c[0] = alpha, sigma = sum c[1..]^2;
 // c becomes v (v[0] = 1). Returns tau; beta in *beta. Every thread of the block calls it.
+template <int T = kT>
 __device__ __forceinline__ double house_lds(double* c, int L, double* red, double* beta) {
   __syncthreads();  // c[] was written by other threads
   double s = 0.0;
-  for (int i = 1 + (int)threadIdx.x; i < L; i += kT) s = fma(c[i], c[i], s);
-  const double sig = block_sum(s, red);  // its barriers also order the c[] writes before this read
+  for (int i = 1 + (int)threadIdx.x; i < L; i += T) s = fma(c[i], c[i], s);
+  const double sig = block_sum<T>(s, red);  // its barriers also order the c[] writes before this read
   const double alpha = c[0];
   double b = alpha, tau = 0.0, scl = 0.0;
   if (sig != 0.0) {
@@ -282,7 +287,7 @@ __device__ __forceinline__ double house_lds(double* c, int L, double* red, doubl
     tau = (b - alpha) / b;
     scl = 1.0 / (alpha - b);
   }
-  for (int i = 1 + (int)threadIdx.x; i < L; i += kT) c[i] *= scl;
+  for (int i = 1 + (int)threadIdx.x; i < L; i += T) c[i] *= scl;
   __syncthreads();  // everyone has read c[0] (alpha) before it becomes 1
   if (threadIdx.x == 0) c[0] = 1.0;
   __syncthreads();

@@ -32,10 +32,10 @@ for n in (1000, 2048, 500):
     C = corr(n)
     ref = torch.linalg.eigvalsh(C)
     row = {"n": n, "rocsolver_ms": round(timed(torch.linalg.eigvalsh, C), 3)}
-    for v, ku in (("twopass", 8), ("fused", 8), ("fused", 16), ("fused", 32)):
+    for v, ku in (("twopass", 8), ("fused", 8)):
         EIG.VARIANT, EIG.KU = v, ku
         w = EIG.eigvalsh(C)
-        tag = v if v == "twopass" else f"fused{ku}"
+        tag = v
         row[tag + "_ms"] = round(timed(EIG.eigvalsh, C), 3)
         row[tag + "_err"] = float((w - ref).abs().max())
     print(row, flush=True)

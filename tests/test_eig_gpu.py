@@ -25,6 +25,17 @@ def test_random_symmetric(cuda, n):
     assert float((w - ref).abs().max()) <= 1e-12 * scale * max(1, n) ** 0.5
 
 
+@pytest.mark.parametrize("variant", ["fused", "twopass"])
+@pytest.mark.parametrize("n", [3, 130, 1000])
+def test_reduction_variants(cuda, variant, n, monkeypatch):
+    """Both reduction forms (fused look-ahead default, two-pass) against rocSOLVER."""
+    monkeypatch.setattr(EIG, "VARIANT", variant)
+    C = _sym(n, 7 * n, cuda)
+    w = EIG.eigvalsh(C)
+    ref = torch.linalg.eigvalsh(C)
+    assert float((w - ref).abs().max()) <= 1e-12 * max(1.0, float(ref.abs().max())) * max(1, n) ** 0.5
+
+
 def test_degenerate_structure(cuda):
     """Zero Householder columns (diagonal, already tridiagonal, repeated eigenvalues) take
     the tau = 0 path."""
