@@ -17,8 +17,8 @@ allreduce + fp64 eig) and LDA-CGS over 1M docs x 1M vocab x 1000 topics with the
 collective, each split over the ranks and bounded by ``--extras-timeout``.
 
 MF-SGD (nested ``sgd`` record): 480,189 x 17,770, 100,480,507 synthetic ratings, rank
-128, H split into 2 slices per rank that rotate around the ring (model rotation); epochs
-timed after warmup; updates/sec = ratings trained / epoch time
+128, H split into ``--sgd-slices`` slices per rank (default 1) that rotate around the ring
+(model rotation); epochs timed after warmup; updates/sec = ratings trained / epoch time
 (SGDCollectiveMapper.java:294-298).
 
 Every record reports the mean (wall clock around the timed loop, max over ranks) and the
@@ -67,7 +67,12 @@ def parse_args(argv=None):
     ap.add_argument("--sgd-rank", type=int, default=128)
     ap.add_argument("--sgd-epochs", type=int, default=10)
     ap.add_argument("--sgd-warmup", type=int, default=1)
-    ap.add_argument("--sgd-slices", type=int, default=2, help="H slices per rank (rotation pipeline depth)")
+    ap.add_argument("--sgd-slices", type=int, default=1,
+                    help="H slices per rank (rotation pipeline depth). 1: each slice step trains twice the cells "
+                         "in half the launches -- 6.3 vs 7.6 ms per 100M-rating epoch on one GPU, 1.76 vs 2.36 ms "
+                         "at the 8-GPU share -- more than the unhidden slice transfer costs (H/P over one xGMI "
+                         "link, ~8 x 40 us per epoch at P = 8; profiles/r3_sgd_slices). 2 overlaps each slice's "
+                         "rotation with the other slice's compute (the reference's numModelSlices default)")
     ap.add_argument("--sgd-timeout", type=float, default=240.0,
                     help="wall-clock bound (s) on the nested MF-SGD record; past it rank 0 prints the "
                          "K-means line with an sgd error and every rank exits")
