@@ -151,7 +151,7 @@ _TINY = ["--points", "3e4", "--centroids", "128", "--backend", "gloo", "--steps"
          "--lda-docs", "600", "--lda-vocab", "900", "--lda-topics", "16", "--lda-len", "20", "--lda-iters", "10"]
 
 
-def _check_full_record(rec, P):
+def _check_full_record(rec, P, slices=1):
     assert rec["n_gpus"] == P and rec["config"]["parallelism"] == f"dp{P}"
     assert rec["steps"] == 10 and rec["value"] > 0 and rec["median_s_per_iter"] > 0
     assert rec["step_s"]["n"] == 10
@@ -163,9 +163,10 @@ def _check_full_record(rec, P):
         assert sub["sync_bytes_per_iter"] > 0, (name, sub)
     s = rec["sgd"]
     assert s["updates_per_sec"] > 0 and s["epoch_s"]["n"] == 10 and 0 < s["train_rmse"] < 2
-    # ring mode: the two slices rotate on different coprime strides (different xGMI links)
+    assert s["slices_per_rank"] == slices
+    # ring mode: two slices rotate on different coprime strides (different xGMI links)
     if P > 2:
-        assert len(set(s["rotation_strides"])) == 2
+        assert len(set(s["rotation_strides"])) == slices
     p = rec["pca"]
     assert p["pass_s"]["n"] == 10 and p["max_eigenvalue"] > 0.9
     lda = rec["lda"]
@@ -174,14 +175,16 @@ def _check_full_record(rec, P):
 
 @pytest.mark.slow
 def test_bench_full_records_three_ranks():
-    """Every nested record (K-means, MF-SGD rotation with ring strides, PCA, LDA push-pull
-    with the server table remote) runs to completion at P=3 over gloo."""
-    _check_full_record(_run_bench(["--gpus", "3"] + _TINY), 3)
+    """Every nested record (K-means, MF-SGD rotation of two slices per rank on ring strides,
+    overlapped with compute, PCA, LDA push-pull with the server table remote) runs to
+    completion at P=3 over gloo."""
+    _check_full_record(_run_bench(["--gpus", "3", "--sgd-slices", "2"] + _TINY), 3, slices=2)
 
 
 @pytest.mark.slow
 def test_bench_full_records_eight_ranks():
-    """Same at the 8-GPU node's world size (8 gloo ranks on the CPU)."""
+    """Same at the 8-GPU node's world size (8 gloo ranks on the CPU), with the bench's
+    default one slice per rank."""
     _check_full_record(_run_bench(["--gpus", "8"] + _TINY), 8)
 
 
