@@ -354,6 +354,9 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     int d = 0, z = 0;
     long p = 0, lo = 0, hi = 0;
     float inv_z = 0.f;
+    // the first 128 entries of the token's doc list sit in registers (zv0: lo + lane, zv1:
+    // lo + 64 + lane), loaded one token ahead; the (rare) rest is read in the loop
+    int zv0 = 0, zv1 = 0;
     if (i < b) {
       d = tdoc[i];
       z = tz[i];
@@ -361,6 +364,8 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       lo = doc_off[d];
       hi = doc_off[d + 1];
       inv_z = inv_nk[z];
+      if (lo + lane < hi) zv0 = __builtin_nontemporal_load(zdoc + lo + lane);
+      if (lo + 64 + lane < hi) zv1 = __builtin_nontemporal_load(zdoc + lo + 64 + lane);
     }
     for (; i < b; i += WAVES) {
       const long inx = i + WAVES;
@@ -373,7 +378,9 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       }
       const float qz = s_qw[z] - inv_z;  // z's factor without this token
       float sb = 0.f;
-      for (long j = lo + lane; j < hi; j += 64) {
+      if (lo + lane < hi && lo + lane != p) sb += zv0 == z ? qz : s_qw[zv0];
+      if (lo + 64 + lane < hi && lo + 64 + lane != p) sb += zv1 == z ? qz : s_qw[zv1];
+      for (long j = lo + 128 + lane; j < hi; j += 64) {
         const int zj = __builtin_nontemporal_load(zdoc + j);
         sb += j == p ? 0.f : (zj == z ? qz : s_qw[zj]);
       }
@@ -386,10 +393,14 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       // next token's doc range and topic factor: its ids have arrived by now
       long lon = 0, hin = 0;
       float invn = 0.f;
+      int zn0 = 0, zn1 = 0;
       if (inx < b) {
         lon = doc_off[dn];
         hin = doc_off[dn + 1];
         invn = inv_nk[zn];
+        // the next token's doc list, in flight while this token samples
+        if (lon + lane < hin) zn0 = __builtin_nontemporal_load(zdoc + lon + lane);
+        if (lon + 64 + lane < hin) zn1 = __builtin_nontemporal_load(zdoc + lon + 64 + lane);
       }
       int nz;
       if (u < B) {  // doc bucket: the topic of one of the doc's other tokens
@@ -400,7 +411,8 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           float pre = inclb - sb;
           for (long j = lo + lane; j < hi; j += 64) {
             if (j == p) continue;
-            const int zj = __builtin_nontemporal_load(zdoc + j);
+            const long o = j - lo - lane;  // 0, 64, 128, ...: registers for the first two
+            const int zj = o == 0 ? zv0 : o == 64 ? zv1 : (int)__builtin_nontemporal_load(zdoc + j);
             f = zj;
             pre += zj == z ? qz : s_qw[zj];
             if (pre > u) break;
@@ -478,12 +490,19 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         flush_wd();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
       }
+      // the next token of the same document: its prefetched list missed this token's move
+      if (dn == d && nz != z && inx < b) {
+        if (lon + lane == p) zn0 = nz;
+        if (lon + 64 + lane == p) zn1 = nz;
+      }
       d = dn;
       z = zn;
       p = pn;
       lo = lon;
       hi = hin;
       inv_z = invn;
+      zv0 = zn0;
+      zv1 = zn1;
     }
     if (wdelta == 1) {
       flush_wd();
