@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--skew", type=float, default=2.0, help="item popularity skew (1 = uniform)")
     ap.add_argument("--blocks-per-xcd", type=int, default=128)
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (only 0 is built)")
-    ap.add_argument("--slices", type=int, default=2, help="H slices per rank (rotation slice steps per epoch)")
+    ap.add_argument("--slices", type=int, default=1,
+                    help="H slices per rank (rotation slice steps per epoch; 1 as in bench.py, profiles/r3_sgd_slices)")
     a = ap.parse_args()
     import torch
 
