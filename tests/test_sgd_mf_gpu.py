@@ -199,3 +199,26 @@ def test_sgd_time_budget_xcd_path(cuda):
         out[name] = m.trained
     assert out["full"] == 2 * 400_000
     assert 0.1 * 800_000 < out["tiny"] < 0.16 * 800_000
+
+
+def test_sgd_one_slice_per_rank_like_two(cuda):
+    """bench.py's MF-SGD record runs one H slice per rank (half the sub-step launches,
+    profiles/r3_sgd_slices): every rating is still trained once per epoch and the model
+    converges like the two-slice rotation."""
+    from harp_amd.models.sgd_mf import SGDCollectiveMapper
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    nu, ni, n = 20000, 3000, 600000
+    u, i, v = synthetic_ratings(nu, ni, n, seed=9)
+    out = {}
+    for S in (1, 2):
+        cfg = SGDConfig(rank=128, epochs=5, test_every=0, num_slices=S, chunk=0, lr=0.005)
+        m = SGDCollectiveMapper(Communicator(None, cuda), cfg, nu, ni, (u, i, v), None)
+        m.init_model(KeyValReader([]))
+        trained = sum(m.train_epoch(ep) for ep in range(cfg.epochs))
+        m.rot.wait_all()
+        torch.cuda.synchronize()
+        out[S] = (trained, m._eval_ring(cfg.epochs - 1)[0])
+    assert out[1][0] == out[2][0] == 5 * n
+    assert abs(out[1][1] - out[2][1]) / out[2][1] < 0.01, out
