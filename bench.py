@@ -344,10 +344,13 @@ def _lda_run(args, comm, torch, local_server: bool, iters: int) -> dict:
     P = comm.world_size
     t0 = time.perf_counter()
     toks = synthetic_corpus(nd, V, 1000, args.lda_len, seed=3, device=comm.device)
+    _trace(comm, "lda corpus", t0)
     cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=1 + iters, local_server=local_server)
     cls = LDAPushPullMapper if args.lda_strategy == "push_pull" else LDACollectiveMapper
     m = cls(comm, cfg, nd, V, toks)
+    _trace(comm, "lda mapper", t0)
     m.init_model(KeyValReader([]))
+    _trace(comm, "lda init_model", t0)
     del toks
     setup_s = time.perf_counter() - t0
     m.iterate(0)
@@ -407,6 +410,12 @@ def bench_lda(args, comm, torch):
 
 
 # ----------------------------------------------------------------------------- helpers
+def _trace(comm, what: str, t0: float) -> None:
+    """HARP_BENCH_TRACE=1: per-rank setup progress on stderr (seconds since ``t0``)."""
+    if os.environ.get("HARP_BENCH_TRACE"):
+        print(f"bench trace rank {comm.rank}: {what} +{time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
+
+
 class _Reader:
     def __iter__(self):
         return iter(())
@@ -509,8 +518,11 @@ def _nested(rec, name, fn, timeout_s, args, comm, torch):
     """rec[name] = fn(...) under a wall-clock guard; a failure is reported inside the
     record, never at the cost of the headline line."""
     guard = _NestedGuard(timeout_s, rec, comm.rank, name)
+    t0 = time.perf_counter()
+    _trace(comm, f"{name} record start", t0)
     try:
         rec[name] = fn(args, comm, torch)
+        _trace(comm, f"{name} record done", t0)
     except Exception as e:  # noqa: BLE001
         rec[name] = {"error": f"{type(e).__name__}: {e}"[:500]}
         print(f"bench: nested {name} record failed on rank {comm.rank}: {e!r}", file=sys.stderr)
