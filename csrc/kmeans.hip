@@ -73,7 +73,7 @@ __device__ __forceinline__ void stage_dma(const __bf16* __restrict__ cm2, int ti
   }
 }
 
-template <int KS, int G, int WAVES, int RG, int PIPE>
+template <int KS, int G, int WAVES, int RG, int PIPE, int PRIO = 0>
 __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
     const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int ntiles, int tail_rg,
     int dcount, int* __restrict__ labels, float* __restrict__ sums, int ld_sums, float* __restrict__ obj_partial,
@@ -85,6 +85,10 @@ __global__ __launch_bounds__(WAVES * 64) void kmeans_assign_kernel(
   const int srot = (r >> 3) & 1;
   const long pbase = ((long)blockIdx.x * WAVES + wave) * (G * 32);
 
+  // PRIO (variant 15): static VALU-arbitration priority for the younger half of the
+  // workgroup, set once (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if constexpr (PRIO)
+    if (__builtin_amdgcn_readfirstlane(tid) >= WAVES * 32) __builtin_amdgcn_s_setprio(1);
   // kick off the first centroid tile before loading this wave's points
   stage_dma<C>(Cm2, 0, smem, wave, lane);
 
@@ -341,27 +345,29 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
   }
 }
 
-template <int KS, int G, int WAVES, int RG, int PIPE = 0>
+template <int KS, int G, int WAVES, int RG, int PIPE = 0, int PRIO = 0>
 int launch_assign(const void* X, long ldx, const void* Cm2, long N, int Kp, int d, int* labels, float* sums,
                   int ld_sums, float* obj_partial, float* mind, hipStream_t stream) {
   using C = KMCfg<KS, G, WAVES, RG>;
   if (Kp % 32) return HARP_EBADARG;
   const long nblk = (N + C::PTS - 1) / C::PTS;
   const int ntiles = (Kp + C::TILE - 1) / C::TILE, tail_rg = (Kp % C::TILE) / 32;
-  kmeans_assign_kernel<KS, G, WAVES, RG, PIPE><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
+  kmeans_assign_kernel<KS, G, WAVES, RG, PIPE, PRIO><<<dim3((unsigned)nblk), dim3(C::THREADS), 0, stream>>>(
       (const __bf16*)X, ldx, (const __bf16*)Cm2, N, ntiles, tail_rg, d, labels, sums, ld_sums, obj_partial, mind);
   return harp_launch_status();
 }
 
 // variant -> (G, WAVES, RG, PIPE). Kp (the rows swept) must be a multiple of 32; Cm2 must
 // hold round_up(Kp, 128) rows (the last stage's DMA reads the whole tile).
-// Only the measured frontier ships (profiles/r1_kmeans_*): 14 is the default for
-// d <= 124, 13 its RG=2 neighbour, 4 the one-group shape wide rows (9..16 k-steps) use.
+// Only the measured frontier ships (profiles/r1_kmeans_*): 15 (= 14 + static priority for the
+// younger half, profiles/r3_setprio) is the default for d <= 124, 13 the RG=2 neighbour of 14,
+// 4 the one-group shape wide rows (9..16 k-steps) use.
 #define KM_VARIANTS(KS)                                                                       \
   switch (variant) {                                                                        \
     case 4: return launch_assign<KS, 1, 16, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s);  \
     case 13: return launch_assign<KS, 4, 8, 2, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     case 14: return launch_assign<KS, 4, 8, 4, 2>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
+    case 15: return launch_assign<KS, 4, 8, 4, 2, 1>(X, ldx, Cm2, N, Kp, d, labels, sums, ld, op, md, s); \
     default: return HARP_EBADARG;                                                           \
   }
 
@@ -370,7 +376,7 @@ int launch_assign(const void* X, long ldx, const void* Cm2, long N, int Kp, int 
 HARP_EXPORT int harp_kmeans_points_per_block(int variant) {
   switch (variant) {
     case 4: return 16 * 1 * 32;
-    case 13: case 14: return 8 * 4 * 32;
+    case 13: case 14: case 15: return 8 * 4 * 32;
     default: return -1;
   }
 }

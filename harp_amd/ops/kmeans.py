@@ -28,7 +28,9 @@ from . import _lib
 
 KP_ALIGN = 128
 ONES = 4  # X columns d..d+3 hold 1.0
-DEFAULT_VARIANT = 14  # (G4, W8, RG4, pipelined): 1024 points per workgroup
+# (G4, W8, RG4, pipelined; 1024 points per workgroup) with static VALU priority for waves 4-7
+# (15; 14 without it: 0.2 % slower, profiles/r3_setprio)
+DEFAULT_VARIANT = 15
 
 
 def padded_dim(d: int) -> int:
@@ -151,7 +153,7 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
             raise NotImplementedError(f"native K-means supports d <= {256 - ONES} (got d={op.d})")
         if dp > 128:
             variant = 4  # the only instantiation for 9..16 k-steps
-        elif variant == DEFAULT_VARIANT and dp // 16 == 5:
+        elif variant in (14, 15) and dp // 16 == 5:
             # the default tiling spills 22 VGPRs at 5 k-steps (d = 61..76); its RG=2 neighbour
             # does not: 112.1 vs 128.5 ms per assign at N = 1e8, d = 64 (profiles/r2_ktail)
             variant = 13

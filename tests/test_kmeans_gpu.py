@@ -29,7 +29,7 @@ def test_generate_points_layout(cuda):
 
 
 @pytest.mark.parametrize("accumulate", ["bucket", "atomic"])
-@pytest.mark.parametrize("variant", [4, 13, 14])
+@pytest.mark.parametrize("variant", [4, 13, 14, 15])
 @pytest.mark.parametrize("n,d,k", [(5000, 100, 300), (777, 10, 10), (4099, 31, 129), (2048, 127, 1000), (1500, 250, 200),
                                    (200000, 100, 2000)])
 def test_assign_matches_torch(cuda, variant, n, d, k, accumulate):
