@@ -16,7 +16,9 @@ no host synchronisation inside an epoch.
 from __future__ import annotations
 
 import math
+import os
 import random
+import sys
 import time
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
@@ -85,6 +87,19 @@ def synthetic_ratings(n_users: int, n_items: int, n_ratings: int, seed: int = 0,
         e = min(s + step, n_ratings)
         val[s:e] = (3.6 + (Ut[u[s:e]] * Vt[it[s:e]]).sum(1) + 0.3 * torch.randn(e - s, generator=g, device=device))
     return u, it, val.clamp_(1.0, 5.0)
+
+
+class _SetupTrace:
+    """HARP_BENCH_TRACE=1: elapsed seconds of init_model's phases on stderr."""
+
+    def __init__(self, rank: int):
+        self.on = bool(os.environ.get("HARP_BENCH_TRACE"))
+        self.rank, self.t0 = rank, time.perf_counter()
+
+    def __call__(self, what: str) -> None:
+        if self.on:
+            print(f"sgd setup rank {self.rank}: {what} +{time.perf_counter() - self.t0:.2f}s", file=sys.stderr,
+                  flush=True)
 
 
 def row_owner(users: torch.Tensor, P: int, seed: int = 0) -> torch.Tensor:
@@ -159,9 +174,11 @@ class SGDCollectiveMapper(CollectiveMapper):
         P, me, dev = self.get_num_workers(), self.get_self_id(), self.device
         S = cfg.num_slices
         n_slices = P * S
+        trace = _SetupTrace(me)
         u, i, v = self._train
         mine = self._owner(u) == me
         u, i, v = u[mine], i[mine], v[mine]
+        trace("own ratings")
         # local dense user index
         self.users = torch.unique(self._all_users_of(me))
         lut = torch.full((self.n_users,), -1, dtype=torch.int64, device=u.device)
@@ -177,7 +194,9 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.local_of_item = (pos % self.ips).to(u.device)
         self.item_perm = perm  # slice s holds items perm[s*ips:(s+1)*ips]
         cells = (self.users.numel(), self.ips) if cfg.xcd_blocks else None
+        trace("user / item maps")
         self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells)
+        trace("rating buckets")
         if self._test is not None:
             tu, ti, tv = self._test
             m = self._owner(tu) == me
@@ -189,13 +208,16 @@ class SGDCollectiveMapper(CollectiveMapper):
         # model: W local, H slices of the blocks initially placed here
         r = cfg.rank
         mean = float(v.mean().item()) if v.numel() else 3.0
+        trace("local mean")
         tot = torch.tensor([mean * v.numel(), float(v.numel())], dtype=torch.float64, device=dev)
         if P > 1:
             self.comm.all_reduce(tot)
         mean = float(tot[0] / max(tot[1], 1))
+        trace("mean allreduce")
         scale = cfg.init_scale if cfg.init_scale > 0 else math.sqrt(mean / r)
         gw = torch.Generator().manual_seed(cfg.seed * 31 + 7 + me)
         self.W = (torch.rand((self.users.numel(), r), generator=gw) * 2 * scale).to(dev)
+        trace("W init")
         orders = get_rotation_sequences(self, cfg.epochs + 2, cfg.seed) if cfg.random_order else None
         # ring mode: slice k rotates on its own stride so the slices use different xGMI links
         # (dymoro.ring_strides); random orders are shared by all slices, as in the reference
@@ -209,6 +231,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             gh = torch.Generator().manual_seed(cfg.seed * 1009 + gs)
             slabs.append((torch.rand((self.ips, r), generator=gh) * 2 * scale).to(dev))
         self.rot = DeviceRotator(self.comm, slabs, name="sgd-h", metrics=self.metrics)
+        trace("H slabs + rotator")
         self.trained = 0
         # timer-bounded steps: one budget for every path (GPU pieces, CPU pieces, and the
         # threaded CPU BlockScheduler, which adds its step times so the tuner can read them)
