@@ -554,13 +554,11 @@ static int launch_fused(double* A, long lda, int n, double* d, double* e, int NB
 }
 
 HARP_EXPORT int harp_eig_sym_fused(double* A, long lda, int n, double* d, double* e, double* w, int nb_max, int* ws,
-                                   double* wsd, int ku, hipStream_t s) {
+                                   double* wsd, hipStream_t s) {
   if (n < 1 || n > kMaxN || lda < n || nb_max < 1 || nb_max > kMaxNB || !ws || !wsd) return HARP_EBADARG;
   const int NB = nb_max;
-  int st = ku == 8 ? launch_fused<8>(A, lda, n, d, e, NB, ws, wsd, s)
-           : ku == 16 ? launch_fused<16>(A, lda, n, d, e, NB, ws, wsd, s)
-           : ku == 32 ? launch_fused<32>(A, lda, n, d, e, NB, ws, wsd, s)
-                      : HARP_EBADARG;
+  // 8 columns per batch of loads: 16 and 32 spill at 16 waves per CU (profiles/r3_eig_fused)
+  int st = launch_fused<8>(A, lda, n, d, e, NB, ws, wsd, s);
   if (st != HARP_OK) return st;
   const size_t lds2 = sizeof(double) * 2 * (size_t)n;
   if (lds2 > 32 * 1024 &&

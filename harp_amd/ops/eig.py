@@ -20,16 +20,15 @@ _lib.register({
     # A, lda, n, d, e, w, nb_max, ws, wsd, stamps, stream
     "harp_eig_sym": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
                      _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
-    # A, lda, n, d, e, w, nb_max, ws, wsd, ku, stream
+    # A, lda, n, d, e, w, nb_max, ws, wsd, stream
     "harp_eig_sym_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
-                           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p],
+                           _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
 })
 
 NB_DEFAULT = 32  # workgroups (CUs) of XCD 0
 # reduction form: "fused" (one pass over the trailing block and one arrival per column,
 # look-ahead Householder vector) or "twopass" (matrix-vector pass + rank-2 update pass)
 VARIANT = os.environ.get("HARP_EIG_VARIANT", "fused")
-KU = int(os.environ.get("HARP_EIG_KU", "8"))  # fused form: columns per batch of loads in flight
 
 
 def usable(C: torch.Tensor) -> bool:
@@ -58,7 +57,7 @@ def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None) -> torch.Tenso
     w = torch.empty(n, dtype=torch.float64, device=dev)
     if VARIANT == "fused" and stamps is None:
         st = k.harp_eig_sym_fused(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb, ws.data_ptr(),
-                                  wsd.data_ptr(), KU, _lib.stream_ptr(dev))
+                                  wsd.data_ptr(), _lib.stream_ptr(dev))
     else:
         st = k.harp_eig_sym(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb_max, ws.data_ptr(),
                             wsd.data_ptr(), _lib.ptr(stamps), _lib.stream_ptr(dev))
