@@ -39,6 +39,9 @@ class SGDConfig:
     epochs: int = 10
     num_slices: int = 2        # model slices per worker (numModelSlices)
     chunk: int = 0             # ratings per GPU update stream (0 = auto: ops.mf.auto_chunk)
+    hot_balance: float = 1.0   # XCD item blocks weigh a row's ratings by 1 + h log2(1 + c / mean c): hot rows
+                               # contend for their L2 lines (ops.mf.balanced_blocks; 6.35 -> 6.02 ms per
+                               # 100M-rating epoch at skew 2, profiles/r3_sgd_hot_balance); 0 = equal counts
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
     kernel_variant: int = 0    # blocked kernel variant (reserved)
@@ -117,7 +120,7 @@ class _Buckets:
     (``ops.mf.sgd_update_blocked``), user-sorted inside a cell; ``cell_off[s]`` holds the
     65 cell offsets of slice s (relative to the slice start)."""
 
-    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device, cells=None):
+    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device, cells=None, hot=0.0):
         g = slice_of_item[cols]
         lc = local_of_item[cols]
         span = int(rows.max().item()) + 1 if rows.numel() else 1
@@ -126,7 +129,7 @@ class _Buckets:
             # equal-work cells: contiguous user / item ranges holding ~1/8 of the slice's
             # ratings each (skewed item popularity would otherwise leave XCDs idle)
             rb = MF.balanced_blocks(g, rows, n_slices, cells[0])
-            cb = MF.balanced_blocks(g, lc, n_slices, cells[1])
+            cb = MF.balanced_blocks(g, lc, n_slices, cells[1], hot=hot)
             cid = g * nc + rb * MF.XCDS + cb
             key = cid * span + rows
         else:
@@ -195,7 +198,8 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.item_perm = perm  # slice s holds items perm[s*ips:(s+1)*ips]
         cells = (self.users.numel(), self.ips) if cfg.xcd_blocks else None
         trace("user / item maps")
-        self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells)
+        self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells,
+                              hot=cfg.hot_balance)
         trace("rating buckets")
         if self._test is not None:
             tu, ti, tv = self._test

@@ -127,15 +127,23 @@ def cell_layout(rows: torch.Tensor, cols: torch.Tensor, n_rows: int, n_cols: int
     return rb * nb + cb
 
 
-def balanced_blocks(group: torch.Tensor, idx: torch.Tensor, n_groups: int, n_idx: int, nb: int = XCDS) -> torch.Tensor:
+def balanced_blocks(group: torch.Tensor, idx: torch.Tensor, n_groups: int, n_idx: int, nb: int = XCDS,
+                    hot: float = 0.0) -> torch.Tensor:
     """Block (0..nb-1) of every (group, idx) record: within each group, contiguous idx
     ranges holding ~equal numbers of records (so skewed item popularity still gives the 8
-    XCDs equal work per sub-step)."""
+    XCDs equal work per sub-step). ``hot`` > 0 weighs each record of an index with c records
+    by 1 + hot * log2(1 + c / mean c): updates of a popular row contend for its L2 lines."""
     flat = group.long() * n_idx + idx.long()
     cnt = torch.bincount(flat, minlength=n_groups * n_idx).view(n_groups, n_idx)
-    excl = torch.cumsum(cnt, 1) - cnt
-    tot = cnt.sum(1, keepdim=True).clamp_min(1)
-    blk = torch.clamp((excl * nb) // tot, max=nb - 1)
+    if hot > 0:
+        c = cnt.double()
+        mean = c.sum(1, keepdim=True) / (c > 0).sum(1, keepdim=True).clamp_min(1)
+        w = c * (1.0 + hot * torch.log2(1.0 + c / mean.clamp_min(1.0)))
+    else:
+        w = cnt
+    excl = torch.cumsum(w, 1) - w
+    tot = w.sum(1, keepdim=True).clamp_min(1)
+    blk = torch.clamp((excl * nb) // tot, max=nb - 1).long()
     return blk.view(-1)[flat]
 
 
