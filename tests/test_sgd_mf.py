@@ -182,3 +182,25 @@ def test_auto_chunk_fills_the_xcd_stream_slots():
     assert auto_chunk(6_280_032, 128) == 32    # 8 GPUs, 2 slices per rank: ~98K ratings per cell
     assert auto_chunk(785_004, 128) == 8       # 8 GPUs, 2 slices, 8 rotation steps: ~12K per cell
     assert auto_chunk(10, 128) == 8            # floor
+
+
+def test_balanced_blocks_hot_weight():
+    """Item blocks stay contiguous and ordered; with the hot-row weight the block holding
+    the most popular items gets fewer ratings (SGDConfig.hot_balance)."""
+    from harp_amd.ops import mf as MF
+
+    g = torch.Generator().manual_seed(3)
+    n_idx, n = 400, 200000
+    idx = (torch.rand(n, generator=g) ** 2 * n_idx).long()  # item 0 hottest (5 % of the ratings)
+    grp = torch.zeros(n, dtype=torch.long)
+    for hot in (0.0, 1.0):
+        blk = MF.balanced_blocks(grp, idx, 1, n_idx, hot=hot)
+        first = torch.full((n_idx,), -1, dtype=torch.long)
+        first[idx] = blk  # one block per item
+        seen = first[first >= 0]
+        assert bool((seen[1:] >= seen[:-1]).all())  # contiguous, ordered ranges
+        counts = torch.bincount(blk, minlength=MF.XCDS)
+        if hot == 0.0:
+            base0 = int(counts[0])
+        else:
+            assert int(counts[0]) < base0  # the hot block sheds ratings
