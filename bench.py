@@ -239,6 +239,10 @@ def bench_sgd(args, comm, torch):
     dt = reduce_max(comm, torch, time.perf_counter() - t0)
     ep_s = clock.durations()
     rot_bytes = _window_bytes(m.metrics, ("rotate_wait",))
+    m.metrics.resolve()
+    # compute-stream time stalled on slice arrivals (HIP events around each stream-level
+    # wait): the part of the model rotation NOT hidden behind the SGD kernels
+    rot_exposed = reduce_max(comm, torch, sum(c["s"] for c in m.metrics.collectives if c["kind"] == "rotate_wait"))
     nt = torch.tensor([float(n)], dtype=torch.float64, device=dev)
     if P > 1:
         comm.all_reduce(nt)
@@ -255,6 +259,7 @@ def bench_sgd(args, comm, torch):
         "warmup": args.sgd_warmup,
         "n_gpus": P,
         "sync_bytes_per_iter": int(rot_bytes / max(args.sgd_epochs, 1)),
+        "rotation_exposed_s_per_epoch": round(rot_exposed / max(args.sgd_epochs, 1), 6),
         "rotation_strides": [s.stride for s in m.schedules],
         "train_rmse": round(train_rmse, 6),
         "users": args.sgd_users, "items": args.sgd_items, "ratings": args.sgd_ratings, "rank": args.sgd_rank,

@@ -164,6 +164,7 @@ def _check_full_record(rec, P, slices=1):
     s = rec["sgd"]
     assert s["updates_per_sec"] > 0 and s["epoch_s"]["n"] == 10 and 0 < s["train_rmse"] < 2
     assert s["slices_per_rank"] == slices
+    assert 0 <= s["rotation_exposed_s_per_epoch"] <= s["s_per_epoch"]
     # ring mode: two slices rotate on different coprime strides (different xGMI links)
     if P > 2:
         assert len(set(s["rotation_strides"])) == slices
