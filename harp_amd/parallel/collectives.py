@@ -480,9 +480,11 @@ def rotate(comm: Communicator, table: Table, rotate_map: Optional[Sequence[int] 
         dst_of = [int(rotate_map[r]) for r in range(P)]
     dst = dst_of[comm.rank]
     srcs = [r for r in range(P) if dst_of[r] == comm.rank]
+    if getattr(table, "_ring_counts", None) is not None and not _derangement(dst_of):
+        table._ring_counts = None  # every rank sees the same map, so all drop the tracked counts
     if (isinstance(table, PackedTable) and table.buffer.is_contiguous() and len(srcs) == 1
             and dst != comm.rank and srcs[0] != comm.rank):
-        return _rotate_packed(comm, table, dst, srcs[0], async_op)
+        return _rotate_packed(comm, table, dst, srcs[0], async_op, dst_of)
     home = _home(table, comm)
     msg = _encode(table.get_partitions(), comm) if dst != comm.rank else None
     if dst == comm.rank and srcs == [comm.rank]:
@@ -518,17 +520,55 @@ class RotateHandle:
         return True
 
 
-def _rotate_packed(comm: Communicator, table: PackedTable, dst: int, src: int, async_op: bool):
+def _derangement(dst_of: Sequence[int]) -> bool:
+    P = len(dst_of)
+    return sorted(dst_of) == list(range(P)) and all(dst_of[r] != r for r in range(P))
+
+
+def _ring_rows(comm: Communicator, table: PackedTable, dst_of: Sequence[int]) -> Optional[int]:
+    """Incoming row count of a header-free rotate, or None when a header is needed.
+
+    A ``static_layout`` PackedTable (flagged on EVERY rank: its row count changes only by
+    rotation) rotated by a derangement (each rank sends to one other rank and receives from
+    one other) lets every rank track all P row counts locally: one all-gather of the counts
+    at the first rotate, then counts[dst_of[r]] <- counts[r] per rotation. Later rotates
+    send the payload with no header round trip and no host sync (the reference's Rotator
+    re-sends the partition headers on every hop, dymoro/Rotator.java)."""
+    P = comm.world_size
+    if not getattr(table, "static_layout", False) or not _derangement(dst_of):
+        return None
+    cache = getattr(table, "_ring_counts", None)
+    if cache is None or cache[0] is not comm:
+        counts = [int(c) for c in comm.all_gather_ints([len(table)])[:, 0]]
+        STATS["rotate_header_roundtrips"] += 1
+    else:
+        counts = cache[1]
+        if counts[comm.rank] != len(table):
+            raise RuntimeError(f"rotate: static_layout table {table.table_id} changed its row count outside "
+                               f"rotate ({counts[comm.rank]} -> {len(table)}); clear static_layout to resize it")
+    nxt = [0] * P
+    for r in range(P):
+        nxt[dst_of[r]] = counts[r]
+    table._ring_counts = (comm, nxt)
+    src = dst_of.index(comm.rank)
+    return counts[src]
+
+
+def _rotate_packed(comm: Communicator, table: PackedTable, dst: int, src: int, async_op: bool,
+                   dst_of: Optional[Sequence[int]] = None):
     """Packed rotate: ONE blocking header round trip (the incoming row count), then the
     incoming ids and rows in one asynchronous grouped send/recv (they used to be two
-    blocking round trips before the payload). ``async_op``: the handle is returned once
-    the payload is in flight; :meth:`RotateHandle.wait` installs it."""
+    blocking round trips before the payload). ``static_layout`` tables under a derangement
+    skip the header after the first rotate (:func:`_ring_rows`). ``async_op``: the handle
+    is returned once the payload is in flight; :meth:`RotateHandle.wait` installs it."""
     dev = comm.device
-    n_out = torch.tensor([len(table)], dtype=torch.int64, device=dev)
-    n_in = torch.empty(1, dtype=torch.int64, device=dev)
-    comm.sendrecv({dst: n_out}, {src: n_in})
-    STATS["rotate_header_roundtrips"] += 1
-    rows = int(n_in.item())
+    rows = _ring_rows(comm, table, dst_of) if dst_of is not None else None
+    if rows is None:
+        n_out = torch.tensor([len(table)], dtype=torch.int64, device=dev)
+        n_in = torch.empty(1, dtype=torch.int64, device=dev)
+        comm.sendrecv({dst: n_out}, {src: n_in})
+        STATS["rotate_header_roundtrips"] += 1
+        rows = int(n_in.item())
     ids_out = torch.tensor(table.ids, dtype=torch.int64, device=dev)
     ids_in = torch.empty(rows, dtype=torch.int64, device=dev)
     buf_out = table.buffer if table.buffer.device == dev else table.buffer.to(dev)

@@ -69,6 +69,29 @@ def _worker(comm):
     src = (r - 1) % P
     out["rotate"] = (t.ids == [src * 2, src * 2 + 1] and bool((t.buffer == float(src)).all()),
                      C.STATS["rotate_header_roundtrips"] - h0)
+    # static_layout packed rotate: row counts tracked locally after one all-gather, so
+    # later rotations (ring, stride 2) send no header; unequal counts per rank
+    s = PackedTable([10 * r + j for j in range(r + 1)], torch.full((r + 1, 2), float(r)), combiner=SUM)
+    s.static_layout = True
+    origin, steps = r, []
+    for stride in (1, 1, 2, 1):
+        h0 = C.STATS["rotate_header_roundtrips"]
+        assert C.rotate(comm, s, [(q + stride) % P for q in range(P)])
+        origin = (origin - stride) % P
+        steps.append((s.ids == [10 * origin + j for j in range(origin + 1)]
+                      and bool((s.buffer == float(origin)).all()),
+                      C.STATS["rotate_header_roundtrips"] - h0))
+    # a map with a fixed point (ranks 0 and 1 swap, 2 keeps) drops the tracked counts on
+    # every rank; the next ring rotation gathers them again
+    held = [(q - 5) % P for q in range(P)]  # origin of each rank's rows after strides 1+1+2+1
+    held = [held[[1, 0, 2][q]] for q in range(P)]  # the swap: rank q now holds its partner's
+    assert C.rotate(comm, s, [1, 0, 2])
+    h0 = C.STATS["rotate_header_roundtrips"]
+    assert C.rotate(comm, s, [(q + 1) % P for q in range(P)])
+    origin = held[(r - 1) % P]
+    steps.append((s.ids == [10 * origin + j for j in range(origin + 1)] and bool((s.buffer == float(origin)).all()),
+                  C.STATS["rotate_header_roundtrips"] - h0))
+    out["ring"] = steps
     out["generic"], out["packed"], out["exp"] = res_generic, res_packed, _expected(r, P)
     return out
 
@@ -83,3 +106,4 @@ def test_join_plan_cached_three_ranks():
         assert p1 == exp and p2 == exp and ok1 and ok2
         assert (m1, b1) == (1, 1) and (m2, b2) == (0, 0)
         assert o["rotate"] == (True, 1)
+        assert o["ring"] == [(True, 1), (True, 0), (True, 0), (True, 0), (True, 1)]
