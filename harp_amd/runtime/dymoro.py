@@ -205,10 +205,19 @@ class Rotator:
 
     Each slice's rotations are issued from its own thread on its own communicator
     channel, so concurrent rotations of different slices keep a per-communicator issue
-    order (the RCCL requirement; SURVEY §2.0 concurrency contract)."""
+    order (the RCCL requirement; SURVEY §2.0 concurrency contract).
 
-    def __init__(self, tables: Sequence[Table], mapper, orders: Optional[Sequence[int]] = None, ctx: str = "rotate"):
+    ``static_rows``: the slices keep their row counts between rotations (the reference's
+    fixed model slices), so PackedTable slices are flagged ``static_layout`` and rotate
+    with no per-hop header round trip after the first (``collectives._ring_rows``)."""
+
+    def __init__(self, tables: Sequence[Table], mapper, orders: Optional[Sequence[int]] = None, ctx: str = "rotate",
+                 static_rows: bool = False):
         self.tables = list(tables)
+        if static_rows:
+            for t in self.tables:
+                if isinstance(t, PackedTable):
+                    t.static_layout = True
         self.mapper = mapper
         P = mapper.get_num_workers()
         self.schedule = RotationSchedule(P, orders)

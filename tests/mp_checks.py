@@ -299,6 +299,16 @@ def runtime_battery(comm):
         a, b = rot.get_split_map(0), rot.get_split_map(1)
     rot.stop()
     res["rotator_full_tour"] = a.get_partition_ids() == [r] and b.get_partition_ids() == [100 + r]
+    # packed slices with fixed (unequal) row counts: header-free after the first hop
+    p0 = PackedTable([10 * r + j for j in range(r + 1)], torch.full((r + 1, 2), float(r)))
+    prot = Rotator([p0], mp, static_rows=True)
+    h0 = C.STATS["rotate_header_roundtrips"]
+    for step in range(P):
+        prot.rotate(0)
+        pa = prot.get_split_map(0)
+    prot.stop()
+    res["rotator_static_rows"] = (pa.ids == [10 * r + j for j in range(r + 1)] and bool((pa.buffer == float(r)).all())
+                                  and C.STATS["rotate_header_roundtrips"] - h0 == (1 if P > 1 else 0))
     # checkpoint / resume across ranks
     d = os.path.join(tempfile.gettempdir(), f"harp_ck_{os.environ.get('MASTER_PORT', '0')}")
     ct = Table(0)
