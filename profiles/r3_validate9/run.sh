@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-3 final validation of HEAD: full GPU suite, smoke, default bench
+set -o pipefail
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r10c
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest_gpu.log
+case $rc in 0|1) ;; *) exit $rc;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 $O/smoke.log
+timeout -k 10 400 python bench.py --steps 10 --warmup 2 > $O/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; grep '^{' $O/bench.log | cut -c1-300
