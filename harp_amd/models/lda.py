@@ -561,6 +561,32 @@ class LDAPushPullMapper(LDACollectiveMapper):
             self.ps.check_overflow()
         super()._after_iteration(it)
 
+    def token_words(self) -> torch.Tensor:
+        """Global word id of each (sorted) local token, from its row in the local layout."""
+        if self.ps is not None:
+            return self.touched.to(self.device)[self.tword.long()]
+        need = torch.tensor(self.need, dtype=torch.int64, device=self.device)
+        r = self.tword.long()
+        return need[r // self.B] * self.B + r % self.B
+
+    def check_counts(self) -> bool:
+        """Exact invariant (test / debug; dense [vocab, K_pad] scratch): the word-topic
+        counts rebuilt from every worker's (word, z) equal the server table at each owner,
+        and the topic sums equal their column sums. Collective; same answer on all ranks."""
+        Kp, B, P = self.Kp, self.B, self.get_num_workers()
+        nblocks = math.ceil(self.vocab / B)
+        flat = self.token_words() * Kp + self.tz.long()
+        rebuilt = torch.bincount(flat, minlength=nblocks * B * Kp).view(nblocks, B, Kp).to(torch.float64)
+        if P > 1:
+            self.comm.all_reduce(rebuilt)
+        ok = bool(torch.equal(rebuilt.sum((0, 1)).round().to(torch.int32), self.nk))
+        for b in self.glob.sorted_ids():
+            ok = ok and bool(torch.equal(rebuilt[b].round().to(torch.int32), self.glob[b]))
+        flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=self.device)
+        if P > 1:
+            self.comm.all_reduce(flag)
+        return float(flag.item()) == 0.0
+
     def log_likelihood(self, it: int) -> float:
         cfg = self.cfg
         K = cfg.num_topics

@@ -480,10 +480,31 @@ def rotate(comm: Communicator, table: Table, rotate_map: Optional[Sequence[int] 
         dst_of = [int(rotate_map[r]) for r in range(P)]
     dst = dst_of[comm.rank]
     srcs = [r for r in range(P) if dst_of[r] == comm.rank]
-    if getattr(table, "_ring_counts", None) is not None and not _derangement(dst_of):
-        table._ring_counts = None  # every rank sees the same map, so all drop the tracked counts
-    if (isinstance(table, PackedTable) and table.buffer.is_contiguous() and len(srcs) == 1
-            and dst != comm.rank and srcs[0] != comm.rank):
+    packed = (isinstance(table, PackedTable) and table.buffer.is_contiguous() and len(srcs) == 1
+              and dst != comm.rank and srcs[0] != comm.rank)
+    if getattr(table, "ring_rows", False):
+        # header-free rotation needs every rank on the packed path with the row count the
+        # others tracked: agree on both (one 2-element all-reduce), so a rank whose buffer
+        # went non-contiguous or whose table was resized outside rotate cannot leave its
+        # peers waiting in a header-free send/recv -- every rank takes the header path or
+        # raises together
+        cache = getattr(table, "_ring_counts", None)
+        resized = cache is not None and cache[0] is comm and cache[1][comm.rank] != len(table)
+        flag = torch.tensor([0.0 if packed else 1.0, 1.0 if resized else 0.0], dtype=torch.float64,
+                            device=comm.device)
+        comm.all_reduce(flag)
+        bad_layout, any_resized = flag.tolist()
+        if any_resized:
+            table._ring_counts = None
+            raise RuntimeError(f"rotate: ring_rows table {table.table_id} changed its row count outside rotate "
+                               f"on some rank (here {len(table)} rows); clear ring_rows to resize it")
+        if bad_layout:
+            packed = False
+    if not packed or not _derangement(dst_of):
+        # every rank sees the same map and the same agreed flag, so all drop the tracked counts
+        if isinstance(table, PackedTable) or getattr(table, "_ring_counts", None) is not None:
+            table._ring_counts = None
+    if packed:
         return _rotate_packed(comm, table, dst, srcs[0], async_op, dst_of)
     home = _home(table, comm)
     msg = _encode(table.get_partitions(), comm) if dst != comm.rank else None
@@ -528,14 +549,15 @@ def _derangement(dst_of: Sequence[int]) -> bool:
 def _ring_rows(comm: Communicator, table: PackedTable, dst_of: Sequence[int]) -> Optional[int]:
     """Incoming row count of a header-free rotate, or None when a header is needed.
 
-    A ``static_layout`` PackedTable (flagged on EVERY rank: its row count changes only by
-    rotation) rotated by a derangement (each rank sends to one other rank and receives from
+    A ``ring_rows`` PackedTable (flagged on EVERY rank: its row count changes only by
+    rotation; ``static_layout`` is a different promise -- a fixed id layout -- and is not
+    read here) rotated by a derangement (each rank sends to one other rank and receives from
     one other) lets every rank track all P row counts locally: one all-gather of the counts
     at the first rotate, then counts[dst_of[r]] <- counts[r] per rotation. Later rotates
     send the payload with no header round trip and no host sync (the reference's Rotator
     re-sends the partition headers on every hop, dymoro/Rotator.java)."""
     P = comm.world_size
-    if not getattr(table, "static_layout", False) or not _derangement(dst_of):
+    if not getattr(table, "ring_rows", False) or not _derangement(dst_of):
         return None
     cache = getattr(table, "_ring_counts", None)
     if cache is None or cache[0] is not comm:
@@ -543,9 +565,7 @@ def _ring_rows(comm: Communicator, table: PackedTable, dst_of: Sequence[int]) ->
         STATS["rotate_header_roundtrips"] += 1
     else:
         counts = cache[1]
-        if counts[comm.rank] != len(table):
-            raise RuntimeError(f"rotate: static_layout table {table.table_id} changed its row count outside "
-                               f"rotate ({counts[comm.rank]} -> {len(table)}); clear static_layout to resize it")
+        assert counts[comm.rank] == len(table), "rotate() agrees on the tracked counts before this point"
     nxt = [0] * P
     for r in range(P):
         nxt[dst_of[r]] = counts[r]
@@ -558,7 +578,7 @@ def _rotate_packed(comm: Communicator, table: PackedTable, dst: int, src: int, a
                    dst_of: Optional[Sequence[int]] = None):
     """Packed rotate: ONE blocking header round trip (the incoming row count), then the
     incoming ids and rows in one asynchronous grouped send/recv (they used to be two
-    blocking round trips before the payload). ``static_layout`` tables under a derangement
+    blocking round trips before the payload). ``ring_rows`` tables under a derangement
     skip the header after the first rotate (:func:`_ring_rows`). ``async_op``: the handle
     is returned once the payload is in flight; :meth:`RotateHandle.wait` installs it."""
     dev = comm.device

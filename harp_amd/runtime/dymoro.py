@@ -208,8 +208,10 @@ class Rotator:
     order (the RCCL requirement; SURVEY §2.0 concurrency contract).
 
     ``static_rows``: the slices keep their row counts between rotations (the reference's
-    fixed model slices), so PackedTable slices are flagged ``static_layout`` and rotate
-    with no per-hop header round trip after the first (``collectives._ring_rows``)."""
+    fixed model slices), so PackedTable slices are flagged ``ring_rows`` and rotate with
+    no per-hop header round trip after the first (``collectives._ring_rows``). Their ids
+    change every hop, so they are NOT ``static_layout`` (that flag promises a fixed id
+    layout to the cached push / pull / join plans)."""
 
     def __init__(self, tables: Sequence[Table], mapper, orders: Optional[Sequence[int]] = None, ctx: str = "rotate",
                  static_rows: bool = False):
@@ -217,7 +219,7 @@ class Rotator:
         if static_rows:
             for t in self.tables:
                 if isinstance(t, PackedTable):
-                    t.static_layout = True
+                    t.ring_rows = True
         self.mapper = mapper
         P = mapper.get_num_workers()
         self.schedule = RotationSchedule(P, orders)

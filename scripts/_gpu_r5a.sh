@@ -1,9 +1,9 @@
 #!/bin/bash
-# bench.py with the nested PCA / LDA records (default N=1 run, as the driver runs it)
-set -o pipefail
-export TMPDIR=/tmp
+# round 4 first look: full GPU suite (no -x) + LDA push-pull layout diagnostic
 mkdir -p gpurun_out/r5a
-s=$(date +%s)
-timeout -k 10 600 python bench.py > gpurun_out/r5a/bench.log 2>&1 || { tail -30 gpurun_out/r5a/bench.log; exit 1; }
-echo "wall $(( $(date +%s) - s )) s"
-grep '^{' gpurun_out/r5a/bench.log | tail -1 | python -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['value']); print(r['sgd']); print(r['pca']); print(r['lda'])"
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r5a/pytest.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 240 python -u scripts/diag_lda_pp.py > gpurun_out/r5a/diag.log 2>&1
+echo "diag rc=$?"

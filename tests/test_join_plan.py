@@ -69,10 +69,10 @@ def _worker(comm):
     src = (r - 1) % P
     out["rotate"] = (t.ids == [src * 2, src * 2 + 1] and bool((t.buffer == float(src)).all()),
                      C.STATS["rotate_header_roundtrips"] - h0)
-    # static_layout packed rotate: row counts tracked locally after one all-gather, so
+    # ring_rows packed rotate: row counts tracked locally after one all-gather, so
     # later rotations (ring, stride 2) send no header; unequal counts per rank
     s = PackedTable([10 * r + j for j in range(r + 1)], torch.full((r + 1, 2), float(r)), combiner=SUM)
-    s.static_layout = True
+    s.ring_rows = True
     origin, steps = r, []
     for stride in (1, 1, 2, 1):
         h0 = C.STATS["rotate_header_roundtrips"]
@@ -107,3 +107,67 @@ def test_join_plan_cached_three_ranks():
         assert (m1, b1) == (1, 1) and (m2, b2) == (0, 0)
         assert o["rotate"] == (True, 1)
         assert o["ring"] == [(True, 1), (True, 0), (True, 0), (True, 0), (True, 1)]
+
+
+def _blk_ids(b):
+    return [3 * b + j for j in range(2 + b % 2)]  # unequal row counts per block
+
+
+def _rot_worker(comm):
+    """Rotator(static_rows=True) under the reference's RANDOM rotation orders (maps with
+    and without fixed points), a join against the rotated table after every hop, then a
+    resize on one rank: every rank must raise together (no header-free hang)."""
+    import random
+
+    from harp_amd.runtime.dymoro import Rotator, RotationSchedule, create_rotation_order
+
+    P, r = comm.world_size, comm.rank
+
+    class _M:
+        pass
+
+    mp = _M()
+    mp.comm, mp.get_num_workers = comm, (lambda: P)
+    orders = create_rotation_order(random.Random(5), 3, P)
+    sched = RotationSchedule(P, orders)
+    tab = PackedTable(_blk_ids(r), torch.full((len(_blk_ids(r)), 2), float(r)), combiner=SUM)
+    rot = Rotator([tab], mp, orders=orders, static_rows=True)
+    steps = []
+    for n in range(1, 2 * P + 1):
+        rot.rotate(0)
+        t = rot.get_split_map(0)
+        it, s = divmod(n, P)
+        blk = [sched.placement(it, s).index(q) for q in range(P)]
+        ok_rows = t.ids == _blk_ids(blk[r]) and bool((t.buffer == float(blk[r])).all())
+        # join against the rotated (ring_rows, NOT static_layout) table
+        mine = [v for v in range(3 * P) if v % P == r]
+        dyn = PackedTable(mine, torch.tensor([[v + 1.0] for v in mine]), combiner=SUM)
+        assert C.join(comm, dyn, None, t)
+        holders = {}
+        for q in range(P):
+            for v in _blk_ids(blk[q]):
+                holders.setdefault(v, set()).add(q)
+        exp = {v: float(v + 1) for v in _blk_ids(blk[r])}
+        exp.update({v: float(v + 1) for v in mine if v not in holders})
+        got = {i: float(dyn[i][0]) for i in dyn.ids}
+        steps.append(ok_rows and got == exp and not getattr(t, "static_layout", False))
+    rot.stop()
+    # a resize outside rotate on rank 0 only: all ranks raise (raise_errors), none hangs
+    ring = [(q + 1) % P for q in range(P)]
+    assert C.rotate(comm, tab, ring)  # a derangement: every rank now tracks the row counts
+    comm.raise_errors = True
+    if r == 0:
+        tab.set_contents(tab.ids[:1], tab.buffer[:1].clone())
+    raised = False
+    try:
+        C.rotate(comm, tab, ring)
+    except RuntimeError:
+        raised = True
+    comm.raise_errors = False
+    return {"steps": steps, "raised": raised}
+
+
+def test_rotator_random_orders_then_join_three_ranks():
+    for o in launch(_rot_worker, 3, timeout=300):
+        assert all(o["steps"]), o["steps"]
+        assert o["raised"]
