@@ -414,8 +414,9 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
 //    started, and a launch starts with invalidated caches), so no invalidation is needed;
 //    W rows (written by other CUs of the same XCD in earlier sub-steps) are read from L2;
 //  * the last block to leave zeroes the counters for the next launch on this stream;
-//  * a wait gives up after ~1 s and raises the error word (a launch-geometry bug must
-//    never hang the GPU); the host checks it.
+//  * a wait gives up after ~1 s and raises the error word (1; a launch-geometry bug must
+//    never hang the GPU); a block that runs on another XCD than blockIdx.x mod 8 raises it
+//    too (2); the host checks it once per epoch.
 // ws layout (int32): claim[64] | done[64] | fin[64] | exit | error
 constexpr int kFlowWs = 3 * 64 + 2;
 
@@ -446,6 +447,12 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
   const int nxt = (x + 1) % XCDS;
   const int sl = threadIdx.x & 15;
   const int sub = threadIdx.x >> 4;
+  // the visibility argument above needs block b to RUN on XCD b mod 8 (the round-robin
+  // dispatch of a single-partition device); a different dispatch mapping would train with
+  // stale L2 lines silently, so check the hardware id and raise the error word (2) -- the
+  // host refuses the pass (ops.mf.check_flow_errors)
+  if (threadIdx.x == 0 && (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf) != x)  // HW_REG_XCC_ID
+    __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int step = 0; step < steps; ++step) {
     const int cell = x * XCDS + (x + step) % XCDS;
     const long a = off[cell];

@@ -44,7 +44,7 @@ class SGDConfig:
                                # 100M-rating epoch at skew 2, profiles/r3_sgd_hot_balance); 0 = equal counts
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
-    kernel_variant: int = 0    # blocked kernel variant (reserved)
+    kernel_variant: int = 0    # blocked kernel: 0 = a launch per sub-step, 1 = persistent flow kernel (ops.mf)
     train_fraction: float = 1.0  # per rotation step each cell trains this fraction (window advances per epoch)
     random_order: bool = False  # random rotation orders (RotationUtil) vs ring
     test_every: int = 5        # rmseIteInterval
@@ -332,6 +332,8 @@ class SGDCollectiveMapper(CollectiveMapper):
             if torch.cuda.is_available() and self.device.type == "cuda":
                 torch.cuda.synchronize()
             self.epoch_times.append(time.perf_counter() - t0)
+            if self.cfg.kernel_variant == MF.FLOW_VARIANT and self.device.type == "cuda":
+                MF.check_flow_errors(self.device)  # a timed-out wait / foreign XCD invalidates the epoch
             self.metrics.end_iteration("sgd", ep, trained=n, epoch_s=self.epoch_times[-1],
                                        updates_per_s=n / max(self.epoch_times[-1], 1e-12))
             if self.cfg.test_every and ((ep + 1) % self.cfg.test_every == 0 or ep == self.cfg.epochs - 1):

@@ -77,7 +77,13 @@ def coop_workgroups(max_n: int, machines: int = 1) -> int:
     one_cu_max = int(_lib.kernels().harp_svm_max_rows())
     env = os.environ.get("HARP_SVM_COOP_NB")
     if env is not None:
-        nb = int(env)
+        try:
+            nb = int(env)
+        except ValueError:
+            nb = -1
+        if not 0 <= nb <= COOP_MAX_NB:
+            warnings.warn(f"HARP_SVM_COOP_NB={env!r} is outside [0, {COOP_MAX_NB}]: cooperative SMO off")
+            nb = 0
     elif max_n < COOP_MIN_ROWS or (machines > COOP_MAX_MACHINES and max_n <= one_cu_max):
         return 0
     else:
@@ -122,11 +128,12 @@ def _smo_coop(K, ids, moff, nm, max_n, y, kd, C, eps, tau, max_iter, ident, nb):
 
 
 def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Tensor]], C: float, eps: float,
-               tau: float, max_iter: int, ident: bool = False) -> List[Tuple[torch.Tensor, torch.Tensor, int]]:
+               tau: float, max_iter: int, ident: bool = False) -> Optional[List[Tuple[torch.Tensor, torch.Tensor, int]]]:
     """Train every binary machine ``(idx, y)`` (rows / columns ``idx`` of the fp64 Gram
     ``K``, labels +-1) with the device SMO, all machines in one launch. ``ident``: one
     machine over all of K (idx = 0..n-1, no index indirection). Returns per machine
-    (alpha, gradient G = Q alpha - e, SMO steps)."""
+    (alpha, gradient G = Q alpha - e, SMO steps), or None when no device kernel can take
+    the machines (the caller runs the PyTorch loop)."""
     dev = K.device
     idx = [m[0].to(dev, torch.int32) for m in machines]
     ys = [m[1].to(dev, torch.float64).reshape(-1) for m in machines]
@@ -147,7 +154,13 @@ def smo_device(K: torch.Tensor, machines: Sequence[Tuple[torch.Tensor, torch.Ten
             o += n
         return out
     if max(sizes) > int(_lib.kernels().harp_svm_max_rows()):
-        raise ValueError(f"device SMO: {max(sizes)} rows per machine exceed {int(_lib.kernels().harp_svm_max_rows())}")
+        # only the cooperative kernel takes machines this large, and it could not run (a
+        # transient co-residency failure, or coop switched off): the caller falls back to
+        # the PyTorch SMO loop instead of aborting the fit
+        warnings.warn(f"device SMO: {max(sizes)} rows per machine exceed the one-CU kernel's "
+                      f"{int(_lib.kernels().harp_svm_max_rows())} and the cooperative kernel did not run; "
+                      "falling back to the PyTorch SMO loop")
+        return None
     iters = torch.zeros(len(machines), dtype=torch.int32, device=dev)
     st = _lib.kernels().harp_svm_smo(K.data_ptr(), K.stride(0), ids.data_ptr(), moff.data_ptr(), len(machines),
                                      max(sizes), y.data_ptr(), kd.data_ptr(), a.data_ptr(), g.data_ptr(),
@@ -180,9 +193,11 @@ class BinarySVM:
         K = kernel_matrix(Xd, Xd, self.kernel, self.sigma) if K is None else K.double()
         if self.solver != "torch" and native_smo_ok(K, n):
             ar = torch.arange(n, device=K.device)
-            a, G, steps = smo_device(K.contiguous(), [(ar, yv)], self.C, self.eps, self.tau, self.max_iter,
-                                     ident=K.shape[0] == n)[0]
-            return self._finish(Xd, yv, a, G, steps)
+            res = smo_device(K.contiguous(), [(ar, yv)], self.C, self.eps, self.tau, self.max_iter,
+                             ident=K.shape[0] == n)
+            if res is not None:
+                a, G, steps = res[0]
+                return self._finish(Xd, yv, a, G, steps)
         Kd = torch.diagonal(K).clone()
         a = torch.zeros(n, dtype=torch.float64, device=K.device)
         G = -torch.ones(n, dtype=torch.float64, device=K.device)
@@ -280,9 +295,10 @@ class MultiClassSVM:
             proto = BinarySVM(**self.kw)
             res = smo_device(Kfull.contiguous(), [(idx, yy) for _, idx, yy in pairs], proto.C, proto.eps, proto.tau,
                              proto.max_iter)
-            for (key, idx, yy), (al, G, steps) in zip(pairs, res):
-                self.machines[key] = BinarySVM(**self.kw)._finish(Xdense[idx], yy.to(al.device), al, G, steps)
-            return self
+            if res is not None:
+                for (key, idx, yy), (al, G, steps) in zip(pairs, res):
+                    self.machines[key] = BinarySVM(**self.kw)._finish(Xdense[idx], yy.to(al.device), al, G, steps)
+                return self
         for key, idx, yy in pairs:
             self.machines[key] = BinarySVM(**self.kw).fit(Xdense[idx], yy, Kfull[idx][:, idx])
         return self

@@ -83,8 +83,12 @@ def _flow_ws(device: torch.device) -> torch.Tensor:
 def check_flow_errors(device: torch.device) -> None:
     """Raise if a flow launch on ``device`` gave up waiting on a neighbour (host sync)."""
     for (idx, _), ws in _FLOW_WS.items():
-        if idx == device.index and int(ws[-1].item()):
+        code = int(ws[-1].item()) if idx == device.index else 0
+        if code:
             ws[-1].zero_()
+            if code == 2:
+                raise RuntimeError("MF-SGD flow kernel: a block ran on another XCD than blockIdx.x mod 8 (dispatch "
+                                   "mapping differs from round-robin; results of that pass are invalid)")
             raise RuntimeError("MF-SGD flow kernel: a cross-XCD wait timed out (results of that pass are invalid)")
 
 
