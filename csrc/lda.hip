@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
-    unsigned long long seed) {
+    unsigned long long seed, int det) {
   constexpr int KP = 64 * TPL;
   constexpr int WAVES = 4;
   __shared__ float s_inv[KP];
@@ -129,8 +129,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const long wave_g = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  // det: ONE wave samples every chunk in order (no races on doc rows: bit-reproducible,
+  // independent of the word-row numbering; a test mode, launched as one workgroup)
+  const long wave_g = det ? (wv == 0 ? 0 : nchunks) : ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = det ? 1 : ((long)gridDim.x * blockDim.x) >> 6;
   const int k0 = lane * TPL;
   int* nw0s = &s_nw0[wv][k0];
   for (long c = wave_g; c < nchunks; c += nwaves) {
@@ -525,22 +527,23 @@ namespace {
 template <class DT, int XW = 0>
 int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
                int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
-               unsigned long long seed, hipStream_t s) {
+               unsigned long long seed, int det, hipStream_t s) {
   long blocks = (nchunks + 3) / 4;  // 4 waves per block
   if (blocks > 8192) blocks = 8192;
+  if (det) blocks = 1;
   const dim3 g((unsigned)blocks), bl(256);
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
     lda_cgs_kernel<4, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                           nk_delta, K, alpha, beta, seed);
+                                           nk_delta, K, alpha, beta, seed, det);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
     lda_cgs_kernel<8, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                           nk_delta, K, alpha, beta, seed);
+                                           nk_delta, K, alpha, beta, seed, det);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
     lda_cgs_kernel<16, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                            nk_delta, K, alpha, beta, seed);
+                                            nk_delta, K, alpha, beta, seed, det);
   }
   return harp_launch_status();
 }
@@ -555,9 +558,12 @@ HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const l
   // variant 0: compiler occupancy; 3: two more waves per SIMD (the default). The doc-row
   // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
   // (profiles/r1_lda/occupancy) and are no longer built.
+  // variant | 0x100: deterministic one-wave sampling (tests)
+  const int det = (variant & 0x100) ? 1 : 0;
+  variant &= 0xff;
   if (K <= 0 || K > 1024 || ldw % 4 || (variant != 0 && variant != 3)) return HARP_EBADARG;
 #define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks
-#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
+#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
     return variant == 3 ? launch_cgs<int, 2>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
@@ -588,7 +594,7 @@ template <int WAVES, class DT>
 int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, const int* order,
                   int* work, const long* tpos,
                   const long* doc_off, unsigned short* zdoc, DT* ndk, int ldd, int* nwk, int ldw, const float* inv_nk,
-                  int* nk_delta, int K, float alpha, float beta, unsigned long long seed, hipStream_t s) {
+                  int* nk_delta, int K, float alpha, float beta, unsigned long long seed, int det, hipStream_t s) {
   const int Kp = (K + 63) / 64 * 64;
   const int ldelta = Kp <= 4096;  // LDS topic-sum deltas while they cost at most 16 KB
   const int wdelta = sparse_wdelta(Kp);
@@ -606,6 +612,7 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
   if (per_cu < 1) per_cu = 1;
   long blocks = nchunks;
   if (blocks > 256 * per_cu) blocks = 256 * per_cu;
+  if (det) blocks = 1;
   lda_cgs_sparse_kernel<WAVES, DT><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
       tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
       beta, seed, ldelta, wdelta);
@@ -623,6 +630,8 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
                                     float alpha, float beta, unsigned long long seed, int waves, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
   if (K <= 0 || K > 16384 || ldw < K || (ndk && ldd < K) || !tpos || !doc_off || !zdoc || !work) return HARP_EBADARG;
+  const int det = waves < 0 ? 1 : 0;  // waves < 0: one one-wave workgroup, bit-reproducible (tests)
+  if (det) waves = 1;
   if (waves == 0) {  // auto: the smallest workgroup that still puts >= 24 waves on a CU
     const int Kp = (K + 63) / 64 * 64;
     waves = 16;
@@ -635,7 +644,7 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
     }
   }
 #define SP_ARGS tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc
-#define SP_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, s
+#define SP_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, s
   if (ndk_bits == 16) {
     if (ldd % 2) return HARP_EBADARG;
     unsigned short* n16 = (unsigned short*)ndk;

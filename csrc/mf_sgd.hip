@@ -417,8 +417,15 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
 //  * a wait gives up after ~1 s and raises the error word (1; a launch-geometry bug must
 //    never hang the GPU); a block that runs on another XCD than blockIdx.x mod 8 raises it
 //    too (2); the host checks it once per epoch.
-// ws layout (int32): claim[64] | done[64] | fin[64] | exit | error
-constexpr int kFlowWs = 3 * 64 + 2;
+// ws layout (int32): claim[64] | done[64] | fin[64] | xcc map[9] | exit | error
+constexpr int kFlowWs = 3 * 64 + 9 + 2;
+
+// compare-and-swap 0 -> v; returns the previous value (0 when this call stored v)
+__device__ __forceinline__ int cas_zero(int* p, int v) {
+  int expected = 0;
+  __hip_atomic_compare_exchange_strong(p, &expected, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return expected;
+}
 
 // raise a completion flag after writing this XCD's L2 back (agent-scope release), with an
 // explicit wait so the flag cannot overtake the write-back
@@ -441,18 +448,28 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
   int* claim = ws;
   int* done = ws + 64;
   int* fin = ws + 128;
-  int* exit_ctr = ws + 192;
-  int* err = ws + 193;
+  int* xccmap = ws + 192;  // [8] XCC id + 1 per residue, [8] bit set of claimed XCCs
+  int* exit_ctr = ws + 201;
+  int* err = ws + 202;
   const int x = blockIdx.x % XCDS;
   const int nxt = (x + 1) % XCDS;
   const int sl = threadIdx.x & 15;
   const int sub = threadIdx.x >> 4;
-  // the visibility argument above needs block b to RUN on XCD b mod 8 (the round-robin
-  // dispatch of a single-partition device); a different dispatch mapping would train with
-  // stale L2 lines silently, so check the hardware id and raise the error word (2) -- the
-  // host refuses the pass (ops.mf.check_flow_errors)
-  if (threadIdx.x == 0 && (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf) != x)  // HW_REG_XCC_ID
-    __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the visibility argument above needs all blocks of one residue b mod 8 to RUN on one
+  // XCD, and the 8 residues on 8 different XCDs (the round-robin dispatch of a single-
+  // partition device; which physical XCD serves a residue does not matter -- measured: the
+  // logical order is not the HW_REG_XCC_ID order on MI355X). The first block of residue x
+  // records its XCC id; a block of x on another XCC, or two residues on one XCC, raise the
+  // error word (2) and the host refuses the pass (ops.mf.check_flow_errors)
+  if (threadIdx.x == 0) {
+    const int hw = (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf) + 1;  // HW_REG_XCC_ID
+    const int prev = cas_zero(xccmap + x, hw);
+    if (prev != 0 && prev != hw) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int bit = 1 << (hw - 1);
+    const int seen = __hip_atomic_fetch_or(xccmap + XCDS, prev == 0 ? bit : 0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == 0 && (seen & bit)) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (int step = 0; step < steps; ++step) {
     const int cell = x * XCDS + (x + step) % XCDS;
     const long a = off[cell];
@@ -522,7 +539,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_flow_kernel(const int* __restr
   if (threadIdx.x == 0) {
     const int prev = __hip_atomic_fetch_add(exit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (int)gridDim.x - 1) {  // every block has left: reset for the next launch
-      for (int k = 0; k < 193; ++k) __hip_atomic_store(ws + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < 202; ++k) __hip_atomic_store(ws + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -51,6 +51,7 @@ class LDAConfig:
     budget_pieces: int = 8    # launches a step's word chunks are cut into
     min_bound: int = 0        # with a budget: retune it every iteration so the trained percentage lands
     max_bound: int = 0        # in [min_bound, max_bound] (dymoro.BudgetTuner); 0 / 0: the budget stays fixed
+    deterministic: bool = False  # GPU: one wave samples in order (bit-reproducible; tests / debugging only)
 
 
 def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, seed: int = 0, device="cpu"):
@@ -197,7 +198,7 @@ class LDACollectiveMapper(CollectiveMapper):
                                      nk_view, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
                                      (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ k, self.doc_index,
                                      self.doc_index.tpos[a:b] if self.doc_index is not None else None,
-                                     self.orders[gs])
+                                     self.orders[gs], deterministic=cfg.deterministic)
                     delta_total += d
                     nk_view = self.nk + delta_total
                     n += b - a
@@ -241,7 +242,7 @@ class LDACollectiveMapper(CollectiveMapper):
             tpos = self.doc_index.tpos[t0:t1] if self.doc_index is not None else None
             d = L.cgs_sample(self.tdoc[t0:t1], self.tword[t0:t1], self.tz[t0:t1], sub, self.ndk, slab,
                              self.nk + state["delta"], cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta,
-                             (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ (k << 4) ^ state["j"], self.doc_index, tpos)
+                             (cfg.seed << 40) ^ (it << 20) ^ (s << 8) ^ (k << 4) ^ state["j"], self.doc_index, tpos, deterministic=cfg.deterministic)
             state["delta"] = state["delta"] + d
             state["j"] += 1
             return t1 - t0
@@ -530,7 +531,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
             n = self.tz.numel()
             if n:
                 d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, self.pull_buf.view(-1, self.Kp),
-                                 self.nk, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index)
+                                 self.nk, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index, deterministic=cfg.deterministic)
                 self.nk += d
             return n
         if self.ps is not None:
@@ -543,7 +544,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         n = self.tz.numel()
         if n:
             d = L.cgs_sample(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, slab, self.nk,
-                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index)
+                             cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index, deterministic=cfg.deterministic)
         else:
             d = torch.zeros(self.Kp, dtype=torch.int32, device=self.device)
         if self.ps is not None:

@@ -157,12 +157,14 @@ def count(tdoc, tword, tz, ndk=None, nwk=None, nk=None) -> None:
 
 def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta: float, vbeta: float,
                seed: int, doc_index: Optional[DocIndex] = None, tpos: Optional[torch.Tensor] = None,
-               order: Optional[torch.Tensor] = None) -> torch.Tensor:
+               order: Optional[torch.Tensor] = None, deterministic: bool = False) -> torch.Tensor:
     """One Gibbs sweep over the given (word-sorted) tokens. Returns the topic-count delta
     [K_pad] int32 of this sweep (nk itself is read, not written, on the GPU; the CPU
     sampler updates a private copy exactly). ``doc_index`` (+ ``tpos``, the tokens'
     positions in it; default all of it) selects the sparse sampler and is kept in step;
-    ``order`` is its chunk order (default :func:`chunk_order`)."""
+    ``order`` is its chunk order (default :func:`chunk_order`). ``deterministic``: on the
+    GPU, ONE wave samples every chunk in order -- bit-reproducible and independent of the
+    word-row numbering (a test mode; the CPU sampler is always sequential)."""
     dev = tz.device
     Kp = ndk.shape[1]
     if doc_index is None and use_sparse(K):
@@ -183,7 +185,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
                 tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(), chunks.numel() - 1,
                 order.data_ptr(), work.data_ptr(), tpos.data_ptr(), doc_index.doc_off.data_ptr(), doc_index.zdoc.data_ptr(), _lib.ptr(ndk),
                 ndk.stride(0) if ndk is not None else 0, _bits(ndk), nwk.data_ptr(), nwk.stride(0), inv.data_ptr(),
-                delta.data_ptr(), K, float(alpha), float(beta), seed & 0xFFFFFFFFFFFFFFFF, SPARSE_WAVES,
+                delta.data_ptr(), K, float(alpha), float(beta), seed & 0xFFFFFFFFFFFFFFFF, -1 if deterministic else SPARSE_WAVES,
                 _lib.stream_ptr(dev))
             _lib.check(st, "lda_cgs_sparse")
             return delta
@@ -191,7 +193,8 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
         st = _lib.kernels().harp_lda_cgs(tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(),
                                          chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
-                                         seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT, _lib.stream_ptr(dev))
+                                         seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0),
+                                         _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
         return delta
     rt = _lib.runtime()

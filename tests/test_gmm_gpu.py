@@ -60,8 +60,9 @@ def test_em_gmm_native_matches_torch_path(cuda):
     assert abs(float(a["loglik"]) - float(b["loglik"])) < 1e-9 * abs(float(b["loglik"]))
 
 
-def test_em_iteration_speed_1e6(cuda):
-    """N = 1e6, d = 32, K = 64: one EM iteration (E-step + statistics) >= 10x the torch path."""
+def test_em_iteration_1e6(cuda):
+    """N = 1e6, d = 32, K = 64: one EM iteration (E-step + statistics) matches the torch
+    path; the timing is printed (the >= 10x gate lives in scripts/bench_speedups.py)."""
     X, w, mu, cov = _mixture(1_000_000, 32, 64, 5)
     Xg, wg, mug, covg = (t.to(cuda) for t in (X, w, mu, cov))
 
@@ -73,6 +74,9 @@ def test_em_iteration_speed_1e6(cuda):
         Rt, _ = _torch_estep(Xg, wg, mug, covg, "full")
         return Rt.sum(0), Rt.t() @ Xg, torch.einsum("nk,ni,nj->kij", Rt, Xg, Xg)
 
+    (nk, sx, sxx), (rk, rx, rxx) = native(), ref()
+    for got, want in ((nk, rk), (sx, rx), (sxx, rxx)):
+        assert float((got - want).abs().max()) <= 1e-5 * float(want.abs().max()), (got - want).abs().max()
     out = {}
     for name, fn, reps in (("native", native, 5), ("torch", ref, 2)):
         fn()
@@ -83,5 +87,4 @@ def test_em_iteration_speed_1e6(cuda):
         torch.cuda.synchronize()
         out[name] = (time.perf_counter() - t0) / reps
     print(f"EM iteration N=1e6 d=32 K=64: native {out['native'] * 1e3:.2f} ms, torch {out['torch'] * 1e3:.1f} ms, "
-          f"{out['torch'] / out['native']:.1f}x")
-    assert out["torch"] / out["native"] >= 10, out
+          f"{out['torch'] / out['native']:.1f}x")  # ratio asserted in scripts/bench_speedups.py

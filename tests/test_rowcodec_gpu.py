@@ -60,28 +60,48 @@ def test_rowcodec_overflow_flag_gpu(cuda):
     assert int(ov.item()) == 1
 
 
-def test_lda_push_pull_sparse_rows_gpu(cuda):
-    from harp_amd.models.lda import LDAConfig, LDAPushPullMapper, synthetic_corpus
+def _lda_pp(cuda, toks, mode, local, seed, det):
+    from harp_amd.models.lda import LDAConfig, LDAPushPullMapper
     from harp_amd.parallel.comm import Communicator
     from harp_amd.runtime.mapper import KeyValReader
 
+    cfg = LDAConfig(num_topics=64, alpha=0.1, beta=0.01, iterations=12, print_interval=6, block_words=512,
+                    sparse_comm=mode, local_server=local, seed=seed, deterministic=det)
+    m = LDAPushPullMapper(Communicator(device=cuda), cfg, 3000, 4000, toks)
+    m.run(KeyValReader([]))
+    return m
+
+
+def test_lda_push_pull_sparse_rows_gpu(cuda):
+    """Dense word blocks, fixed-layout sparse rows (HIP row codec) and the local server
+    must carry the SAME model: (1) the exact invariant -- the word-topic counts rebuilt
+    from the final (word, z) equal the server table bit for bit, and the topic sums equal
+    its column sums -- under the production (racing) sampler, for every layout and seed;
+    (2) with the one-wave deterministic sampler the three layouts take bit-identical
+    trajectories (the sampler's random stream is keyed by token index, and token order /
+    chunking / initial z do not depend on the row layout). The production sampler's
+    doc-row races make same-seed runs differ by as much as different seeds (measured:
+    0.07 nats/token between two runs of one seed after 12 sweeps, profiles/r4_lda_pp), so
+    no single-run likelihood comparison is asserted."""
+    from harp_amd.models.lda import synthetic_corpus
+
     toks = synthetic_corpus(3000, 4000, 20, 50, seed=2)
-    out = {}
-    for mode, seed in (("off", 0), ("off", 1), ("on", 0)):
-        cfg = LDAConfig(num_topics=64, alpha=0.1, beta=0.01, iterations=12, print_interval=6, block_words=512,
-                        sparse_comm=mode, local_server=False, seed=seed)
-        m = LDAPushPullMapper(Communicator(device=cuda), cfg, 3000, 4000, toks)
-        m.run(KeyValReader([]))
-        owned = sum(p.get().sum(0) for p in m.glob.get_partitions())
-        assert torch.equal(owned[:64].cpu(), m.nk[:64].cpu())
-        assert int(m.nk.sum()) == toks[0].numel()
-        ll = [v for _, v in m.result["loglik"]]
-        assert ll[-1] > ll[0]
-        out[(mode, seed)] = (m.comm_mode, ll[-1])
-    assert out[("off", 0)][0] == "dense" and out[("on", 0)][0] == "sparse"
     n = toks[0].numel()
-    # the GPU sampler's random streams follow the row layout, so the two paths take different
-    # (equally valid) trajectories: the gap must be within the seed-to-seed spread
-    spread = abs(out[("off", 1)][1] - out[("off", 0)][1]) / n
-    gap = abs(out[("on", 0)][1] - out[("off", 0)][1]) / n
-    assert gap < 3 * spread + 0.01, (gap, spread, out)
+    for seed in range(2):
+        for mode, local in (("off", False), ("on", False), ("off", True)):
+            m = _lda_pp(cuda, toks, mode, local, seed, det=False)
+            assert m.comm_mode == {("off", False): "dense", ("on", False): "sparse", ("off", True): "local"}[(mode, local)]
+            assert m.check_counts(), (mode, local, seed)
+            assert int(m.nk.sum()) == n
+            ll = [v for _, v in m.result["loglik"]]
+            assert ll[-1] > ll[0]
+    ref = None
+    for mode, local in (("off", False), ("on", False), ("off", True)):
+        m = _lda_pp(cuda, toks, mode, local, 3, det=True)
+        assert m.check_counts()
+        got = (m.tz.cpu(), m.ndk.cpu(), [v for _, v in m.result["loglik"]])
+        if ref is None:
+            ref = got
+        else:
+            assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), m.comm_mode
+            assert got[2] == ref[2], (m.comm_mode, got[2], ref[2])
