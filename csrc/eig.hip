@@ -362,9 +362,13 @@ __device__ __forceinline__ void fused_pass(double* __restrict__ A, long lda, int
 // A: n x n symmetric, column-major (lda), overwritten. d[n], e[n-1]: the tridiagonal.
 // wsd (doubles, zeroed): p[3][n] (p_k, p_{k+1}, and the buffer zeroed for p_{k+2}).
 template <int KU>
+// vout / tauout (nullable): the Householder vectors (column k = v_k, v_k[k + 1] = 1 and
+// zeros above, n x n column-major, zeroed by the host) and their factors, written by
+// workgroup 0 for the eigenvector back-transform
 __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A, long lda, int n,
                                                          double* __restrict__ dout, double* __restrict__ eout, int NB,
-                                                         int* __restrict__ ws, double* __restrict__ wsd) {
+                                                         int* __restrict__ ws, double* __restrict__ wsd,
+                                                         double* __restrict__ vout, double* __restrict__ tauout) {
   extern __shared__ double smem[];
   double* sv = smem;          // v_k
   double* sw = smem + n;      // w_k
@@ -401,6 +405,10 @@ __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A,
   if (lead) {
     dout[0] = A[0];
     eout[0] = beta;
+  }
+  if (vout && b == 0) {
+    for (int i = tid; i < n - 1; i += kT) vout[1 + i] = sn[i];
+    if (tid == 0) tauout[0] = tn;
   }
   fused_pass<KU>(A, lda, 1, n - 1, b, NB, false, nullptr, nullptr, tn, sn, wsd, spart);
   if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
@@ -456,10 +464,15 @@ __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A,
     if (k + 3 < n) {
       tn = house_lds(sn, m - 1, red, &beta);
       if (lead) eout[k + 1] = beta;
+      if (vout && b == 0) {
+        double* vc = vout + (long)(k + 1) * n + (k + 2);
+        for (int i = tid; i < m - 1; i += kT) vc[i] = sn[i];
+      }
     } else {
       tn = 0.0;
       if (lead) eout[k + 1] = sn[0];
     }
+    if (vout && lead) tauout[k + 1] = tn;
     // trailing block of the next step: update by (v_k, w_k) and p_{k+1} in one pass
     fused_pass<KU>(A, lda, off + 1, m - 1, b, NB, tk != 0.0, sv + 1, sw + 1, tn, sn, pn, spart);
     if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
@@ -544,12 +557,13 @@ __global__ __launch_bounds__(256) void tridiag_multisect_kernel(const double* __
 
 // Fused look-ahead reduction (sytrd_fused_kernel) + multisection; wsd: zeroed 3 n doubles.
 template <int KU>
-static int launch_fused(double* A, long lda, int n, double* d, double* e, int NB, int* ws, double* wsd, hipStream_t s) {
+static int launch_fused(double* A, long lda, int n, double* d, double* e, int NB, int* ws, double* wsd, hipStream_t s,
+                        double* V = nullptr, double* tau = nullptr) {
   const size_t lds1 = sizeof(double) * 3 * (size_t)n;
   if (lds1 > 32 * 1024 && hipFuncSetAttribute((const void*)sytrd_fused_kernel<KU>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess)
     return HARP_ELAUNCH;
-  sytrd_fused_kernel<KU><<<dim3((unsigned)(NB * 8)), dim3(kT), lds1, s>>>(A, lda, n, d, e, NB, ws, wsd);
+  sytrd_fused_kernel<KU><<<dim3((unsigned)(NB * 8)), dim3(kT), lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, V, tau);
   return harp_launch_status();
 }
 
@@ -567,6 +581,15 @@ HARP_EXPORT int harp_eig_sym_fused(double* A, long lda, int n, double* d, double
     return HARP_ELAUNCH;
   tridiag_multisect_kernel<<<dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), lds2, s>>>(d, e, n, w);
   return harp_launch_status();
+}
+
+// Tridiagonalisation only, keeping the reflectors: A = Q T Q^T with Q = H_0 H_1 ... H_{n-3},
+// H_k = I - tau_k v_k v_k^T, v_k = V[:, k] (n x n column-major, zeroed by the caller; tau:
+// n doubles). d, e: the tridiagonal. Same cooperative contract as harp_eig_sym_fused.
+HARP_EXPORT int harp_sytrd_fused(double* A, long lda, int n, double* d, double* e, double* V, double* tau, int nb_max,
+                                 int* ws, double* wsd, hipStream_t s) {
+  if (n < 1 || n > kMaxN || lda < n || nb_max < 1 || nb_max > kMaxNB || !ws || !wsd || !V || !tau) return HARP_EBADARG;
+  return launch_fused<8>(A, lda, n, d, e, nb_max, ws, wsd, s, V, tau);
 }
 
 HARP_EXPORT int harp_eig_ws_ints() { return kWsInts; }

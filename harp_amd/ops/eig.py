@@ -1,5 +1,12 @@
-"""Symmetric eigenvalues on one XCD (``csrc/eig.hip``): cooperative Householder
-tridiagonalisation + multisection, for the PCA pass's d x d fp64 correlation matrix.
+"""Symmetric eigen-decomposition of the PCA pass's d x d fp64 correlation matrix.
+
+* :func:`eigvalsh`: cooperative Householder tridiagonalisation on one XCD + multisection
+  (``csrc/eig.hip``);
+* :func:`eigh`: eigenvalues AND eigenvectors -- the same reduction keeping its reflectors,
+  divide and conquer on the tridiagonal (``csrc/tridiag_dc.hip``: Cuppen merges with
+  Gu-Eisenstat vectors, host reference ``ops/tridiag_dc.py``), and the back-transform
+  X = Q Z = Z - V T (V^T Z) with the compact-WY triangle T^-1 = diag(1/tau) + striu(V^T V)
+  as rocBLAS GEMMs and one triangular solve.
 
 Reference: the DAAL PCA correlation step 3 (eigen-decomposition on the master),
 ml/daal/src/main/java/edu/iu/daal_pca/cordensedistr/PCADaalCollectiveMapper.java:121-147.
@@ -20,6 +27,14 @@ _lib.register({
     # A, lda, n, d, e, w, nb_max, ws, wsd, stamps, stream
     "harp_eig_sym": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
                      _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    # A, lda, n, d, e, V, tau, nb_max, ws, wsd, stream
+    "harp_sytrd_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                         _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    "harp_dc_max_n": [],
+    "harp_dc_ws_doubles": [_lib.c_int],
+    # dmod, e, n, Q, merges, level_off, level_smax, nlevels, ws, stream
+    "harp_dc_tridiag": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                        _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
     # A, lda, n, d, e, w, nb_max, ws, wsd, stream
     "harp_eig_sym_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                            _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
@@ -68,3 +83,110 @@ def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None) -> torch.Tenso
                       "using torch.linalg.eigvalsh")
         return torch.linalg.eigvalsh(C)
     return w
+
+
+# ------------------------------------------------------------------ eigenvectors
+_TREES: dict = {}
+
+
+def _tree(n: int, device: torch.device):
+    """Cached D&C tree of size n: (merges int32 device [3 m], level offsets, level max
+    block sizes (ctypes int arrays), split points int64 device)."""
+    key = (n, str(device))
+    t = _TREES.get(key)
+    if t is None:
+        import ctypes
+
+        from .tridiag_dc import tree_levels
+
+        levels = tree_levels(n)
+        flat, off, smax = [], [0], []
+        for lev in levels:
+            lev = sorted(lev)
+            for m in lev:
+                flat += list(m)
+            off.append(off[-1] + len(lev))
+            smax.append(max(hi - lo for lo, _, hi in lev))
+        merges = torch.tensor(flat if flat else [0, 0, 0], dtype=torch.int32, device=device)
+        mids = torch.tensor([m[1] for lev in levels for m in lev], dtype=torch.int64, device=device)
+        t = (merges, (ctypes.c_int * len(off))(*off), (ctypes.c_int * max(1, len(smax)))(*smax), len(levels), mids)
+        _TREES[key] = t
+    return t
+
+
+def eigh_tridiag(d: torch.Tensor, e: torch.Tensor):
+    """Eigenvalues (ascending) and eigenvectors of the symmetric tridiagonal (d, e) (fp64
+    on a GPU: the D&C kernels; otherwise the host reference)."""
+    n = d.numel()
+    if not (d.device.type == "cuda" and d.dtype == torch.float64 and _lib.use_native(d)
+            and 0 < n <= int(_lib.kernels().harp_dc_max_n())):
+        from .tridiag_dc import eigh_tridiag as ref
+
+        w, V = ref(d.detach().cpu().numpy(), e.detach().cpu().numpy())
+        return torch.from_numpy(w).to(d), torch.from_numpy(V).to(d)
+    dev = d.device
+    k = _lib.kernels()
+    merges, off, smax, nlev, mids = _tree(n, dev)
+    dmod = d.clone().contiguous()
+    ec = e.contiguous() if e.numel() else torch.zeros(1, dtype=torch.float64, device=dev)
+    if mids.numel():
+        b = e[mids - 1].abs()
+        dmod.index_add_(0, mids - 1, -b)
+        dmod.index_add_(0, mids, -b)
+    Qt = torch.eye(n, dtype=torch.float64, device=dev)  # column-major Q == row-major Q^T
+    ws = torch.zeros(int(k.harp_dc_ws_doubles(n)), dtype=torch.float64, device=dev)
+    st = k.harp_dc_tridiag(dmod.data_ptr(), ec.data_ptr(), n, Qt.data_ptr(), merges.data_ptr(), off, smax, nlev,
+                           ws.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(st, "dc_tridiag")
+    order = torch.argsort(dmod)
+    return dmod[order], Qt[order].t()
+
+
+def eigh(C: torch.Tensor):
+    """Eigenvalues (ascending) and eigenvectors (columns) of the symmetric matrix ``C``
+    (fp64 on a GPU: one-XCD reduction + D&C + WY back-transform; otherwise, or if the
+    cooperative launch could not claim its workgroups, torch.linalg.eigh)."""
+    if not usable(C):
+        return torch.linalg.eigh(C)
+    n = C.shape[0]
+    dev = C.device
+    k = _lib.kernels()
+    nb = int(k.harp_eig_workgroups(n, int(os.environ.get("HARP_EIG_NB", NB_DEFAULT))))
+    if nb < 1:
+        return torch.linalg.eigh(C)
+    A = C.contiguous().clone()
+    ws = torch.zeros(int(k.harp_eig_ws_ints()), dtype=torch.int32, device=dev)
+    wsd = torch.zeros(3 * n + 4, dtype=torch.float64, device=dev)
+    d = torch.empty(n, dtype=torch.float64, device=dev)
+    e = torch.zeros(max(n, 1), dtype=torch.float64, device=dev)
+    Vt = torch.zeros((n, n), dtype=torch.float64, device=dev)  # column-major reflectors
+    tau = torch.zeros(n, dtype=torch.float64, device=dev)
+    st = k.harp_sytrd_fused(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), Vt.data_ptr(), tau.data_ptr(), nb,
+                            ws.data_ptr(), wsd.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(st, "sytrd_fused")
+    claims, _, err = ws[:3].tolist()
+    if claims < nb or err:
+        warnings.warn(f"one-XCD reduction did not run cooperatively (claims {claims}/{nb}, error {err}); "
+                      "using torch.linalg.eigh")
+        return torch.linalg.eigh(C)
+    lam, Z = eigh_tridiag(d, e[:max(n - 1, 0)])
+    return lam, back_transform(Vt, tau, Z)
+
+
+def back_transform(Vt: torch.Tensor, tau: torch.Tensor, Z: torch.Tensor) -> torch.Tensor:
+    """X = H_0 H_1 ... H_{n-3} Z for the reflectors of :func:`eigh` (``Vt`` row c = v_c):
+    compact WY, Q = I - V T V^T with T^-1 = diag(1/tau) + striu(V^T V), as two GEMMs and
+    one triangular solve (rocBLAS; a reflector with tau = 0 is the identity)."""
+    n = Z.shape[0]
+    m = n - 2
+    if m <= 0:
+        return Z
+    V = Vt[:m].t()  # n x m
+    t = tau[:m]
+    live = t != 0
+    if not bool(live.all()):
+        V = V * live.to(V.dtype)
+    Tinv = torch.triu(V.t() @ V, 1)
+    Tinv.diagonal().copy_(torch.where(live, 1.0 / torch.where(live, t, torch.ones_like(t)), torch.ones_like(t)))
+    Y = torch.linalg.solve_triangular(Tinv, V.t() @ Z, upper=True)
+    return Z - V @ Y

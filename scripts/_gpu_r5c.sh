@@ -1,9 +1,10 @@
 #!/bin/bash
-# LDA push-pull single-worker local server: LDA GPU tests + bench (local server on / off)
-set -o pipefail
-export TMPDIR=/tmp
+# eigenvectors: D&C kernels + eigh tests, timing, kernel stats
 mkdir -p gpurun_out/r5c
-timeout -k 10 300 python -u -m pytest tests/test_lda_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r5c/tests.log 2>&1 || { tail -30 gpurun_out/r5c/tests.log; exit 1; }
-tail -1 gpurun_out/r5c/tests.log
-timeout -k 10 300 python bench.py --points 1e6 --steps 2 --warmup 1 --sgd off --extras on --pca-n 4.8e5 > gpurun_out/r5c/bench.log 2>&1 || { tail -20 gpurun_out/r5c/bench.log; exit 1; }
-grep '^{' gpurun_out/r5c/bench.log | tail -1 | python -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['lda'])"
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_eig_gpu.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r5c/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 120 python -u scripts/prof_eigh.py > gpurun_out/r5c/time.log 2>&1 || exit $?
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/r5c/prof -o run -- python3 scripts/prof_eigh.py > gpurun_out/r5c/prof.log 2>&1
+echo "prof rc=$?"
