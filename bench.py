@@ -273,12 +273,15 @@ def bench_sgd(args, comm, torch):
 # ----------------------------------------------------------------------------- PCA (config 4)
 def bench_pca(args, comm, torch):
     """One PCA / correlation pass per step over N x d synthetic U[0,1) samples split over
-    the ranks: MFMA SYRK partial result (G = [X 1]^T [X 1], upper tiles), one allreduce,
-    fp64 correlation, eigenvalues on the master then broadcast
-    (PCADaalCollectiveMapper.java:121-147: step 2 runs on the master only). CPU ranks
-    (gloo rehearsal) form the same G with an fp32 matmul."""
-    from harp_amd.models.common import reduce_partials
-    from harp_amd.ops.eig import eigvalsh
+    the ranks, through the library API ``stats.pca`` (PCADaalCollectiveMapper.java:121-154):
+    step 1 is the MFMA SYRK partial result of the bf16 feature-major block with a row of
+    ones (n, column sums and X^T X from ONE pass over one operand), one fp64 allreduce, the
+    fp64 correlation, step 2 -- eigenvalues AND eigenvectors of the d x d correlation on the
+    master (one-XCD reduction + divide and conquer + WY back-transform, ``ops.eig.eigh``) --
+    and the broadcast of the d + 1 x d result. CPU ranks (gloo rehearsal) run the same API on
+    row-major blocks (dtype bf16: the same rounding, fp32 accumulation)."""
+    from harp_amd.models import stats as ST
+    from harp_amd.ops import eig as EIG
 
     P, r = comm.world_size, comm.rank
     N, d = int(args.pca_n), args.pca_d
@@ -287,35 +290,23 @@ def bench_pca(args, comm, torch):
     if dev.type == "cuda":
         from harp_amd.ops import linalg as LA
 
-        fm = LA.FeatureMajor.uniform(n, d, 0.0, 1.0, seed=11 + r, device=dev)
-        syrk, upper = (lambda: LA.syrk_t(fm)), LA.symmetrize_upper
+        data = LA.FeatureMajor.uniform(n, d, 0.0, 1.0, seed=11 + r, device=dev)
+        syrk = lambda: LA.syrk_t(data)  # noqa: E731
     else:
         g = torch.Generator().manual_seed(11 + r)
-        Xa = torch.cat([torch.rand((n, d), generator=g), torch.ones((n, 1))], 1)
-        syrk, upper = (lambda: Xa.t() @ Xa), (lambda G: G)
+        data = torch.rand((n, d), generator=g)
+        syrk = lambda: data.t() @ data  # noqa: E731
 
     def one_pass():
-        G = syrk()
-        Gs = upper(reduce_partials(comm, {"g": G}, dtype=torch.float32)["g"])[:d + 1, :d + 1].double()
-        cnt = Gs[d, d]
-        mean = Gs[:d, d] / cnt
-        cov = (Gs[:d, :d] - cnt * torch.outer(mean, mean)) / (cnt - 1)
-        sd = torch.diagonal(cov).sqrt()
-        if r == 0:
-            ev = eigvalsh(cov / torch.outer(sd, sd))  # one-XCD tridiagonalisation (csrc/eig.hip) on GPUs
-        else:
-            ev = torch.empty(d, dtype=torch.float64, device=dev)
-        if P > 1:
-            comm.broadcast(ev, 0)
-        return ev, G.numel() * 4
+        return ST.pca(data, comm, dtype="bf16")
 
-    one_pass()
+    res = one_pass()
     sync(comm, torch)
     clock = StepClock(comm, torch)
     t0 = time.perf_counter()
     clock.mark()
     for _ in range(args.pca_steps):
-        ev, gbytes = one_pass()
+        res = one_pass()
         clock.mark()
     sync(comm, torch)
     dt = reduce_max(comm, torch, time.perf_counter() - t0) / args.pca_steps
@@ -326,17 +317,41 @@ def bench_pca(args, comm, torch):
     sclock.mark()
     sync(comm, torch)
     syrk_s = sclock.durations()[0]
+    # step 2 alone on the master: eigenvalues + eigenvectors of the correlation matrix
+    corr = ST.correlation(data, comm, dtype="bf16")["correlation"]
+    eig_s = None
+    orth = res_rel = None
+    if r == 0:
+        lam, V = EIG.eigh(corr)
+        reps = 3
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(reps):
+            lam, V = EIG.eigh(corr)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        eig_s = (time.perf_counter() - te) / reps
+        eye = torch.eye(d, dtype=torch.float64, device=V.device)
+        orth = float((V.t() @ V - eye).abs().max())
+        res_rel = float((corr @ V - V * lam).abs().max()) / float(lam.abs().max())
+    if P > 1:
+        comm.barrier()
     # useful SYRK work: the upper triangle (diagonal included) of the (d+1)^2 Gram of [X 1]
     # over this rank's rows -- what the kernel must compute, not the full-Gram equivalent
     flop = float(n) * (d + 1) * (d + 2)
-    sync_bytes = (gbytes + d * 8) if P > 1 else 0
-    return {"metric": "PCA correlation pass s/pass (N x d, MFMA SYRK + allreduce + fp64 eig)",
+    sync_bytes = ((d * d + d + 1) * 8 + (d + 1) * d * 8) if P > 1 else 0
+    ev = res["eigenvalues"]
+    return {"metric": "PCA correlation pass s/pass (N x d, stats.pca: MFMA SYRK + allreduce + fp64 eigenvalues "
+                      "and eigenvectors)",
             "s_per_pass": round(dt, 6), "median_s_per_pass": round(st["median"], 6), "pass_s": st,
-            "syrk_s": round(syrk_s, 6), "N": N, "d": d, "steps": args.pca_steps, "n_gpus": P,
+            "syrk_s": round(syrk_s, 6), "eig_s": round(eig_s, 6) if eig_s is not None else None,
+            "eig": "eigenvalues + eigenvectors (ops.eig.eigh)", "eigvec_orth_err": orth, "eig_residual": res_rel,
+            "N": N, "d": d, "steps": args.pca_steps, "n_gpus": P,
             "syrk_tflops": round(flop / syrk_s / 1e12, 1) if syrk_s > 0 else None,
             "syrk_flop_per_rank": flop, "sync_bytes_per_iter": int(sync_bytes),
             "max_eigenvalue": round(float(ev.max()), 6),
-            "dtype": "bf16 in / fp32 acc / fp64 finalize" if dev.type == "cuda" else "fp32 (CPU rehearsal)",
+            "dtype": "bf16 in / fp32 acc / fp64 finalize" if dev.type == "cuda" else "bf16-rounded fp32 (CPU rehearsal)",
             "data": "synthetic U[0,1) generated on device", "scaling": "strong"}
 
 

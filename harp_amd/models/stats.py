@@ -32,11 +32,84 @@ def _local(comm: Optional[Communicator]) -> Communicator:
 
 
 # ------------------------------------------------------------------ covariance / moments
-def covariance_partial(X: torch.Tensor) -> Dict[str, torch.Tensor]:
-    """Step 1: n, sum x, X^T X (cross-product) of the local block."""
-    n = X.shape[0]
-    s = LA.colsum(X)
-    return {"n": torch.tensor([float(n)], device=s.device), "sum": s, "xtx": LA.gram(X)}
+# Precision policy of the partial-result family (DAAL computes these in fp64:
+# COVDaalCollectiveMapper.java:146-175, PCADaalCollectiveMapper.java:121 Double.class):
+#  * "bf16": the MFMA SYRK fast path -- operands rounded to bf16 ONCE (ops.linalg.FeatureMajor),
+#    fp32 accumulation; n, the column sums and X^T X all come from that one rounded operand
+#    (a row of ones in the Gram), so the finalize never mixes operands. The bf16 rounding
+#    (2^-9 relative per element) bounds the result: tests/test_partial_results.py pins it
+#    (<= 3e-3 relative covariance error on U[0,1) data);
+#  * "fp32": fp32 operands, rocBLAS fp32 GEMMs over row slices of ops.linalg.ATB_CHUNK
+#    rows on data shifted by a per-rank reference row (no cancellation in the centred
+#    sums), slices summed in fp64: <= 1e-6 relative to an fp64 covariance;
+#  * "fp64": fp64 operands and GEMMs (the reference's precision).
+# dtype=None picks by the input: bf16 / FeatureMajor -> "bf16", fp32 -> "fp32", fp64 or
+# CPU -> "fp64" (an fp32 input is never silently rounded to bf16).
+DTYPES = ("bf16", "fp32", "fp64")
+
+
+def _policy(X, dtype: Optional[str]) -> str:
+    if dtype is not None:
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype={dtype!r}: expected one of {DTYPES}")
+        return dtype
+    if isinstance(X, LA.FeatureMajor) or X.dtype == torch.bfloat16:
+        return "bf16"
+    if X.device.type == "cpu" or X.dtype == torch.float64 or LA._is_sparse(X):
+        return "fp64"
+    return "fp32"
+
+
+def _shifted_sums(X: torch.Tensor, acc: torch.dtype):
+    """(n, sum x, X^T X) in fp64 from GEMMs in ``acc`` over row slices of X - c, c = X's
+    first row (the centred sums carry no cancellation; the shift is undone in fp64)."""
+    n, d = X.shape
+    if n == 0:
+        z = torch.zeros(d, dtype=torch.float64, device=X.device)
+        return 0.0, z, torch.zeros((d, d), dtype=torch.float64, device=X.device)
+    c = X[0].to(acc)
+    S = torch.zeros((d, d), dtype=torch.float64, device=X.device)
+    s = torch.zeros(d, dtype=torch.float64, device=X.device)
+    step = LA.ATB_CHUNK * 64
+    for a in range(0, n, step):
+        Y = X[a:a + step].to(acc) - c
+        S += LA.atb(Y, Y).double() if acc != torch.float64 else LA.atb(Y, Y)
+        s += Y.double().sum(0) if acc != torch.float64 else Y.sum(0)
+    c64 = c.double()
+    xtx = S + torch.outer(c64, s) + torch.outer(s, c64) + n * torch.outer(c64, c64)
+    return float(n), s + n * c64, xtx
+
+
+def covariance_partial(X, dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
+    """Step 1: n, sum x, X^T X (cross-product) of the local block, at the ``dtype``
+    precision (module notes above). ``X``: a row-major tensor (dense or sparse) or an
+    :class:`ops.linalg.FeatureMajor` block."""
+    mode = _policy(X, dtype)
+    if isinstance(X, LA.FeatureMajor):
+        if mode != "bf16":
+            raise ValueError("a FeatureMajor block holds bf16 operands: use dtype='bf16'")
+        n, s, G = LA.gram_stats(X)
+        return {"n": n.reshape(1).double(), "sum": s.double(), "xtx": G.double()}
+    if LA._is_sparse(X):
+        n = X.shape[0]
+        s = LA.colsum(X)
+        return {"n": torch.tensor([float(n)], dtype=torch.float64, device=s.device), "sum": s.double(),
+                "xtx": LA.gram(X).double()}
+    if mode == "bf16":
+        if X.device.type == "cuda" and LA._has_syrk() and _native(X):
+            return covariance_partial(LA.FeatureMajor.from_rows(X), "bf16")
+        Xb = X.to(torch.bfloat16).float()  # the same rounding, fp32 accumulation (CPU)
+        n = float(X.shape[0])
+        return {"n": torch.tensor([n], dtype=torch.float64, device=X.device), "sum": Xb.sum(0).double(),
+                "xtx": (Xb.t() @ Xb).double()}
+    n, s, xtx = _shifted_sums(X, torch.float32 if mode == "fp32" else torch.float64)
+    return {"n": torch.tensor([n], dtype=torch.float64, device=X.device), "sum": s, "xtx": xtx}
+
+
+def _native(X) -> bool:
+    from ..ops import _lib
+
+    return _lib.use_native(X)
 
 
 def covariance_finalize(p: Dict[str, torch.Tensor], bias: bool = False) -> Dict[str, torch.Tensor]:
@@ -46,62 +119,104 @@ def covariance_finalize(p: Dict[str, torch.Tensor], bias: bool = False) -> Dict[
     return {"mean": mean, "covariance": cov}
 
 
-def covariance(X: torch.Tensor, comm: Optional[Communicator] = None, bias: bool = False) -> Dict[str, torch.Tensor]:
-    return covariance_finalize(reduce_partials(_local(comm), covariance_partial(X)), bias)
+def covariance(X, comm: Optional[Communicator] = None, bias: bool = False,
+               dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
+    return covariance_finalize(reduce_partials(_local(comm), covariance_partial(X, dtype), dtype=torch.float64), bias)
 
 
-def correlation(X: torch.Tensor, comm: Optional[Communicator] = None) -> Dict[str, torch.Tensor]:
-    r = covariance(X, comm)
+def correlation(X, comm: Optional[Communicator] = None, dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
+    r = covariance(X, comm, dtype=dtype)
     sd = r["covariance"].diagonal().clamp_min(0).sqrt()
     r["correlation"] = r["covariance"] / torch.outer(sd, sd).clamp_min(1e-300)
     return r
 
 
-def low_order_moments(X: torch.Tensor, comm: Optional[Communicator] = None) -> Dict[str, torch.Tensor]:
+def low_order_moments(X: torch.Tensor, comm: Optional[Communicator] = None,
+                      dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
     """DAAL low_order_moments: minimum, maximum, sum, sumSquares, sumSquaresCentered, mean,
-    secondOrderRawMoment, variance, standardDeviation, variation."""
+    secondOrderRawMoment, variance, standardDeviation, variation. ``dtype`` as for
+    :func:`covariance`: "bf16" sums the bf16-rounded operands in fp32, "fp32" / "fp64" sum
+    shifted row slices and accumulate in fp64 (sumSquaresCentered then has no cancellation)."""
     comm = _local(comm)
     Xd = X.to_dense() if X.is_sparse or X.layout == torch.sparse_csr else X
-    Xf = Xd.double() if Xd.device.type == "cpu" else Xd.float()
-    sums = reduce_partials(comm, {"n": torch.tensor([float(Xd.shape[0])], device=Xd.device),
-                                  "sum": Xf.sum(0), "sumsq": (Xf * Xf).sum(0)})
-    mm = reduce_partials(comm, {"min": Xf.min(0).values, "negmax": -Xf.max(0).values}, Operation.MIN)
-    n = sums["n"].item()
-    mean = sums["sum"] / n
-    ssc = sums["sumsq"] - n * mean * mean
-    var = ssc / max(n - 1, 1)
+    mode = _policy(Xd, dtype)
+    n = float(Xd.shape[0])
+    if mode == "bf16":
+        Xf = Xd.to(torch.bfloat16).float()
+        s1, s2 = Xf.sum(0).double(), (Xf * Xf).sum(0).double()
+        c = torch.zeros_like(s1)
+        sc1, sc2 = s1, s2
+    else:
+        acc = torch.float32 if mode == "fp32" else torch.float64
+        c = Xd[0].to(acc).double() if Xd.shape[0] else torch.zeros(Xd.shape[1], dtype=torch.float64, device=Xd.device)
+        sc1 = torch.zeros(Xd.shape[1], dtype=torch.float64, device=Xd.device)
+        sc2 = torch.zeros_like(sc1)
+        step = 1 << 16
+        for a in range(0, Xd.shape[0], step):
+            Y = Xd[a:a + step].to(acc) - c.to(acc)
+            sc1 += Y.sum(0).double()
+            sc2 += (Y * Y).sum(0).double()
+        s1 = sc1 + n * c
+        s2 = sc2 + 2 * c * sc1 + n * c * c
+    # shifted sums combine across ranks through the raw sums; the centred sum of squares is
+    # formed from per-rank centred pieces (Chan et al.) so no rank's shift cancels
+    sums = reduce_partials(comm, {"n": torch.tensor([n], dtype=torch.float64, device=Xd.device), "sum": s1,
+                                  "sumsq": s2}, dtype=torch.float64)
+    N = sums["n"].item()
+    mean = sums["sum"] / N
+    local_mean = s1 / max(n, 1.0)
+    # this rank's centred SS around its own mean, then the between-rank term
+    ss_local = sc2 - (sc1 * sc1) / max(n, 1.0) if mode != "bf16" else s2 - s1 * s1 / max(n, 1.0)
+    ss = reduce_partials(comm, {"ss": ss_local + n * (local_mean - mean) ** 2}, dtype=torch.float64)["ss"]
+    Xm = Xd.double() if Xd.device.type == "cpu" else Xd.float()
+    mm = reduce_partials(comm, {"min": Xm.min(0).values.double(), "negmax": -Xm.max(0).values.double()},
+                         Operation.MIN, dtype=torch.float64)
+    var = ss / max(N - 1, 1)
     sd = var.clamp_min(0).sqrt()
     return {"minimum": mm["min"], "maximum": -mm["negmax"], "sum": sums["sum"], "sumSquares": sums["sumsq"],
-            "sumSquaresCentered": ssc, "mean": mean, "secondOrderRawMoment": sums["sumsq"] / n, "variance": var,
+            "sumSquaresCentered": ss, "mean": mean, "secondOrderRawMoment": sums["sumsq"] / N, "variance": var,
             "standardDeviation": sd, "variation": sd / mean}
 
 
 # ------------------------------------------------------------------ PCA
-def pca(X: torch.Tensor, comm: Optional[Communicator] = None, method: str = "correlation",
-        n_components: Optional[int] = None) -> Dict[str, torch.Tensor]:
+def pca_step2(corr: torch.Tensor, comm: Optional[Communicator] = None):
+    """Step 2 of the correlation method on the master (PCADaalCollectiveMapper.java:136-154):
+    eigenvalues AND eigenvectors of the d x d fp64 correlation matrix -- on a GPU the one-XCD
+    reduction + divide and conquer of ``ops.eig.eigh`` -- then broadcast. Returns
+    (eigenvalues ascending, eigenvectors as columns)."""
+    from ..ops import eig as EIG
+
+    comm = _local(comm)
+    d = corr.shape[0]
+    dev = corr.device
+    if comm.rank == 0:
+        evals, evecs = EIG.eigh(corr.double().contiguous())
+        packed = torch.cat([evals.reshape(1, d), evecs]).contiguous()
+    else:
+        packed = None
+    packed = broadcast_tensor(comm, packed, (d + 1, d), torch.float64).to(dev)
+    return packed[0], packed[1:]
+
+
+def pca(X, comm: Optional[Communicator] = None, method: str = "correlation",
+        n_components: Optional[int] = None, dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
     """PCA of the (standardized) data: eigenvalues descending + eigenvectors (rows).
 
-    ``correlation``: eigen-decomposition of the distributed correlation matrix.
+    ``correlation``: eigen-decomposition of the distributed correlation matrix (``X`` may
+    be a :class:`ops.linalg.FeatureMajor` block: the one-pass MFMA SYRK path).
     ``svd``: z-score the data with global moments, distributed TSQR, SVD of R
-    (the DAAL svdDense method); both yield the correlation-PCA spectrum."""
+    (the DAAL svdDense method); both yield the correlation-PCA spectrum. ``dtype``: the
+    step-1 precision (see :func:`covariance`)."""
     comm = _local(comm)
     if method == "correlation":
-        r = correlation(X, comm)
-        # step 2 on the master only (PCADaalCollectiveMapper.java:121-147), then broadcast:
-        # the d x d fp64 eigensolve is not repeated on every worker
-        d = r["correlation"].shape[0]
-        dev = r["correlation"].device
-        if comm.rank == 0:
-            evals, evecs = torch.linalg.eigh(r["correlation"])
-            packed = torch.cat([evals.reshape(1, d), evecs]).contiguous()
-        else:
-            packed = None
-        packed = broadcast_tensor(comm, packed, (d + 1, d), torch.float64).to(dev)
-        evals, evecs = packed[0], packed[1:]
+        r = correlation(X, comm, dtype=dtype)
+        evals, evecs = pca_step2(r["correlation"], comm)
         order = torch.argsort(evals, descending=True)
         evals, evecs = evals[order], evecs[:, order].t()
     elif method == "svd":
-        mom = low_order_moments(X, comm)
+        if isinstance(X, LA.FeatureMajor):
+            raise ValueError("method='svd' needs the row-major data")
+        mom = low_order_moments(X, comm, dtype=dtype)
         Z = (X.double() - mom["mean"].to(X.device)) / mom["standardDeviation"].to(X.device).clamp_min(1e-300)
         qr = tsqr(Z, comm, want_q=False)
         ntot = reduce_partials(comm, {"n": torch.tensor([float(X.shape[0])], device=X.device)})["n"].item()

@@ -170,6 +170,8 @@ def _check_full_record(rec, P, slices=1):
         assert len(set(s["rotation_strides"])) == slices
     p = rec["pca"]
     assert p["pass_s"]["n"] == 10 and p["max_eigenvalue"] > 0.9
+    # step 2 includes eigenvectors (the reference's PCA result) through the library path
+    assert p["eig_s"] is not None and p["eigvec_orth_err"] <= 1e-10 and p["eig_residual"] <= 1e-10
     lda = rec["lda"]
     assert lda["iter_s"]["n"] == 10 and lda["tokens_per_sec"] > 0 and lda["local_server"] is False
 

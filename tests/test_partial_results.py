@@ -207,3 +207,70 @@ def test_cholesky_qr2_refuses_kahan_with_small_diagonal_spread():
     out = ST.tsqr(X, method="householder")
     eye = torch.eye(n, dtype=torch.float64)
     assert (out["Q"].t() @ out["Q"] - eye).abs().max() < 1e-12
+
+
+def _np_cov(X):
+    import numpy as np
+
+    return np.cov(X.astype(np.float64), rowvar=False)
+
+
+def test_precision_policy_covariance_cpu():
+    """dtype='fp32' / 'fp64' / 'bf16' on an fp32 block (CPU): fp32 within 1e-6 (normwise,
+    relative) of the fp64 covariance, fp64 within 1e-12, bf16 within its documented 3e-3;
+    an fp32 input defaults to the fp32 mode, never to bf16."""
+    import numpy as np
+
+    from harp_amd.models import stats as ST
+
+    g = torch.Generator().manual_seed(4)
+    X = torch.rand(200_000, 40, generator=g, dtype=torch.float32) + 10.0  # a large mean: cancellation
+    ref = _np_cov(X.numpy())
+    nrm = np.abs(ref).max()
+    errs = {}
+    for mode in ("fp32", "fp64", "bf16", None):
+        cov = ST.covariance(X, dtype=mode)["covariance"].numpy()
+        errs[mode] = np.abs(cov - ref).max() / nrm
+    assert errs["fp64"] <= 1e-12 and errs["fp32"] <= 1e-6, errs
+    assert ST._policy(X.cuda() if torch.cuda.is_available() else X, None) in ("fp32", "fp64")
+    # bf16 of data offset by +10 keeps 3 significant digits of the U[0,1) part: not bounded;
+    # on U[0,1) data the module's documented bound holds
+    Xu = X - 10.0  # U[0,1): the bf16 bound the module notes state
+    e16 = np.abs(ST.covariance(Xu, dtype="bf16")["covariance"].numpy() - _np_cov(Xu.numpy())).max() / nrm
+    assert e16 <= 3e-3, e16
+
+
+def test_precision_policy_moments_cpu():
+    import numpy as np
+
+    from harp_amd.models import stats as ST
+
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand(100_000, 16, generator=g, dtype=torch.float32) * 3 + 100.0
+    Xn = X.numpy().astype(np.float64)
+    for mode, tol in (("fp32", 1e-6), ("fp64", 1e-12)):
+        m = ST.low_order_moments(X, dtype=mode)
+        assert np.abs(m["variance"].numpy() - Xn.var(0, ddof=1)).max() <= tol * Xn.var(0).max(), mode
+        assert np.abs(m["mean"].numpy() - Xn.mean(0)).max() <= tol * 100
+
+
+def _prec_worker(comm):
+    from harp_amd.models import stats as ST
+
+    g = torch.Generator().manual_seed(100 + comm.rank)
+    X = torch.rand(30_000 + 1000 * comm.rank, 12, generator=g, dtype=torch.float32) + 5.0
+    return {"cov": ST.covariance(X, comm, dtype="fp32")["covariance"],
+            "var": ST.low_order_moments(X, comm, dtype="fp32")["variance"], "X": X}
+
+
+def test_precision_policy_distributed_gloo():
+    import numpy as np
+
+    from harp_amd.runtime.launcher import launch
+
+    outs = launch(_prec_worker, 2, timeout=300)
+    Xall = torch.cat([o["X"] for o in outs]).numpy().astype(np.float64)
+    ref = np.cov(Xall, rowvar=False)
+    for o in outs:
+        assert np.abs(o["cov"].numpy() - ref).max() <= 1e-6 * np.abs(ref).max()
+        assert np.abs(o["var"].numpy() - Xall.var(0, ddof=1)).max() <= 1e-6 * Xall.var(0).max()
