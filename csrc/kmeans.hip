@@ -30,6 +30,8 @@
 //    per wave-instruction (the full-rate atomic shape on gfx950).
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr float KM_BIG = 1.0e38f;
@@ -345,6 +347,194 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Wide rows (dp > 256, any d up to the operand's padding): X fragments no longer fit the
+// register file for a whole centroid sweep, so the reduction over features is staged:
+//  * a workgroup (4 waves, 64 points per wave = 2 MFMA point groups) owns 256 points and ONE
+//    block of 256 centroids (8 row groups of 32); its 16 accumulators (256 fp32 per lane)
+//    stay live across the feature stages;
+//  * feature stage f covers dp columns [64 f, 64 f + 64): the centroid block's 256 x 64 bf16
+//    slice streams through double-buffered LDS by LDS-DMA (the swizzled image of the
+//    narrow kernel), the points' 64-column slices are register double-buffered straight
+//    from global (next stage's loads in flight under this stage's 64 MFMAs per wave);
+//  * the epilogue is the narrow kernel's keyed argmin over the block's 256 candidates, the
+//    workgroup's result (squared distance, index) is merged across centroid blocks with ONE
+//    64-bit atomic min per point (distance bits above the index: non-negative floats order
+//    as integers, ties go to the lower index);
+//  * grid: consecutive ids of one XCD (id mod 8) take the centroid blocks of one point block
+//    one after another, so that block's rows come from HBM once and from L2 after.
+constexpr int KW_PTS = 256, KW_CB = 256, KW_DC = 64, KW_RG = KW_CB / 32, KW_KS = KW_DC / 16;
+constexpr int KW_CPR = KW_DC / 8;                       // 16-B chunks per centroid row per stage
+constexpr int KW_TILE_BYTES = KW_CB * KW_DC * 2;        // 32 KiB
+constexpr int KW_DMA = KW_CB * KW_CPR / 64;             // 1-KiB DMA pieces per stage (32)
+
+__device__ __forceinline__ void stage_dma_wide(const __bf16* __restrict__ cm2, int dp, int row0, int kp, int f,
+                                               char* lds, int wave, int lane) {
+#pragma unroll
+  for (int j0 = 0; j0 < KW_DMA; j0 += 4) {
+    const int j = j0 + wave;
+    const int q = j * 64 + lane;
+    const int row = q / KW_CPR;
+    int c = q - row * KW_CPR - ((row >> 3) & 1);
+    if (c < 0) c += KW_CPR;
+    int gr = row0 + row;
+    if (gr > kp - 1) gr = kp - 1;  // past the padded rows: a valid address, never read
+    const __bf16* src = cm2 + (size_t)gr * dp + f * KW_DC + c * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
+    int nkb, unsigned long long* __restrict__ keys) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * KW_TILE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int srot = (r >> 3) & 1;
+  // XCD-aware id -> (point block, centroid block): ids x, x + 8, x + 16, ... (one XCD) walk
+  // the nkb centroid blocks of one point block before the next
+  const long id = blockIdx.x;
+  const long xcd = id & 7, round = id >> 3;
+  const long pb = (round / nkb) * 8 + xcd;
+  const int kb = (int)(round % nkb);
+  const long npb = (N + KW_PTS - 1) / KW_PTS;
+  if (pb >= npb) return;
+  const int row0 = kb * KW_CB;
+  const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
+  const long pbase = pb * KW_PTS + wave * 64;
+  const int nst = dp / KW_DC;
+
+  stage_dma_wide(Cm2, dp, row0, kp, 0, smem, wave, lane);
+  const bf16x8* xrow[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    long p = pbase + g * 32 + r;
+    if (p > N - 1) p = N - 1;
+    xrow[g] = (const bf16x8*)(X + p * ldx);
+  }
+  bf16x8 xf[2][2][KW_KS];  // [buffer][point group][k-step]
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int k = 0; k < KW_KS; ++k) xf[0][g][k] = xrow[g][2 * k + h];
+  floatx16 acc[KW_RG][2];
+#pragma unroll
+  for (int a = 0; a < KW_RG; ++a)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
+  int aoff[KW_KS];
+#pragma unroll
+  for (int k = 0; k < KW_KS; ++k) {
+    int cp = 2 * k + h + srot;
+    if (cp >= KW_CPR) cp -= KW_CPR;
+    aoff[k] = (r * KW_CPR + cp) * 16;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // one feature stage; the register buffer index is a template constant (a runtime index
+  // into xf would put the fragments in scratch)
+  auto stage = [&](int f, auto curtag) {
+    constexpr int cur = decltype(curtag)::value;
+    if (f + 1 < nst) {
+      stage_dma_wide(Cm2, dp, row0, kp, f + 1, smem + (cur ^ 1) * KW_TILE_BYTES, wave, lane);
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int k = 0; k < KW_KS; ++k) xf[cur ^ 1][g][k] = xrow[g][(f + 1) * KW_CPR + 2 * k + h];
+    }
+    const char* buf = smem + cur * KW_TILE_BYTES;
+    bf16x8 af[2][KW_KS];
+#pragma unroll
+    for (int k = 0; k < KW_KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
+#pragma unroll
+    for (int rg = 0; rg < KW_RG; ++rg) {
+      if (rg + 1 < KW_RG) {
+        const char* nb = buf + (rg + 1) * 32 * KW_CPR * 16;
+#pragma unroll
+        for (int k = 0; k < KW_KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
+      }
+      if (rg < live_rg) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int k = 0; k < KW_KS; ++k)
+            acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[cur][g][k], acc[rg][g], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  for (int f = 0; f < nst; f += 2) {
+    stage(f, std::integral_constant<int, 0>{});
+    if (f + 1 < nst) stage(f + 1, std::integral_constant<int, 1>{});
+  }
+  // |x|^2 per point group, from global once after the sweep (L2-warm rows)
+  float xsg[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float t = 0.f;
+    for (int c = h; c < dp / 8; c += 2) {
+      const bf16x8 v = xrow[g][c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t = fmaf((float)v[j], (float)v[j], t);
+    }
+    t += __shfl_xor(t, 32, 64);
+    xsg[g] = t - (float)KM_ONES;
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float best = KM_BIG;
+    int bestt = 0;
+#pragma unroll
+    for (int rg = 0; rg < KW_RG; ++rg) {
+      if (rg >= live_rg) break;
+      float m = keyed(acc[rg][g][0], 0u);
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
+      if (m < best) {
+        best = m;
+        bestt = rg;
+      }
+    }
+    const float ob = __shfl_xor(best, 32, 64);
+    const int obt = __shfl_xor(bestt, 32, 64);
+    const bool take = h ? (ob <= best) : (ob < best);
+    const float bv = take ? ob : best;
+    const int bt = take ? obt : bestt;
+    const int hw = take ? (1 - h) : h;
+    const unsigned reg = __float_as_uint(bv) & 0xFu;
+    const int idx = row0 + bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
+    const long p = pbase + g * 32 + r;
+    if (h == 0 && p < N) {
+      const float dist = fmaxf(bv + xsg[g], 0.f);
+      const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
+      __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// keys -> labels, squared distances, per-block objective partials (256 points per block)
+__global__ __launch_bounds__(256) void kmeans_wide_finish_kernel(const unsigned long long* __restrict__ keys, long N,
+                                                                 int* __restrict__ labels, float* __restrict__ obj_partial,
+                                                                 float* __restrict__ mind) {
+  __shared__ float red[4];
+  const long p = blockIdx.x * 256L + threadIdx.x;
+  float v = 0.f;
+  if (p < N) {
+    const unsigned long long k = keys[p];
+    labels[p] = (int)(k & 0xffffffffull);
+    v = __uint_as_float((unsigned)(k >> 32));
+    if (mind) mind[p] = v;
+  }
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0 && obj_partial) obj_partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 template <int KS, int G, int WAVES, int RG, int PIPE = 0, int PRIO = 0>
 int launch_assign(const void* X, long ldx, const void* Cm2, long N, int Kp, int d, int* labels, float* sums,
                   int ld_sums, float* obj_partial, float* mind, hipStream_t stream) {
@@ -402,6 +592,29 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, long ldx, const void* Cm2, lon
 #undef KM_WIDE
     default: return HARP_EUNSUPPORTED;
   }
+}
+
+// Wide rows (dp > 256, dp % 64 == 0): keys (N uint64, filled with ~0 by the caller) take the
+// per-point (distance, index) minimum over all centroid blocks; harp_kmeans_wide_finish then
+// writes labels / distances / objective partials (one per 256 points).
+HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
+                                        int d, unsigned long long* keys, hipStream_t s) {
+  if (N <= 0 || d + KM_ONES > dp || dp % KW_DC || dp <= 0 || kswept <= 0 || kswept % 32 || kp < kswept ||
+      ldx < dp || ldx % 8 || !keys)
+    return HARP_EBADARG;
+  const long npb = (N + KW_PTS - 1) / KW_PTS;
+  const int nkb = (kswept + KW_CB - 1) / KW_CB;
+  const long rounds = (npb + 7) / 8 * nkb;
+  kmeans_assign_wide_kernel<<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_kmeans_wide_finish(const unsigned long long* keys, long N, int* labels, float* obj_partial,
+                                        float* mind, hipStream_t s) {
+  if (N <= 0) return HARP_OK;
+  kmeans_wide_finish_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(keys, N, labels, obj_partial, mind);
+  return harp_launch_status();
 }
 
 HARP_EXPORT int harp_kmeans_normalize(const float* sums, int ld, float* c, int Kr, int d, float* counts,

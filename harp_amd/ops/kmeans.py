@@ -33,8 +33,13 @@ ONES = 4  # X columns d..d+3 hold 1.0
 DEFAULT_VARIANT = 15
 
 
+NARROW_MAX_DP = 256  # the register-resident assign kernel (X fragments live for the sweep)
+WIDE_ALIGN = 64      # wider rows: the feature-staged kernel's stage width
+
+
 def padded_dim(d: int) -> int:
-    return (d + ONES + 15) // 16 * 16
+    dp = (d + ONES + 15) // 16 * 16
+    return dp if dp <= NARROW_MAX_DP else (d + ONES + WIDE_ALIGN - 1) // WIDE_ALIGN * WIDE_ALIGN
 
 
 def padded_k(k: int) -> int:
@@ -131,6 +136,35 @@ def swept_k(op: "CentroidOperand") -> int:
     return min(op.Cm2.shape[0], (op.K + 31) // 32 * 32)
 
 
+def _assign_wide(X, op, sums, labels, want_objective, obj_partial, min_dist):
+    """dp > 256 (any d): the feature-staged kernel (csrc/kmeans.hip kmeans_assign_wide_kernel)
+    merges per-centroid-block minima with 64-bit atomics, then the bucketed gather-sum."""
+    n, dp = X.shape
+    dev = X.device
+    lib = _lib.kernels()
+    assert X.dtype == torch.bfloat16 and X.stride(1) == 1 and X.stride(0) % 8 == 0 and op.Cm2.shape[1] == dp
+    assert dp % WIDE_ALIGN == 0, f"wide rows need dp % {WIDE_ALIGN} == 0 (pack with padded_dim)"
+    keys = torch.full((n,), -1, dtype=torch.int64, device=dev)  # all ones: +inf distance
+    _lib.check(lib.harp_kmeans_assign_wide(X.data_ptr(), X.stride(0), op.Cm2.data_ptr(), n, dp, swept_k(op),
+                                           op.Cm2.shape[0], op.d, keys.data_ptr(), _lib.stream_ptr(dev)),
+               "kmeans_assign_wide")
+    nblk = (n + 255) // 256
+    if want_objective and (obj_partial is None or obj_partial.numel() < nblk):
+        obj_partial = torch.empty(nblk, dtype=torch.float32, device=dev)
+    _lib.check(lib.harp_kmeans_wide_finish(keys.data_ptr(), n, labels.data_ptr(),
+                                           obj_partial.data_ptr() if want_objective else None,
+                                           min_dist.data_ptr() if min_dist is not None else None,
+                                           _lib.stream_ptr(dev)), "kmeans_wide_finish")
+    if sums is not None:
+        from . import segment
+
+        assert sums.dtype == torch.float32 and sums.shape[1] >= op.d + 1 and sums.is_contiguous()
+        perm, start = segment.bucket_labels(labels, op.Cm2.shape[0])
+        segment.bucket_rowsum(X, perm, start, sums)
+    obj = obj_partial[:nblk].double().sum() if want_objective else None
+    return labels, obj
+
+
 def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = None,
            labels: Optional[torch.Tensor] = None, want_objective: bool = True, variant: int = DEFAULT_VARIANT,
            obj_partial: Optional[torch.Tensor] = None, accumulate: str = "bucket",
@@ -149,8 +183,8 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
         labels = torch.empty(n, dtype=torch.int32, device=dev)
     if _lib.use_native(X):
         lib = _lib.kernels()
-        if dp > 256:
-            raise NotImplementedError(f"native K-means supports d <= {256 - ONES} (got d={op.d})")
+        if dp > NARROW_MAX_DP:
+            return _assign_wide(X, op, sums, labels, want_objective, obj_partial, min_dist)
         if dp > 128:
             variant = 4  # the only instantiation for 9..16 k-steps
         elif variant in (14, 15) and dp // 16 == 5:

@@ -63,8 +63,11 @@ def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out:
         out[:K, : X.shape[1]].index_add_(0, idx, X[perm.long()].float())
         return out
     assert X.dtype == torch.bfloat16 and X.stride(1) == 1 and out.dtype == torch.float32 and out.is_contiguous()
-    st = _lib.kernels().harp_bucket_rowsum_bf16(X.data_ptr(), X.shape[1], X.stride(0), perm.data_ptr(),
-                                                start.data_ptr(), K, perm.numel(), out.data_ptr(), out.stride(0),
-                                                _lib.stream_ptr(X.device))
-    _lib.check(st, "bucket_rowsum")
+    # the kernel sums rows of up to 256 columns; wider rows go as 256-column slices
+    for c0 in range(0, X.shape[1], 256):
+        w = min(256, X.shape[1] - c0)
+        st = _lib.kernels().harp_bucket_rowsum_bf16(X[:, c0:].data_ptr(), w, X.stride(0), perm.data_ptr(),
+                                                    start.data_ptr(), K, perm.numel(), out[:, c0:].data_ptr(),
+                                                    out.stride(0), _lib.stream_ptr(X.device))
+        _lib.check(st, "bucket_rowsum")
     return out

@@ -179,3 +179,47 @@ def test_row_stride_view_matches_contiguous(cuda):
         out.append((lab.clone(), obj.item(), sums))
     assert torch.equal(out[0][0], out[1][0]) and out[0][1] == pytest.approx(out[1][1], rel=1e-12)
     assert torch.allclose(out[0][2], out[1][2], rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,d,k", [(5000, 300, 300), (3000, 512, 1000), (4099, 1000, 257), (2000, 253, 100),
+                                   (1000, 2000, 64), (70000, 1000, 1000)])
+def test_assign_wide_rows_matches_torch(cuda, n, d, k):
+    """d > 252 (padded rows wider than 256): the feature-staged kernel against a torch fp64
+    argmin on the same bf16 operands (the reference has no d limit,
+    CenCalcTask.java:67-100)."""
+    torch.manual_seed(1)
+    x = torch.rand(n, d, device=cuda) * 1000
+    X = K.pack_points(x, cuda)
+    assert X.shape[1] > 256 and X.shape[1] % 64 == 0
+    c = torch.rand(k, d, device=cuda) * 1000
+    op = K.prepare(c, X.shape[1])
+    sums = torch.zeros((K.padded_k(k), X.shape[1]), dtype=torch.float32, device=cuda)
+    md = torch.empty(n, dtype=torch.float32, device=cuda)
+    lab, obj = K.assign(X, op, sums=sums, min_dist=md)
+    torch.cuda.synchronize()
+    c_bf = c.to(torch.bfloat16).float()
+    rlab, dist, rbest = _ref_assign(X, c_bf, d)
+    lab = lab.long()
+    assert int(lab.min()) >= 0 and int(lab.max()) < k
+    chosen = dist.gather(1, lab[:, None])[:, 0]
+    best = dist.gather(1, rlab[:, None])[:, 0]
+    scale = (X[:, :d].double() ** 2).sum(1) + (c_bf.double() ** 2).sum(1).max()
+    assert bool(((chosen - best) <= 1e-5 * scale).all())
+    assert (lab == rlab).float().mean() > 0.99
+    assert abs(obj.item() - rbest.sum().item()) <= 1e-4 * abs(rbest.sum().item()) + 1e-3
+    assert torch.allclose(md.double(), chosen + (X[:, :d].double() ** 2).sum(1), rtol=1e-4, atol=1.0)
+    ref = torch.zeros_like(sums, dtype=torch.float64)
+    ref[:, : d + 1].index_add_(0, lab, X[:, : d + 1].double())
+    assert torch.allclose(sums[:, : d + 1].double(), ref[:, : d + 1], rtol=1e-5, atol=1e-1)
+    assert int(sums[:, d].sum().item()) == n
+
+
+def test_kmeans_model_wide_d(cuda):
+    """The model runs natively at d = 1000 (no NotImplementedError, objective decreasing)."""
+    from harp_amd.models.kmeans import KMeansConfig, run_kmeans
+    from harp_amd.parallel.comm import Communicator
+
+    cfg = KMeansConfig(num_points=20000, num_centroids=100, dim=1000, iterations=3, strategy="allreduce")
+    res = run_kmeans(Communicator(None, cuda), cfg)
+    obj = res["objective"]
+    assert len(obj) == 3 and obj[2] <= obj[0]
