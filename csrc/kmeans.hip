@@ -363,32 +363,43 @@ __global__ void uniform_rows_bf16_kernel(__bf16* __restrict__ X, long N, int d, 
 //    as integers, ties go to the lower index);
 //  * grid: consecutive ids of one XCD (id mod 8) take the centroid blocks of one point block
 //    one after another, so that block's rows come from HBM once and from L2 after.
-constexpr int KW_PTS = 256, KW_CB = 256, KW_DC = 64, KW_RG = KW_CB / 32, KW_KS = KW_DC / 16;
-constexpr int KW_CPR = KW_DC / 8;                       // 16-B chunks per centroid row per stage
-constexpr int KW_TILE_BYTES = KW_CB * KW_DC * 2;        // 32 KiB
-constexpr int KW_DMA = KW_CB * KW_CPR / 64;             // 1-KiB DMA pieces per stage (32)
+constexpr int KW_CB = 256, KW_RG = KW_CB / 32;  // centroids per workgroup (8 row groups of 32)
 
+// G point groups of 32 per wave (4 waves), DC features per stage, OCC waves per SIMD
+template <int G, int DC>
+struct KWCfg {
+  static constexpr int KS = DC / 16;                  // MFMA k-steps per stage
+  static constexpr int CPR = DC / 8;                  // 16-B chunks per centroid row per stage
+  static constexpr int TILE_BYTES = KW_CB * DC * 2;
+  static constexpr int DMA = KW_CB * CPR / 64;        // 1-KiB DMA pieces per stage
+  static constexpr int PTS = 4 * G * 32;              // points per workgroup
+};
+
+template <class C>
 __device__ __forceinline__ void stage_dma_wide(const __bf16* __restrict__ cm2, int dp, int row0, int kp, int f,
                                                char* lds, int wave, int lane) {
 #pragma unroll
-  for (int j0 = 0; j0 < KW_DMA; j0 += 4) {
+  for (int j0 = 0; j0 < C::DMA; j0 += 4) {
     const int j = j0 + wave;
     const int q = j * 64 + lane;
-    const int row = q / KW_CPR;
-    int c = q - row * KW_CPR - ((row >> 3) & 1);
-    if (c < 0) c += KW_CPR;
+    const int row = q / C::CPR;
+    int c = q - row * C::CPR - ((row >> 3) & 1);
+    if (c < 0) c += C::CPR;
     int gr = row0 + row;
     if (gr > kp - 1) gr = kp - 1;  // past the padded rows: a valid address, never read
-    const __bf16* src = cm2 + (size_t)gr * dp + f * KW_DC + c * 8;
+    const __bf16* src = cm2 + (size_t)gr * dp + f * (C::CPR * 8) + c * 8;
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                      (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
   }
 }
 
-__global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
+template <int G, int DC, int OCC>
+__global__ __launch_bounds__(256, OCC) void kmeans_assign_wide_kernel(
     const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
     int nkb, unsigned long long* __restrict__ keys) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * KW_TILE_BYTES];
+  using C = KWCfg<G, DC>;
+  constexpr int KS = C::KS;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::TILE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int srot = (r >> 3) & 1;
@@ -398,39 +409,39 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
   const long xcd = id & 7, round = id >> 3;
   const long pb = (round / nkb) * 8 + xcd;
   const int kb = (int)(round % nkb);
-  const long npb = (N + KW_PTS - 1) / KW_PTS;
+  const long npb = (N + C::PTS - 1) / C::PTS;
   if (pb >= npb) return;
   const int row0 = kb * KW_CB;
   const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
-  const long pbase = pb * KW_PTS + wave * 64;
-  const int nst = dp / KW_DC;
+  const long pbase = pb * C::PTS + wave * (G * 32);
+  const int nst = dp / DC;
 
-  stage_dma_wide(Cm2, dp, row0, kp, 0, smem, wave, lane);
-  const bf16x8* xrow[2];
+  stage_dma_wide<C>(Cm2, dp, row0, kp, 0, smem, wave, lane);
+  const bf16x8* xrow[G];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < G; ++g) {
     long p = pbase + g * 32 + r;
     if (p > N - 1) p = N - 1;
     xrow[g] = (const bf16x8*)(X + p * ldx);
   }
-  bf16x8 xf[2][2][KW_KS];  // [buffer][point group][k-step]
+  bf16x8 xf[2][G][KS];  // [buffer][point group][k-step]
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int k = 0; k < KW_KS; ++k) xf[0][g][k] = xrow[g][2 * k + h];
-  floatx16 acc[KW_RG][2];
+    for (int k = 0; k < KS; ++k) xf[0][g][k] = xrow[g][2 * k + h];
+  floatx16 acc[KW_RG][G];
 #pragma unroll
   for (int a = 0; a < KW_RG; ++a)
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
-  int aoff[KW_KS];
+  int aoff[KS];
 #pragma unroll
-  for (int k = 0; k < KW_KS; ++k) {
+  for (int k = 0; k < KS; ++k) {
     int cp = 2 * k + h + srot;
-    if (cp >= KW_CPR) cp -= KW_CPR;
-    aoff[k] = (r * KW_CPR + cp) * 16;
+    if (cp >= C::CPR) cp -= C::CPR;
+    aoff[k] = (r * C::CPR + cp) * 16;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -439,28 +450,28 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
   auto stage = [&](int f, auto curtag) {
     constexpr int cur = decltype(curtag)::value;
     if (f + 1 < nst) {
-      stage_dma_wide(Cm2, dp, row0, kp, f + 1, smem + (cur ^ 1) * KW_TILE_BYTES, wave, lane);
+      stage_dma_wide<C>(Cm2, dp, row0, kp, f + 1, smem + (cur ^ 1) * C::TILE_BYTES, wave, lane);
 #pragma unroll
-      for (int g = 0; g < 2; ++g)
+      for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int k = 0; k < KW_KS; ++k) xf[cur ^ 1][g][k] = xrow[g][(f + 1) * KW_CPR + 2 * k + h];
+        for (int k = 0; k < KS; ++k) xf[cur ^ 1][g][k] = xrow[g][(f + 1) * C::CPR + 2 * k + h];
     }
-    const char* buf = smem + cur * KW_TILE_BYTES;
-    bf16x8 af[2][KW_KS];
+    const char* buf = smem + cur * C::TILE_BYTES;
+    bf16x8 af[2][KS];
 #pragma unroll
-    for (int k = 0; k < KW_KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
+    for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
 #pragma unroll
     for (int rg = 0; rg < KW_RG; ++rg) {
       if (rg + 1 < KW_RG) {
-        const char* nb = buf + (rg + 1) * 32 * KW_CPR * 16;
+        const char* nb = buf + (rg + 1) * 32 * C::CPR * 16;
 #pragma unroll
-        for (int k = 0; k < KW_KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
+        for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
       }
       if (rg < live_rg) {
 #pragma unroll
-        for (int g = 0; g < 2; ++g)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-          for (int k = 0; k < KW_KS; ++k)
+          for (int k = 0; k < KS; ++k)
             acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[cur][g][k], acc[rg][g], 0, 0, 0);
       }
     }
@@ -472,9 +483,9 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
     if (f + 1 < nst) stage(f + 1, std::integral_constant<int, 1>{});
   }
   // |x|^2 per point group, from global once after the sweep (L2-warm rows)
-  float xsg[2];
+  float xsg[G];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < G; ++g) {
     float t = 0.f;
     for (int c = h; c < dp / 8; c += 2) {
       const bf16x8 v = xrow[g][c];
@@ -485,7 +496,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
     xsg[g] = t - (float)KM_ONES;
   }
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < G; ++g) {
     float best = KM_BIG;
     int bestt = 0;
 #pragma unroll
@@ -514,6 +525,19 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_kernel(
       __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+template <int G, int DC, int OCC>
+int launch_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
+                unsigned long long* keys, hipStream_t s) {
+  using C = KWCfg<G, DC>;
+  if (dp % DC) return HARP_EBADARG;
+  const long npb = (N + C::PTS - 1) / C::PTS;
+  const int nkb = (kswept + KW_CB - 1) / KW_CB;
+  const long rounds = (npb + 7) / 8 * nkb;
+  kmeans_assign_wide_kernel<G, DC, OCC><<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
+  return harp_launch_status();
 }
 
 // keys -> labels, squared distances, per-block objective partials (256 points per block)
@@ -596,18 +620,20 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, long ldx, const void* Cm2, lon
 
 // Wide rows (dp > 256, dp % 64 == 0): keys (N uint64, filled with ~0 by the caller) take the
 // per-point (distance, index) minimum over all centroid blocks; harp_kmeans_wide_finish then
-// writes labels / distances / objective partials (one per 256 points).
+// writes labels / distances / objective partials (one per 256 points). variant: 0 = auto,
+// 1 = (2 point groups, 64-feature stages, 1 wave / SIMD), 2 = (2, 128, 1), 3 = (1, 64, 2).
 HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
-                                        int d, unsigned long long* keys, hipStream_t s) {
-  if (N <= 0 || d + KM_ONES > dp || dp % KW_DC || dp <= 0 || kswept <= 0 || kswept % 32 || kp < kswept ||
+                                        int d, unsigned long long* keys, int variant, hipStream_t s) {
+  if (N <= 0 || d + KM_ONES > dp || dp % 64 || dp <= 0 || kswept <= 0 || kswept % 32 || kp < kswept ||
       ldx < dp || ldx % 8 || !keys)
     return HARP_EBADARG;
-  const long npb = (N + KW_PTS - 1) / KW_PTS;
-  const int nkb = (kswept + KW_CB - 1) / KW_CB;
-  const long rounds = (npb + 7) / 8 * nkb;
-  kmeans_assign_wide_kernel<<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
-      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
-  return harp_launch_status();
+  if (variant == 0) variant = dp % 128 == 0 ? 2 : 1;
+  switch (variant) {
+    case 1: return launch_wide<2, 64, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 2: return launch_wide<2, 128, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 3: return launch_wide<1, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    default: return HARP_EBADARG;
+  }
 }
 
 HARP_EXPORT int harp_kmeans_wide_finish(const unsigned long long* keys, long N, int* labels, float* obj_partial,

@@ -27,8 +27,9 @@ _SIGNATURES = {
     "harp_kmeans_points_per_block": [c_int],
     "harp_kmeans_assign": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_int, c_void_p],
-    # X, ldx, Cm2, N, dp, kswept, kp, d, keys, stream
-    "harp_kmeans_assign_wide": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    # X, ldx, Cm2, N, dp, kswept, kp, d, keys, variant, stream
+    "harp_kmeans_assign_wide": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                c_void_p],
     "harp_kmeans_wide_finish": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
     "harp_kmeans_normalize": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "harp_kmeans_prepare": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

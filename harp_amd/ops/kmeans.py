@@ -35,6 +35,7 @@ DEFAULT_VARIANT = 15
 
 NARROW_MAX_DP = 256  # the register-resident assign kernel (X fragments live for the sweep)
 WIDE_ALIGN = 64      # wider rows: the feature-staged kernel's stage width
+WIDE_VARIANT = int(os.environ.get("HARP_KMEANS_WIDE_VARIANT", "0"))  # 0: the kernel's default tiling
 
 
 def padded_dim(d: int) -> int:
@@ -146,7 +147,7 @@ def _assign_wide(X, op, sums, labels, want_objective, obj_partial, min_dist):
     assert dp % WIDE_ALIGN == 0, f"wide rows need dp % {WIDE_ALIGN} == 0 (pack with padded_dim)"
     keys = torch.full((n,), -1, dtype=torch.int64, device=dev)  # all ones: +inf distance
     _lib.check(lib.harp_kmeans_assign_wide(X.data_ptr(), X.stride(0), op.Cm2.data_ptr(), n, dp, swept_k(op),
-                                           op.Cm2.shape[0], op.d, keys.data_ptr(), _lib.stream_ptr(dev)),
+                                           op.Cm2.shape[0], op.d, keys.data_ptr(), WIDE_VARIANT, _lib.stream_ptr(dev)),
                "kmeans_assign_wide")
     nblk = (n + 255) // 256
     if want_objective and (obj_partial is None or obj_partial.numel() < nblk):

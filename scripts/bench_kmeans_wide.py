@@ -15,7 +15,9 @@ X = K.generate_points(N, d, 0.0, 1000.0, seed=1, device="cuda")
 c = torch.rand(Kc, d, device="cuda") * 1000
 op = K.prepare(c, X.shape[1])
 lab = torch.empty(N, dtype=torch.int32, device="cuda")
-for mode in ("assign", "assign+sums"):
+variants = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]
+for var, mode in [(v, "assign") for v in variants] + [(variants[0], "assign+sums")]:
+    K.WIDE_VARIANT = var
     sums = torch.zeros((K.padded_k(Kc), X.shape[1]), dtype=torch.float32, device="cuda") if mode != "assign" else None
     K.assign(X, op, sums=sums, labels=lab)
     torch.cuda.synchronize()
@@ -27,5 +29,5 @@ for mode in ("assign", "assign+sums"):
         K.assign(X, op, sums=sums, labels=lab)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    print(f"{mode}: N={N} K={Kc} d={d} dp={X.shape[1]}: {dt * 1e3:.2f} ms, {2.0 * N * Kc * d / dt / 1e12:.0f} TFLOP/s "
+    print(f"variant {var} {mode}: N={N} K={Kc} d={d} dp={X.shape[1]}: {dt * 1e3:.2f} ms, {2.0 * N * Kc * d / dt / 1e12:.0f} TFLOP/s "
           "useful", flush=True)
