@@ -527,6 +527,150 @@ __global__ __launch_bounds__(256, OCC) void kmeans_assign_wide_kernel(
   }
 }
 
+// The same tile with a 3-deep pipeline: stage f + 2's centroid slice (LDS-DMA) and point
+// slices (registers) are issued once stage f's have landed, so two stages of loads are in
+// flight under each stage's MFMAs (counted vmcnt waits, one barrier per stage).
+template <int G, int DC>
+__global__ __launch_bounds__(256, 1) void kmeans_assign_wide3_kernel(
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
+    int nkb, unsigned long long* __restrict__ keys) {
+  using C = KWCfg<G, DC>;
+  constexpr int KS = C::KS;
+  constexpr int OPS = C::DMA / 4 + G * KS;  // vector-memory instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[3 * C::TILE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int srot = (r >> 3) & 1;
+  const long id = blockIdx.x;
+  const long xcd = id & 7, round = id >> 3;
+  const long pb = (round / nkb) * 8 + xcd;
+  const int kb = (int)(round % nkb);
+  const long npb = (N + C::PTS - 1) / C::PTS;
+  if (pb >= npb) return;
+  const int row0 = kb * KW_CB;
+  const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
+  const long pbase = pb * C::PTS + wave * (G * 32);
+  const int nst = dp / DC;
+  const bf16x8* xrow[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    long p = pbase + g * 32 + r;
+    if (p > N - 1) p = N - 1;
+    xrow[g] = (const bf16x8*)(X + p * ldx);
+  }
+  bf16x8 xf[3][G][KS];
+  floatx16 acc[KW_RG][G];
+#pragma unroll
+  for (int a = 0; a < KW_RG; ++a)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
+  int aoff[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    int cp = 2 * k + h + srot;
+    if (cp >= C::CPR) cp -= C::CPR;
+    aoff[k] = (r * C::CPR + cp) * 16;
+  }
+  auto issue = [&](int f, auto btag) {
+    constexpr int b = decltype(btag)::value;
+    stage_dma_wide<C>(Cm2, dp, row0, kp, f, smem + b * C::TILE_BYTES, wave, lane);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) xf[b][g][k] = xrow[g][f * C::CPR + 2 * k + h];
+  };
+  issue(0, std::integral_constant<int, 0>{});
+  if (nst > 1) issue(1, std::integral_constant<int, 1>{});
+  auto stage = [&](int f, auto btag) {
+    constexpr int b = decltype(btag)::value;
+    if (f + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (f + 2 < nst) issue(f + 2, std::integral_constant<int, (b + 2) % 3>{});
+    const char* buf = smem + b * C::TILE_BYTES;
+    bf16x8 af[2][KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
+#pragma unroll
+    for (int rg = 0; rg < KW_RG; ++rg) {
+      if (rg + 1 < KW_RG) {
+        const char* nb = buf + (rg + 1) * 32 * C::CPR * 16;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
+      }
+      if (rg < live_rg) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int k = 0; k < KS; ++k)
+            acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[b][g][k], acc[rg][g], 0, 0, 0);
+      }
+    }
+  };
+  for (int f = 0; f < nst; f += 3) {
+    stage(f, std::integral_constant<int, 0>{});
+    if (f + 1 < nst) stage(f + 1, std::integral_constant<int, 1>{});
+    if (f + 2 < nst) stage(f + 2, std::integral_constant<int, 2>{});
+  }
+  float xsg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float t = 0.f;
+    for (int c = h; c < dp / 8; c += 2) {
+      const bf16x8 v = xrow[g][c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t = fmaf((float)v[j], (float)v[j], t);
+    }
+    t += __shfl_xor(t, 32, 64);
+    xsg[g] = t - (float)KM_ONES;
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float best = KM_BIG;
+    int bestt = 0;
+#pragma unroll
+    for (int rg = 0; rg < KW_RG; ++rg) {
+      if (rg >= live_rg) break;
+      float m = keyed(acc[rg][g][0], 0u);
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
+      if (m < best) {
+        best = m;
+        bestt = rg;
+      }
+    }
+    const float ob = __shfl_xor(best, 32, 64);
+    const int obt = __shfl_xor(bestt, 32, 64);
+    const bool take = h ? (ob <= best) : (ob < best);
+    const float bv = take ? ob : best;
+    const int bt = take ? obt : bestt;
+    const int hw = take ? (1 - h) : h;
+    const unsigned reg = __float_as_uint(bv) & 0xFu;
+    const int idx = row0 + bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
+    const long p = pbase + g * 32 + r;
+    if (h == 0 && p < N) {
+      const float dist = fmaxf(bv + xsg[g], 0.f);
+      const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
+      __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int G, int DC>
+int launch_wide3(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
+                 unsigned long long* keys, hipStream_t s) {
+  using C = KWCfg<G, DC>;
+  if (dp % DC) return HARP_EBADARG;
+  const long npb = (N + C::PTS - 1) / C::PTS;
+  const int nkb = (kswept + KW_CB - 1) / KW_CB;
+  const long rounds = (npb + 7) / 8 * nkb;
+  kmeans_assign_wide3_kernel<G, DC><<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
+  return harp_launch_status();
+}
+
 template <int G, int DC, int OCC>
 int launch_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                 unsigned long long* keys, hipStream_t s) {
@@ -632,6 +776,7 @@ HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2
     case 1: return launch_wide<2, 64, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 2: return launch_wide<2, 128, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 3: return launch_wide<1, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 4: return launch_wide3<2, 64>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     default: return HARP_EBADARG;
   }
 }

@@ -116,3 +116,24 @@ def test_tsqr_auto_cholqr2_on_gpu(cuda, d):
     assert ST.cholesky_qr2(bad) is None
     fb = ST.tsqr(bad)
     assert torch.allclose(fb["Q"] @ fb["R"], bad, atol=1e-8 * float(bad.abs().max()))
+
+
+def test_precision_policy_covariance_1e6x1000(cuda):
+    """on 1e6 x 1000 U[0,1) fp32 data the fp32 mode is within 1e-6 (normwise,
+    relative) of an fp64 covariance; the bf16 fast path (one bf16 operand, fp32 accumulation,
+    sums from the same operand) within its documented 3e-3; fp64 within 1e-12."""
+    from harp_amd.models import stats as ST
+
+    g = torch.Generator(device=cuda).manual_seed(9)
+    X = torch.rand(1_000_000, 1000, generator=g, device=cuda, dtype=torch.float32)
+    X64 = X.double()
+    mu = X64.mean(0)
+    ref = (X64.t() @ X64 - X64.shape[0] * torch.outer(mu, mu)) / (X64.shape[0] - 1)
+    del X64
+    nrm = float(ref.abs().max())
+    err = {}
+    for mode in ("fp32", "bf16", "fp64"):
+        err[mode] = float((ST.covariance(X, dtype=mode)["covariance"] - ref).abs().max()) / nrm
+    print("covariance relative error by mode:", err)
+    assert err["fp32"] <= 1e-6 and err["bf16"] <= 3e-3 and err["fp64"] <= 1e-12, err
+    assert ST._policy(X, None) == "fp32"  # an fp32 input is never silently rounded to bf16
