@@ -17,7 +17,7 @@ allreduce + fp64 eig) and LDA-CGS over 1M docs x 1M vocab x 1000 topics with the
 collective, each split over the ranks and bounded by ``--extras-timeout``.
 
 MF-SGD (nested ``sgd`` record): 480,189 x 17,770, 100,480,507 synthetic ratings, rank
-128, H split into ``--sgd-slices`` slices per rank (default 1) that rotate around the ring
+128, H split into ``--sgd-slices`` slices per rank (default: 1 on one GPU, 2 at P > 1) that rotate around the ring
 (model rotation); epochs timed after warmup; updates/sec = ratings trained / epoch time
 (SGDCollectiveMapper.java:294-298).
 
@@ -67,12 +67,12 @@ def parse_args(argv=None):
     ap.add_argument("--sgd-rank", type=int, default=128)
     ap.add_argument("--sgd-epochs", type=int, default=10)
     ap.add_argument("--sgd-warmup", type=int, default=1)
-    ap.add_argument("--sgd-slices", type=int, default=1,
-                    help="H slices per rank (rotation pipeline depth). 1: each slice step trains twice the cells "
-                         "in half the launches -- 6.3 vs 7.6 ms per 100M-rating epoch on one GPU, 1.76 vs 2.36 ms "
-                         "at the 8-GPU share -- more than the unhidden slice transfer costs (H/P over one xGMI "
-                         "link, ~8 x 40 us per epoch at P = 8; profiles/r3_sgd_slices). 2 overlaps each slice's "
-                         "rotation with the other slice's compute (the reference's numModelSlices default)")
+    ap.add_argument("--sgd-slices", type=int, default=0,
+                    help="H slices per rank (rotation pipeline depth); 0 = auto: 1 on one GPU (nothing rotates; "
+                         "each slice step then trains twice the cells in half the launches, 6.3 vs 7.6 ms per "
+                         "100M-rating epoch, profiles/r3_sgd_slices), 2 at P > 1 so every slice's transfer to "
+                         "the ring neighbour overlaps the other slice's compute (the reference's numModelSlices "
+                         "default, MJ/dymoro/Rotator.java:30-86)")
     ap.add_argument("--sgd-timeout", type=float, default=240.0,
                     help="wall-clock bound (s) on the nested MF-SGD record; past it rank 0 prints the "
                          "K-means line with an sgd error and every rank exits")
@@ -216,7 +216,7 @@ def bench_sgd(args, comm, torch):
     t0 = time.perf_counter()
     u, i, v = synthetic_ratings(args.sgd_users, args.sgd_items, args.sgd_ratings, seed=7, device=dev)
     cfg = SGDConfig(rank=args.sgd_rank, epochs=args.sgd_warmup + args.sgd_epochs, test_every=0,
-                    xcd_blocks=dev.type == "cuda", num_slices=args.sgd_slices)
+                    xcd_blocks=dev.type == "cuda", num_slices=args.sgd_slices or (1 if P == 1 else 2))
     m = SGDCollectiveMapper(comm, cfg, args.sgd_users, args.sgd_items, (u, i, v), None)
     m.init_model(_Reader())
     del u, i, v

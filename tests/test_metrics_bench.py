@@ -188,7 +188,7 @@ def test_bench_full_records_three_ranks():
 def test_bench_full_records_eight_ranks():
     """Same at the 8-GPU node's world size (8 gloo ranks on the CPU), with the bench's
     default one slice per rank."""
-    _check_full_record(_run_bench(["--gpus", "8"] + _TINY), 8)
+    _check_full_record(_run_bench(["--gpus", "8"] + _TINY), 8, slices=2)  # auto: 2 slices at P > 1
 
 
 def test_bench_single_rank_lda_records_collective_cost():
