@@ -375,6 +375,16 @@ struct KWCfg {
   static constexpr int PTS = 4 * G * 32;              // points per workgroup
 };
 
+// LDS chunk rotation of centroid row `row` for the wide tiles: ds_read_b128 serves 16 lanes
+// (rows r..r+15 of one 16-B chunk column) per LDS cycle, so their 16 addresses must fall on
+// 16 distinct 16-B slots of a 256-B bank row. With 128-B rows (CPR 8) rows r and r + 2
+// alias, so the rotation walks r >> 1; with 256-B rows (CPR 16) every row aliases, so it
+// walks r.
+template <int CPR>
+__device__ __forceinline__ int wide_rot(int row) {
+  return CPR == 8 ? (row >> 1) & 7 : CPR == 16 ? row & 15 : (row >> 3) & 1;
+}
+
 template <class C>
 __device__ __forceinline__ void stage_dma_wide(const __bf16* __restrict__ cm2, int dp, int row0, int kp, int f,
                                                char* lds, int wave, int lane) {
@@ -383,7 +393,7 @@ __device__ __forceinline__ void stage_dma_wide(const __bf16* __restrict__ cm2, i
     const int j = j0 + wave;
     const int q = j * 64 + lane;
     const int row = q / C::CPR;
-    int c = q - row * C::CPR - ((row >> 3) & 1);
+    int c = q - row * C::CPR - wide_rot<C::CPR>(row);
     if (c < 0) c += C::CPR;
     int gr = row0 + row;
     if (gr > kp - 1) gr = kp - 1;  // past the padded rows: a valid address, never read
@@ -439,8 +449,7 @@ __global__ __launch_bounds__(256, OCC) void kmeans_assign_wide_kernel(
   int aoff[KS];
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
-    int cp = 2 * k + h + srot;
-    if (cp >= C::CPR) cp -= C::CPR;
+    const int cp = (2 * k + h + wide_rot<C::CPR>(r)) % C::CPR;
     aoff[k] = (r * C::CPR + cp) * 16;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -569,8 +578,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide3_kernel(
   int aoff[KS];
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
-    int cp = 2 * k + h + srot;
-    if (cp >= C::CPR) cp -= C::CPR;
+    const int cp = (2 * k + h + wide_rot<C::CPR>(r)) % C::CPR;
     aoff[k] = (r * C::CPR + cp) * 16;
   }
   auto issue = [&](int f, auto btag) {
