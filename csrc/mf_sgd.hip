@@ -30,7 +30,6 @@
 #include "common.h"
 
 #include <climits>
-#include <type_traits>
 
 namespace {
 
@@ -346,101 +345,6 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
   store_row<EPL>(W + (cur * ldw + lo), w);
 }
 
-// sgd_stream_lds with the H rows prefetched PD ratings ahead (ring of PD row buffers): a
-// stream's update is a dependent chain through its W row, and each rating waits for an H
-// load issued PD ratings earlier, so PD bounds the loads in flight per stream. At small
-// per-rank shares the chip holds few streams (the cell's ratings / chunk), so the chain's
-// L2 latency per rating, not bandwidth, sets the launch (~0.6 us per rating at PD = 2,
-// profiles/r3_sgd_flow). Rows updated by the last two ratings are forwarded as in
-// sgd_stream_lds; an item repeated 3..PD ratings later inside one stream (only across a
-// user boundary of the user-sorted stream) reads the prefetched copy -- the staleness every
-// Hogwild stream already has with respect to the other streams of the XCD.
-template <int R, int PD>
-__device__ __forceinline__ void sgd_stream_lds_pd(const int* sR, const int* sC, const float* sV, int n, int sl,
-                                                  float* __restrict__ W, unsigned ldw, float* __restrict__ H,
-                                                  unsigned ldh, float lr, float lam) {
-  constexpr int EPL = R / 16;
-  constexpr int PAIRS = EPL / 2;
-  const float decay = 1.0f - lr * lam;
-  const unsigned lo = lane_off<EPL>(sl);
-  float w[EPL], h[EPL], hp[EPL];
-  float hb[PD][EPL];
-  unsigned cur = (unsigned)sR[0], col0 = (unsigned)sC[0], colp = 0xffffffffu;
-  float v0 = sV[0];
-  load_row<EPL>(W + (cur * ldw + lo), w);
-  load_row_l2<EPL>(H + (col0 * ldh + lo), h);
-#pragma unroll
-  for (int q = 1; q <= PD; ++q) {  // ratings 1..PD into ring slots q % PD
-    const int iq = q < n ? q : n - 1;
-    load_row_l2<EPL>(H + ((unsigned)sC[iq] * ldh + lo), hb[q % PD]);
-  }
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) hp[k] = 0.f;
-  int i = 0;
-  auto step = [&](auto btag) -> bool {
-    constexpr int b = decltype(btag)::value;  // == i % PD: the slot rating i's prefetch used
-    floatx2 d2 = {0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < PAIRS; ++p)
-      d2 = __builtin_elementwise_fma(floatx2{w[2 * p], w[2 * p + 1]}, floatx2{h[2 * p], h[2 * p + 1]}, d2);
-    float dot = d2[0] + d2[1];
-    if constexpr (EPL % 2) dot = fmaf(w[EPL - 1], h[EPL - 1], dot);
-    const float ge = -lr * (sub16_sum(dot) - v0);
-    const floatx2 g = {ge, ge}, dc = {decay, decay};
-#pragma unroll
-    for (int p = 0; p < PAIRS; ++p) {
-      const floatx2 wk = {w[2 * p], w[2 * p + 1]}, hk = {h[2 * p], h[2 * p + 1]};
-      const floatx2 wn = __builtin_elementwise_fma(g, hk, dc * wk);
-      const floatx2 hn = __builtin_elementwise_fma(g, wk, dc * hk);
-      w[2 * p] = wn[0];
-      w[2 * p + 1] = wn[1];
-      h[2 * p] = hn[0];
-      h[2 * p + 1] = hn[1];
-    }
-    if constexpr (EPL % 2) {
-      const float wk = w[EPL - 1], hk = h[EPL - 1];
-      w[EPL - 1] = fmaf(ge, hk, decay * wk);
-      h[EPL - 1] = fmaf(ge, wk, decay * hk);
-    }
-    const bool last = i + 1 >= n;
-    const int i1 = last ? i : i + 1;
-    const unsigned row1 = (unsigned)sR[i1], col1 = (unsigned)sC[i1];
-    if (!last && row1 != cur) {
-      store_row<EPL>(W + (cur * ldw + lo), w);
-      cur = row1;
-      load_row<EPL>(W + (cur * ldw + lo), w);
-    }
-    // slot b (rating i's, consumed) takes rating i + PD (clamped: a harmless re-read)
-    const int ip = i + PD < n ? i + PD : n - 1;
-    load_row_l2<EPL>(H + ((unsigned)sC[ip] * ldh + lo), hb[b]);
-    store_row<EPL>(H + (col0 * ldh + lo), h);
-    if (last) return false;
-    const bool s0 = col1 == col0, s1 = col1 == colp;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const float nx = s0 ? h[k] : (s1 ? hp[k] : hb[(b + 1) % PD][k]);
-      hp[k] = h[k];
-      h[k] = nx;
-    }
-    colp = col0;
-    col0 = col1;
-    v0 = sV[i1];
-    ++i;
-    return true;
-  };
-  if constexpr (PD == 4) {
-    while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{}) &&
-           step(std::integral_constant<int, 2>{}) && step(std::integral_constant<int, 3>{})) {
-    }
-  } else {
-    static_assert(PD == 3, "PD 3 or 4");
-    while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{}) &&
-           step(std::integral_constant<int, 2>{})) {
-    }
-  }
-  store_row<EPL>(W + (cur * ldw + lo), w);
-}
-
 // Sub-step `step` of the XCD-blocked schedule. off[c] .. off[c + 1] are the ratings of cell
 // c = user_block * 8 + item_block (cell-major, user-sorted inside a cell). The blocks that
 // share an XCD (same blockIdx.x % 8) take rounds of 16 consecutive streams of CH ratings:
@@ -448,7 +352,7 @@ __device__ __forceinline__ void sgd_stream_lds_pd(const int* sR, const int* sC, 
 // 16-lane subgroup runs one stream. `win` (optional, 2 x 64 int64): cell c trains only the
 // window of win[64 + c] ratings starting at win[c], wrapping around the cell — the
 // fixed-fraction mode standing in for the reference's timer-bounded rotation steps.
-template <int R, int CH, int PD = 2>
+template <int R, int CH>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
                                                          const long* __restrict__ win, int step,
@@ -481,14 +385,9 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
     }
     __syncthreads();
     const long mine = n - (r0 + (long)sub * CH);
-    if (mine > 0) {
-      if constexpr (PD == 2)
-        sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
-                          (unsigned)ldw, H, (unsigned)ldh, lr, lam);
-      else
-        sgd_stream_lds_pd<R, PD>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
-                                 (unsigned)ldw, H, (unsigned)ldh, lr, lam);
-    }
+    if (mine > 0)
+      sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
+                             (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
 }
 
@@ -694,18 +593,10 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
 
 template <int R, int CH>
 int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win, int steps,
-                   int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, int pd,
-                   hipStream_t s) {
+                   int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
-    if (pd == 4)
-      mf_sgd_xcd_kernel<R, CH, 4><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
-    else if (pd == 3)
-      mf_sgd_xcd_kernel<R, CH, 3><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
-    else
-      mf_sgd_xcd_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
+    mf_sgd_xcd_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+        rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -966,11 +857,8 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
                                 int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
                                 float* H, int ldh, float lr, float lam, hipStream_t s) {
-  // variant 0: H rows prefetched 2 ratings ahead; 2 / 3: 4 / 3 ahead (sgd_stream_lds_pd)
-  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r ||
-      (variant != 0 && variant != 2 && variant != 3))
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant != 0)
     return HARP_EBADARG;
-  const int pd = variant == 2 ? 4 : variant == 3 ? 3 : 2;
   if (wide_ok(r)) {  // wide ranks: one wave per stream, variants do not apply
     if (chunk != 32 && chunk != 64 && chunk != 128) return HARP_EBADARG;
 #define SGDXW_CALL(QQ) \
@@ -978,7 +866,7 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
     WIDE_DISPATCH(r, SGDXW_CALL)
 #undef SGDXW_CALL
   }
-#define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, pd, s
+#define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
 #define SGDX_CALL(RR)                                                             \
   (chunk == 8 ? launch_sgd_xcd<RR, 8>(SGDX_ARGS)                                    \
    : chunk == 16 ? launch_sgd_xcd<RR, 16>(SGDX_ARGS)                                \

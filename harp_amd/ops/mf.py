@@ -65,9 +65,6 @@ def _rt():
 # variant 1 = one persistent launch per slice pass ordered by neighbour completion flags
 # (mf_sgd_xcd_flow_kernel) instead of one launch per sub-step; ranks <= 256
 FLOW_VARIANT = 1
-# variants 2 / 3: the per-sub-step kernel with H rows prefetched 4 / 3 ratings ahead
-# (csrc/mf_sgd.hip sgd_stream_lds_pd; 0 = 2 ahead)
-PD_VARIANTS = (2, 3)
 _FLOW_WS: dict = {}
 
 
@@ -213,8 +210,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
             _lib.check(st, "mf_sgd_xcd_flow")
         else:
             st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
-                                     _lib.ptr(win), r, nb, chunk, blocks_per_xcd, variant if variant in PD_VARIANTS else 0,
-                                     W.data_ptr(), W.stride(0),
+                                     _lib.ptr(win), r, nb, chunk, blocks_per_xcd, 0, W.data_ptr(), W.stride(0),
                                      H.data_ptr(), H.stride(0), float(lr), float(lam), _lib.stream_ptr(W.device))
             _lib.check(st, "mf_sgd_xcd")
         if win is not None:

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--layout", choices=("xcd", "flat"), default="xcd")
     ap.add_argument("--skew", type=float, default=2.0, help="item popularity skew (1 = uniform)")
     ap.add_argument("--blocks-per-xcd", type=int, default=128)
-    ap.add_argument("--variant", type=int, default=0, help="kernel variant: 0 (H prefetch 2 ahead), 1 (flow), 2 / 3 (prefetch 4 / 3 ahead)")
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant: 0 (per-sub-step launches), 1 (flow)")
     ap.add_argument("--slices", type=int, default=1,
                     help="H slices per rank (rotation slice steps per epoch; 1 as in bench.py, profiles/r3_sgd_slices)")
     a = ap.parse_args()
