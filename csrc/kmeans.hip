@@ -679,6 +679,162 @@ int launch_wide3(const void* X, long ldx, const void* Cm2, long N, int dp, int k
   return harp_launch_status();
 }
 
+// Both operands through LDS: the points' 64-feature slices ride LDS-DMA too (a stage's slice
+// of 32 G rows per wave is 1-KiB contiguous pieces, where per-lane 16-B register loads touch
+// 32 rows per instruction), fragments read conflict-free with the same rotation as the
+// centroid slices. G point groups per wave (4 waves), NBUF-deep LDS ring (stage f + NBUF - 1
+// is issued once stage f has landed: counted vmcnt waits, one barrier per stage).
+template <int G, int NBUF>
+__global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
+    int nkb, unsigned long long* __restrict__ keys) {
+  using C = KWCfg<G, 64>;
+  constexpr int KS = C::KS, CPR = C::CPR;
+  constexpr int XROWS = 4 * G * 32;                  // points per workgroup
+  constexpr int XBYTES = XROWS * 64 * 2;             // point slice per stage
+  constexpr int SBYTES = C::TILE_BYTES + XBYTES;     // one ring slot
+  constexpr int XDMA = XROWS * CPR / 64;             // 1-KiB pieces of the point slice
+  constexpr int OPS = C::DMA / 4 + XDMA / 4;         // DMA instructions per wave per stage
+  static_assert(C::DMA % 4 == 0 && XDMA % 4 == 0, "whole pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const long id = blockIdx.x;
+  const long xcd = id & 7, round = id >> 3;
+  const long pb = (round / nkb) * 8 + xcd;
+  const int kb = (int)(round % nkb);
+  const long npb = (N + XROWS - 1) / XROWS;
+  if (pb >= npb) return;
+  const int row0 = kb * KW_CB;
+  const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
+  const long p0 = pb * XROWS;  // first point of the workgroup
+  const long pbase = p0 + wave * (G * 32);
+  const int nst = dp / 64;
+  auto issue = [&](int f, int slot) {
+    char* buf = smem + slot * SBYTES;
+    stage_dma_wide<C>(Cm2, dp, row0, kp, f, buf, wave, lane);
+    char* xb = buf + C::TILE_BYTES;
+#pragma unroll
+    for (int j0 = 0; j0 < XDMA; j0 += 4) {
+      const int j = j0 + wave;
+      const int q = j * 64 + lane;
+      const int row = q / CPR;
+      int c = q - row * CPR - wide_rot<CPR>(row);
+      if (c < 0) c += CPR;
+      long pr = p0 + row;
+      if (pr > N - 1) pr = N - 1;
+      const __bf16* src = X + pr * ldx + f * 64 + c * 8;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)(xb + j * 1024), 16, 0, 0);
+    }
+  };
+  floatx16 acc[KW_RG][G];
+#pragma unroll
+  for (int a = 0; a < KW_RG; ++a)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
+  int aoff[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) aoff[k] = (r * CPR + (2 * k + h + wide_rot<CPR>(r)) % CPR) * 16;
+#pragma unroll
+  for (int q = 0; q < NBUF - 1; ++q)
+    if (q < nst) issue(q, q);
+  float xs[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) xs[g] = 0.f;
+  for (int f = 0; f < nst; ++f) {
+    // stage f landed when at most the younger stages' pieces are outstanding
+    const int younger = (nst - 1 - f) < (NBUF - 2) ? (nst - 1 - f) : (NBUF - 2);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (f + NBUF - 1 < nst) issue(f + NBUF - 1, (f + NBUF - 1) % NBUF);
+    const char* buf = smem + (f % NBUF) * SBYTES;
+    const char* xb = buf + C::TILE_BYTES + wave * (G * 32) * CPR * 16;
+    bf16x8 xf[G][KS];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) xf[g][k] = *(const bf16x8*)(xb + g * 32 * CPR * 16 + aoff[k]);
+    // |x|^2 from the staged fragments (VALU work under the stage's MFMAs)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xs[g] = fmaf((float)xf[g][k][j], (float)xf[g][k][j], xs[g]);
+    bf16x8 af[2][KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
+#pragma unroll
+    for (int rg = 0; rg < KW_RG; ++rg) {
+      if (rg + 1 < KW_RG) {
+        const char* nb = buf + (rg + 1) * 32 * CPR * 16;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
+      }
+      if (rg < live_rg) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int k = 0; k < KS; ++k)
+            acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[g][k], acc[rg][g], 0, 0, 0);
+      }
+    }
+  }
+  float xsg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) xsg[g] = xs[g] + __shfl_xor(xs[g], 32, 64) - (float)KM_ONES;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float best = KM_BIG;
+    int bestt = 0;
+#pragma unroll
+    for (int rg = 0; rg < KW_RG; ++rg) {
+      if (rg >= live_rg) break;
+      float m = keyed(acc[rg][g][0], 0u);
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
+      if (m < best) {
+        best = m;
+        bestt = rg;
+      }
+    }
+    const float ob = __shfl_xor(best, 32, 64);
+    const int obt = __shfl_xor(bestt, 32, 64);
+    const bool take = h ? (ob <= best) : (ob < best);
+    const float bv = take ? ob : best;
+    const int bt = take ? obt : bestt;
+    const int hw = take ? (1 - h) : h;
+    const unsigned reg = __float_as_uint(bv) & 0xFu;
+    const int idx = row0 + bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
+    const long p = pbase + g * 32 + r;
+    if (h == 0 && p < N) {
+      const float dist = fmaxf(bv + xsg[g], 0.f);
+      const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
+      __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int G, int NBUF>
+int launch_wide_lds(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
+                    unsigned long long* keys, hipStream_t s) {
+  constexpr int XROWS = 4 * G * 32;
+  constexpr int SBYTES = KW_CB * 64 * 2 + XROWS * 64 * 2;
+  if (dp % 64 || (ldx * 2) % 16) return HARP_EBADARG;
+  const long npb = (N + XROWS - 1) / XROWS;
+  const int nkb = (kswept + KW_CB - 1) / KW_CB;
+  const long rounds = (npb + 7) / 8 * nkb;
+  (void)SBYTES;
+  kmeans_assign_wide_lds_kernel<G, NBUF><<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
+  return harp_launch_status();
+}
+
 template <int G, int DC, int OCC>
 int launch_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                 unsigned long long* keys, hipStream_t s) {
@@ -785,6 +941,8 @@ HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2
     case 2: return launch_wide<2, 128, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 3: return launch_wide<1, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 4: return launch_wide3<2, 64>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 5: return launch_wide_lds<2, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 6: return launch_wide_lds<1, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     default: return HARP_EBADARG;
   }
 }

@@ -223,3 +223,25 @@ def test_kmeans_model_wide_d(cuda):
     res = run_kmeans(Communicator(None, cuda), cfg)
     obj = res["objective"]
     assert len(obj) == 3 and obj[2] <= obj[0]
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+def test_assign_wide_variants_agree(cuda, variant, monkeypatch):
+    """Every wide-row tiling gives the labels of the torch fp64 argmin (near-ties aside)."""
+    monkeypatch.setattr(K, "WIDE_VARIANT", variant)
+    torch.manual_seed(2)
+    n, d, k = 9000, 700, 600
+    x = torch.rand(n, d, device=cuda) * 1000
+    X = K.pack_points(x, cuda)
+    c = torch.rand(k, d, device=cuda) * 1000
+    op = K.prepare(c, X.shape[1])
+    lab, obj = K.assign(X, op)
+    c_bf = c.to(torch.bfloat16).float()
+    rlab, dist, rbest = _ref_assign(X, c_bf, d)
+    lab = lab.long()
+    chosen = dist.gather(1, lab[:, None])[:, 0]
+    best = dist.gather(1, rlab[:, None])[:, 0]
+    scale = (X[:, :d].double() ** 2).sum(1) + (c_bf.double() ** 2).sum(1).max()
+    assert bool(((chosen - best) <= 1e-5 * scale).all())
+    assert (lab == rlab).float().mean() > 0.99
+    assert abs(obj.item() - rbest.sum().item()) <= 1e-4 * abs(rbest.sum().item()) + 1e-3
