@@ -107,6 +107,50 @@ struct DocRow<unsigned short> {
   }
 };
 
+// packed uint8 counts (every doc shorter than 256 tokens, so no byte carries or borrows):
+// a token's doc-row read halves again (1 KB at K_pad = 1024)
+template <>
+struct DocRow<unsigned char> {
+  template <int TPL>
+  __device__ static __forceinline__ void load(const unsigned char* drow, int k0, int (&nd)[TPL]) {
+    static_assert(TPL % 4 == 0, "TPL must be a multiple of 4");
+    if constexpr (TPL % 16 == 0) {
+#pragma unroll
+      for (int t = 0; t < TPL; t += 16) {
+        const uint4 v = *(const uint4*)(drow + k0 + t);
+        const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) nd[t + 4 * q + b] = (int)((w[q] >> (8 * b)) & 0xFFu);
+      }
+    } else if constexpr (TPL % 8 == 0) {
+#pragma unroll
+      for (int t = 0; t < TPL; t += 8) {
+        const uint2 v = *(const uint2*)(drow + k0 + t);
+        const unsigned w[2] = {v.x, v.y};
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) nd[t + 4 * q + b] = (int)((w[q] >> (8 * b)) & 0xFFu);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TPL; t += 4) {
+        const unsigned w = *(const unsigned*)(drow + k0 + t);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) nd[t + b] = (int)((w >> (8 * b)) & 0xFFu);
+      }
+    }
+  }
+  __device__ static __forceinline__ void add(unsigned char* drow, int k, int v) {
+    unsigned* word = (unsigned*)(drow + (k & ~3));
+    const unsigned sh = (unsigned)(k & 3) * 8u;
+    if (v > 0) atomicAdd(word, (unsigned)v << sh);
+    else atomicSub(word, (unsigned)(-v) << sh);
+  }
+};
+
 // XW: extra waves per SIMD over the compiler's occupancy (a few VGPRs spill; more resident
 // waves hide the random doc-row fetch). A one-token-ahead doc-row prefetch measured slower
 // (0.90e9 vs 1.17e9 tokens/s at K = 1000, profiles/r1_lda/ldapf: its extra VGPRs cost a
@@ -549,7 +593,8 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
 }
 }  // namespace
 
-// ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8)
+// ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8); 8 -> packed
+// uint8 (every doc < 256 tokens; ldd multiple of 16)
 // variant: 0 = compiler occupancy, 3 = two more waves per SIMD (fewer VGPRs, some spilled)
 HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
                              void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
@@ -573,6 +618,11 @@ HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const l
     if (ldd % 8) return HARP_EBADARG;
     return variant == 3 ? launch_cgs<unsigned short, 2>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
                         : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
+  }
+  if (ndk_bits == 8) {
+    if (ldd % 16) return HARP_EBADARG;
+    return variant == 3 ? launch_cgs<unsigned char, 2>(CGS_ARGS, (unsigned char*)ndk, ldd, CGS_TAIL)
+                        : launch_cgs<unsigned char, 0>(CGS_ARGS, (unsigned char*)ndk, ldd, CGS_TAIL);
   }
 #undef CGS_ARGS
 #undef CGS_TAIL
@@ -654,6 +704,15 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
            : waves == 16 ? launch_sparse<16>(SP_ARGS, n16, ldd, SP_TAIL)
                          : launch_sparse<8>(SP_ARGS, n16, ldd, SP_TAIL);
   }
+  if (ndk_bits == 8) {
+    if (ldd % 4) return HARP_EBADARG;
+    unsigned char* n8 = (unsigned char*)ndk;
+    return waves == 1    ? launch_sparse<1>(SP_ARGS, n8, ldd, SP_TAIL)
+           : waves == 2  ? launch_sparse<2>(SP_ARGS, n8, ldd, SP_TAIL)
+           : waves == 4  ? launch_sparse<4>(SP_ARGS, n8, ldd, SP_TAIL)
+           : waves == 16 ? launch_sparse<16>(SP_ARGS, n8, ldd, SP_TAIL)
+                         : launch_sparse<8>(SP_ARGS, n8, ldd, SP_TAIL);
+  }
   if (ndk_bits != 32) return HARP_EBADARG;
   int* n32 = (int*)ndk;
   return waves == 1    ? launch_sparse<1>(SP_ARGS, n32, ldd, SP_TAIL)
@@ -675,6 +734,10 @@ HARP_EXPORT int harp_lda_count(const int* tdoc, const int* tword, const int* tz,
     lda_count_kernel<unsigned short><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(tdoc, tword, tz, n,
                                                                                   (unsigned short*)ndk, ldd, nwk, ldw,
                                                                                   nk);
+  } else if (ndk_bits == 8) {
+    if (ldd % 4) return HARP_EBADARG;
+    lda_count_kernel<unsigned char><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(tdoc, tword, tz, n,
+                                                                                 (unsigned char*)ndk, ldd, nwk, ldw, nk);
   } else {
     lda_count_kernel<int><<<dim3((unsigned)blocks), dim3(256), 0, s>>>(tdoc, tword, tz, n, (int*)ndk, ldd, nwk, ldw,
                                                                        nk);
