@@ -382,7 +382,7 @@ struct KWCfg {
 // walks r.
 template <int CPR>
 __device__ __forceinline__ int wide_rot(int row) {
-  return CPR == 8 ? (row >> 1) & 7 : CPR == 16 ? row & 15 : (row >> 3) & 1;
+  return CPR == 4 ? (row >> 2) & 3 : CPR == 8 ? (row >> 1) & 7 : CPR == 16 ? row & 15 : (row >> 3) & 1;
 }
 
 template <class C>
@@ -684,14 +684,14 @@ int launch_wide3(const void* X, long ldx, const void* Cm2, long N, int dp, int k
 // 32 rows per instruction), fragments read conflict-free with the same rotation as the
 // centroid slices. G point groups per wave (4 waves), NBUF-deep LDS ring (stage f + NBUF - 1
 // is issued once stage f has landed: counted vmcnt waits, one barrier per stage).
-template <int G, int NBUF>
+template <int G, int DC, int NBUF>
 __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
     const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
     int nkb, unsigned long long* __restrict__ keys) {
-  using C = KWCfg<G, 64>;
+  using C = KWCfg<G, DC>;
   constexpr int KS = C::KS, CPR = C::CPR;
   constexpr int XROWS = 4 * G * 32;                  // points per workgroup
-  constexpr int XBYTES = XROWS * 64 * 2;             // point slice per stage
+  constexpr int XBYTES = XROWS * DC * 2;             // point slice per stage
   constexpr int SBYTES = C::TILE_BYTES + XBYTES;     // one ring slot
   constexpr int XDMA = XROWS * CPR / 64;             // 1-KiB pieces of the point slice
   constexpr int OPS = C::DMA / 4 + XDMA / 4;         // DMA instructions per wave per stage
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
   const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
   const long p0 = pb * XROWS;  // first point of the workgroup
   const long pbase = p0 + wave * (G * 32);
-  const int nst = dp / 64;
+  const int nst = dp / DC;
   auto issue = [&](int f, int slot) {
     char* buf = smem + slot * SBYTES;
     stage_dma_wide<C>(Cm2, dp, row0, kp, f, buf, wave, lane);
@@ -723,7 +723,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
       if (c < 0) c += CPR;
       long pr = p0 + row;
       if (pr > N - 1) pr = N - 1;
-      const __bf16* src = X + pr * ldx + f * 64 + c * 8;
+      const __bf16* src = X + pr * ldx + f * DC + c * 8;
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                        (void __attribute__((address_space(3)))*)(xb + j * 1024), 16, 0, 0);
     }
@@ -820,17 +820,17 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
   }
 }
 
-template <int G, int NBUF>
+template <int G, int DC, int NBUF>
 int launch_wide_lds(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                     unsigned long long* keys, hipStream_t s) {
   constexpr int XROWS = 4 * G * 32;
-  constexpr int SBYTES = KW_CB * 64 * 2 + XROWS * 64 * 2;
-  if (dp % 64 || (ldx * 2) % 16) return HARP_EBADARG;
+  constexpr int SBYTES = KW_CB * DC * 2 + XROWS * DC * 2;
+  if (dp % DC || (ldx * 2) % 16) return HARP_EBADARG;
   const long npb = (N + XROWS - 1) / XROWS;
   const int nkb = (kswept + KW_CB - 1) / KW_CB;
   const long rounds = (npb + 7) / 8 * nkb;
   (void)SBYTES;
-  kmeans_assign_wide_lds_kernel<G, NBUF><<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
+  kmeans_assign_wide_lds_kernel<G, DC, NBUF><<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
       (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
   return harp_launch_status();
 }
@@ -941,8 +941,10 @@ HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2
     case 2: return launch_wide<2, 128, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 3: return launch_wide<1, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 4: return launch_wide3<2, 64>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 5: return launch_wide_lds<2, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 6: return launch_wide_lds<1, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 5: return launch_wide_lds<2, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 6: return launch_wide_lds<1, 64, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 7: return launch_wide_lds<2, 32, 4>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 8: return launch_wide_lds<2, 32, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     default: return HARP_EBADARG;
   }
 }
