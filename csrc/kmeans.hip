@@ -820,6 +820,166 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
   }
 }
 
+// Persistent form of the LDS-staged tiling (G = 2, 64-feature stages, 2-deep ring): one
+// workgroup per CU walks its XCD's (point block, centroid block) tiles -- workgroup j of XCD
+// x takes tiles j, j + W, j + 2W, ... of x's tile list (point blocks x, x + 8, ...; centroid
+// blocks minor), so the workgroups resident on an XCD still share their point rows in L2 --
+// and the stage stream runs across tile boundaries: the next tile's first stage is in flight
+// while a tile's argmin epilogue and atomics run (no per-tile launch, prologue or drain).
+__global__ __launch_bounds__(256, 1) void kmeans_assign_wide_persist_kernel(
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
+    int nkb, unsigned long long* __restrict__ keys) {
+  constexpr int G = 2, DC = 64;
+  using C = KWCfg<G, DC>;
+  constexpr int KS = C::KS, CPR = C::CPR;
+  constexpr int XROWS = 4 * G * 32;
+  constexpr int XBYTES = XROWS * DC * 2;
+  constexpr int SBYTES = C::TILE_BYTES + XBYTES;
+  constexpr int XDMA = XROWS * CPR / 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int xcd = (int)(blockIdx.x & 7);
+  const int wpx = (int)(gridDim.x >> 3);      // workgroups per XCD
+  const int j = (int)(blockIdx.x >> 3);
+  const long npb = (N + XROWS - 1) / XROWS;
+  const long npb_x = npb > xcd ? (npb - xcd + 7) / 8 : 0;  // point blocks of this XCD
+  const long ntile_x = npb_x * nkb;
+  const long nmine = ntile_x > j ? (ntile_x - j + wpx - 1) / wpx : 0;
+  const int nst = dp / DC;
+  if (nmine == 0) return;
+  auto tile_of = [&](long t, long& p0, int& row0) {  // t-th tile of this workgroup
+    const long q = j + t * wpx;  // index in the XCD's tile list
+    p0 = ((q / nkb) * 8 + xcd) * XROWS;
+    row0 = (int)(q % nkb) * KW_CB;
+  };
+  auto issue = [&](long p0, int row0, int f, int slot) {
+    char* buf = smem + slot * SBYTES;
+    stage_dma_wide<C>(Cm2, dp, row0, kp, f, buf, wave, lane);
+    char* xb = buf + C::TILE_BYTES;
+#pragma unroll
+    for (int j0 = 0; j0 < XDMA; j0 += 4) {
+      const int jj = j0 + wave;
+      const int q = jj * 64 + lane;
+      const int row = q / CPR;
+      int c = q - row * CPR - wide_rot<CPR>(row);
+      if (c < 0) c += CPR;
+      long pr = p0 + row;
+      if (pr > N - 1) pr = N - 1;
+      const __bf16* src = X + pr * ldx + f * DC + c * 8;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)(xb + jj * 1024), 16, 0, 0);
+    }
+  };
+  floatx16 acc[KW_RG][G];
+  int aoff[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) aoff[k] = (r * CPR + (2 * k + h + wide_rot<CPR>(r)) % CPR) * 16;
+  long p0, np0;
+  int row0, nrow0;
+  tile_of(0, p0, row0);
+  issue(p0, row0, 0, 0);
+  int slot = 0;
+  for (long t = 0; t < nmine; ++t) {
+    const bool more = t + 1 < nmine;
+    if (more) tile_of(t + 1, np0, nrow0);
+    const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
+#pragma unroll
+    for (int a = 0; a < KW_RG; ++a)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
+    float xs[G] = {0.f, 0.f};
+    for (int f = 0; f < nst; ++f) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      // the next stage: this tile's, or the next tile's first (in flight under the epilogue)
+      if (f + 1 < nst) issue(p0, row0, f + 1, slot ^ 1);
+      else if (more) issue(np0, nrow0, 0, slot ^ 1);
+      const char* buf = smem + slot * SBYTES;
+      const char* xb = buf + C::TILE_BYTES + wave * (G * 32) * CPR * 16;
+      bf16x8 xf[G][KS];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) xf[g][k] = *(const bf16x8*)(xb + g * 32 * CPR * 16 + aoff[k]);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xs[g] = fmaf((float)xf[g][k][e], (float)xf[g][k][e], xs[g]);
+      bf16x8 af[2][KS];
+#pragma unroll
+      for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
+#pragma unroll
+      for (int rg = 0; rg < KW_RG; ++rg) {
+        if (rg + 1 < KW_RG) {
+          const char* nb = buf + (rg + 1) * 32 * CPR * 16;
+#pragma unroll
+          for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
+        }
+        if (rg < live_rg) {
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < KS; ++k)
+              acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[g][k], acc[rg][g], 0, 0, 0);
+        }
+      }
+      slot ^= 1;
+    }
+    // tile epilogue: keyed argmin over the block's 256 candidates, one 64-bit atomic per point
+    const long pbase = p0 + wave * (G * 32);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float xsg = xs[g] + __shfl_xor(xs[g], 32, 64) - (float)KM_ONES;
+      float best = KM_BIG;
+      int bestt = 0;
+#pragma unroll
+      for (int rg = 0; rg < KW_RG; ++rg) {
+        if (rg >= live_rg) break;
+        float m = keyed(acc[rg][g][0], 0u);
+#pragma unroll
+        for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
+        if (m < best) {
+          best = m;
+          bestt = rg;
+        }
+      }
+      const float ob = __shfl_xor(best, 32, 64);
+      const int obt = __shfl_xor(bestt, 32, 64);
+      const bool take = h ? (ob <= best) : (ob < best);
+      const float bv = take ? ob : best;
+      const int bt = take ? obt : bestt;
+      const int hw = take ? (1 - h) : h;
+      const unsigned reg = __float_as_uint(bv) & 0xFu;
+      const int idx = row0 + bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
+      const long p = pbase + g * 32 + r;
+      if (h == 0 && p < N) {
+        const float dist = fmaxf(bv + xsg, 0.f);
+        const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
+        __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    p0 = np0;
+    row0 = nrow0;
+  }
+}
+
+int launch_wide_persist(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
+                        unsigned long long* keys, hipStream_t s) {
+  if (dp % 64 || (ldx * 2) % 16) return HARP_EBADARG;
+  const int nkb = (kswept + KW_CB - 1) / KW_CB;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int wpx = cus / 8 > 0 ? cus / 8 : 1;  // one resident workgroup per CU (LDS + registers)
+  kmeans_assign_wide_persist_kernel<<<dim3((unsigned)(wpx * 8)), dim3(256), 0, s>>>(
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
+  return harp_launch_status();
+}
+
 template <int G, int DC, int NBUF>
 int launch_wide_lds(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                     unsigned long long* keys, hipStream_t s) {
@@ -945,6 +1105,7 @@ HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2
     case 6: return launch_wide_lds<1, 64, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 7: return launch_wide_lds<2, 32, 4>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 8: return launch_wide_lds<2, 32, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 9: return launch_wide_persist(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     default: return HARP_EBADARG;
   }
 }
