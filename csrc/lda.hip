@@ -151,6 +151,23 @@ struct DocRow<unsigned char> {
   }
 };
 
+// Fused parameter-server rows (push-pull with sparse rows, models/lda.py): the word rows
+// are read straight from the PULL payload (slot of local row w at pull_off[w], capacity
+// pull_cap[w]; parallel/sparse_ps.py layout, csrc/rowcodec.hip slot format) into the wave's
+// LDS row, and a chunk's word-row delta is written straight into the PUSH payload slot
+// (dense slot: atomic adds; sparse slot: one reservation per wave on the slot's nnz word,
+// entries of several chunks of one word may repeat a topic -- the owner's decode_add sums
+// them). No dense local table is materialised, decoded or re-encoded.
+struct PsRows {
+  const unsigned char* pbuf;
+  const long* poff;
+  const int* pcap;
+  unsigned char* qbuf;
+  const long* qoff;
+  const int* qcap;
+  int* overflow;
+};
+
 // XW: extra waves per SIMD over the compiler's occupancy (a few VGPRs spill; more resident
 // waves hide the random doc-row fetch). A one-token-ahead doc-row prefetch measured slower
 // (0.90e9 vs 1.17e9 tokens/s at K = 1000, profiles/r1_lda/ldapf: its extra VGPRs cost a
@@ -160,7 +177,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
-    unsigned long long seed, int det) {
+    unsigned long long seed, int det, PsRows ps) {
   constexpr int KP = 64 * TPL;
   constexpr int WAVES = 4;
   __shared__ float s_inv[KP];
@@ -188,11 +205,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     // topic, p_t = (n_dt + alpha) * qw_t, and only the two topics a token moves have
     // their qw refreshed
     float nwf[TPL], qw[TPL];
+    if (ps.pbuf) {
+      // the word row from its pull slot into this wave's LDS row (zero, then scatter)
+      int* lrow = &s_nw0[wv][0];
+      const unsigned char* slot = ps.pbuf + ps.poff[w];
+      const int cap = ps.pcap[w];
 #pragma unroll
-    for (int t = 0; t < TPL; t += 4) {
-      const int4 v = *(const int4*)(wrow + t);
-      *(int4*)(nw0s + t) = v;
-      nwf[t] = (float)v.x; nwf[t + 1] = (float)v.y; nwf[t + 2] = (float)v.z; nwf[t + 3] = (float)v.w;
+      for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (cap < 0) {
+        const int4* s4 = (const int4*)slot;
+        for (int q = lane; q < K / 4; q += 64) ((int4*)lrow)[q] = s4[q];
+      } else {
+        int nnz = *(const int*)slot;
+        nnz = nnz < 0 ? 0 : (nnz > cap ? cap : nnz);
+        const int* cnt = (const int*)(slot + 4);
+        const unsigned short* top = (const unsigned short*)(slot + 4 + 4 * (long)cap);
+        for (int e = lane; e < nnz; e += 64) {
+          const int t = top[e];
+          if (t < K) lrow[t] = cnt[e];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int t = 0; t < TPL; t += 4) {
+        const int4 v = *(const int4*)(nw0s + t);
+        nwf[t] = (float)v.x; nwf[t + 1] = (float)v.y; nwf[t + 2] = (float)v.z; nwf[t + 3] = (float)v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TPL; t += 4) {
+        const int4 v = *(const int4*)(wrow + t);
+        *(int4*)(nw0s + t) = v;
+        nwf[t] = (float)v.x; nwf[t + 1] = (float)v.y; nwf[t + 2] = (float)v.z; nwf[t + 3] = (float)v.w;
+      }
     }
 #pragma unroll
     for (int t = 0; t < TPL; ++t) qw[t] = (nwf[t] + beta) * s_inv[k0 + t];
@@ -273,10 +323,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
       }
     }
     // flush this chunk's word-row delta
+    if (ps.qbuf) {
+      unsigned char* slot = ps.qbuf + ps.qoff[w];
+      const int cap = ps.qcap[w];
+      if (cap < 0) {
 #pragma unroll
-    for (int t = 0; t < TPL; ++t) {
-      const int dlt = (int)nwf[t] - nw0s[t];
-      if (dlt) atomicAdd(wrow + t, dlt);
+        for (int t = 0; t < TPL; ++t) {
+          const int dlt = (int)nwf[t] - nw0s[t];
+          if (dlt) atomicAdd((int*)slot + k0 + t, dlt);
+        }
+      } else {
+        int mine = 0;
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) mine += ((int)nwf[t] != nw0s[t]) ? 1 : 0;
+        const float incl = wave_incl_scan((float)mine, lane);
+        const int tot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+        int base = 0;
+        if (tot) {
+          if (lane == 0) base = atomicAdd((int*)slot, tot);
+          base = __builtin_amdgcn_readfirstlane(base);
+        }
+        int pos = base + (int)incl - mine;
+        int* cnt = (int*)(slot + 4);
+        unsigned short* top = (unsigned short*)(slot + 4 + 4 * (long)cap);
+        bool over = false;
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) {
+          const int dlt = (int)nwf[t] - nw0s[t];
+          if (dlt) {
+            if (pos < cap) {
+              cnt[pos] = dlt;
+              top[pos] = (unsigned short)(k0 + t);
+            } else {
+              over = true;
+            }
+            ++pos;
+          }
+        }
+        if (__ballot(over) && lane == 0) ps.overflow[0] = 1;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TPL; ++t) {
+        const int dlt = (int)nwf[t] - nw0s[t];
+        if (dlt) atomicAdd(wrow + t, dlt);
+      }
     }
   }
   __syncthreads();
@@ -571,7 +662,7 @@ namespace {
 template <class DT, int XW = 0>
 int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
                int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
-               unsigned long long seed, int det, hipStream_t s) {
+               unsigned long long seed, int det, PsRows ps, hipStream_t s) {
   long blocks = (nchunks + 3) / 4;  // 4 waves per block
   if (blocks > 8192) blocks = 8192;
   if (det) blocks = 1;
@@ -579,15 +670,15 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
     lda_cgs_kernel<4, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                           nk_delta, K, alpha, beta, seed, det);
+                                           nk_delta, K, alpha, beta, seed, det, ps);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
     lda_cgs_kernel<8, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                           nk_delta, K, alpha, beta, seed, det);
+                                           nk_delta, K, alpha, beta, seed, det, ps);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
     lda_cgs_kernel<16, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                            nk_delta, K, alpha, beta, seed, det);
+                                            nk_delta, K, alpha, beta, seed, det, ps);
   }
   return harp_launch_status();
 }
@@ -596,9 +687,35 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
 // ndk_bits: 32 -> int32 doc-topic counts; 16 -> packed uint16 (ldd multiple of 8); 8 -> packed
 // uint8 (every doc < 256 tokens; ldd multiple of 16)
 // variant: 0 = compiler occupancy, 3 = two more waves per SIMD (fewer VGPRs, some spilled)
+static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, void* ndk,
+                        int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
+                        float beta, unsigned long long seed, int variant, PsRows ps, hipStream_t s);
+
 HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
                              void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
                              int K, float alpha, float beta, unsigned long long seed, int variant, hipStream_t s) {
+  const PsRows none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  return lda_cgs_impl(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, ndk_bits, nwk, ldw, inv_nk, nk_delta, K, alpha,
+                      beta, seed, variant, none, s);
+}
+
+// The dense sampler on fused parameter-server rows (PsRows above): pull payload slots in,
+// push payload slots out (zeroed by the caller); nwk / ldw are unused.
+HARP_EXPORT int harp_lda_cgs_ps(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
+                                void* ndk, int ldd, int ndk_bits, const float* inv_nk, int* nk_delta, int K,
+                                float alpha, float beta, unsigned long long seed, int variant,
+                                const unsigned char* pbuf, const long* poff, const int* pcap, unsigned char* qbuf,
+                                const long* qoff, const int* qcap, int* overflow, hipStream_t s) {
+  if (!pbuf || !poff || !pcap || !qbuf || !qoff || !qcap || !overflow) return HARP_EBADARG;
+  const PsRows ps{pbuf, poff, pcap, qbuf, qoff, qcap, overflow};
+  int kp = K <= 256 ? 256 : K <= 512 ? 512 : 1024;
+  return lda_cgs_impl(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, ndk_bits, nullptr, kp, inv_nk, nk_delta, K,
+                      alpha, beta, seed, variant, ps, s);
+}
+
+static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, void* ndk,
+                        int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
+                        float beta, unsigned long long seed, int variant, PsRows ps, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
   // variant 0: compiler occupancy; 3: two more waves per SIMD (the default). The doc-row
   // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
@@ -608,7 +725,7 @@ HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const l
   variant &= 0xff;
   if (K <= 0 || K > 1024 || ldw % 4 || (variant != 0 && variant != 3)) return HARP_EBADARG;
 #define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks
-#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, s
+#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, ps, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
     return variant == 3 ? launch_cgs<int, 2>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)

@@ -52,6 +52,8 @@ class LDAConfig:
     min_bound: int = 0        # with a budget: retune it every iteration so the trained percentage lands
     max_bound: int = 0        # in [min_bound, max_bound] (dymoro.BudgetTuner); 0 / 0: the budget stays fixed
     deterministic: bool = False  # GPU: one wave samples in order (bit-reproducible; tests / debugging only)
+    fused_rows: bool = True   # push-pull over sparse rows, GPU dense sampler: sample straight from the pull
+                              # payload into the push payload (no dense local table, no decode / re-encode)
 
 
 def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, seed: int = 0, device="cpu"):
@@ -453,6 +455,13 @@ class LDAPushPullMapper(LDACollectiveMapper):
             self.glob.static_layout = True
             self.before = self.want_pt = None
             self.ps.push(self.pull_buf, self._glob_rows(), delta=False)  # initial counts into an empty model
+            # fused rows: the dense sampler reads the pull payload and writes the push payload
+            # itself, so the dense local table is only the initial-count source
+            self.fused = (cfg.fused_rows and not self.sparse and K <= 1024 and dev.type == "cuda"
+                          and L._lib.use_native(self.tz))
+            if self.fused:
+                self.slots = self.ps.row_slots()
+                self.pull_buf = None
         else:
             # one persistent buffer of the blocks this worker's tokens touch: pulled into,
             # sampled on in place, turned into the count delta and pushed back (cached plans)
@@ -540,6 +549,20 @@ class LDAPushPullMapper(LDACollectiveMapper):
                                  self.nk, cfg.num_topics, cfg.alpha, cfg.beta, self.vbeta, seed, self.doc_index, deterministic=cfg.deterministic)
                 self.nk += d
             return n
+        if self.ps is not None and getattr(self, "fused", False):
+            pull_b, push_b = self.ps.bytes_per_call(remote_only=True)
+            self._timed_ps("pull", lambda: self.ps.pull_payload(self._glob_rows()), pull_b)
+            pbuf, qbuf = self.ps.pull_recv.buf, self.ps.push_payload_buffer()
+            n = self.tz.numel()
+            d = (L.cgs_sample_ps(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, self.nk, cfg.num_topics,
+                                 cfg.alpha, cfg.beta, self.vbeta, seed, pbuf, qbuf, self.slots, self.ps.overflow,
+                                 deterministic=cfg.deterministic)
+                 if n else torch.zeros(self.Kp, dtype=torch.int32, device=self.device))
+            self._timed_ps("push", lambda: self.ps.push_payload(self._glob_rows()), push_b)
+            if self.get_num_workers() > 1:
+                d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
+            self.nk += d
+            return n
         if self.ps is not None:
             pull_b, push_b = self.ps.bytes_per_call(remote_only=True)
             self._timed_ps("pull", lambda: self.ps.pull(self._glob_rows(), self.pull_buf), pull_b)
@@ -621,7 +644,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
                 self.loglik.append((it + 1, self.log_likelihood(it)))
             self._after_iteration(it)
         self.result = {"loglik": self.loglik, "iter_s": self.iter_times, "start_iteration": start,
-                       "local_server": self.local_server, "comm_mode": self.comm_mode}
+                       "local_server": self.local_server, "comm_mode": self.comm_mode,
+                       "fused_rows": bool(getattr(self, "fused", False))}
 
     def _state_tables(self, it: int) -> dict:
         from ..utils.checkpoint import blob_table, tensor_table

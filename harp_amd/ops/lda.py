@@ -17,6 +17,11 @@ _lib.register({
     "harp_lda_cgs_sparse": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 6 + [
         _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
         _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
+    # tdoc, tword, tz, chunks, nchunks, ndk, ldd, ndk_bits, inv_nk, nk_delta, K, alpha, beta, seed, variant,
+    # pull buf / off / cap, push buf / off / cap, overflow, stream
+    "harp_lda_cgs_ps": [_lib.c_void_p] * 4 + [_lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p,
+                                              _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_ulonglong,
+                                              _lib.c_int] + [_lib.c_void_p] * 8,
     "harp_lda_count": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_int,
                        _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
 })
@@ -221,6 +226,30 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
     if doc_index is not None:
         doc_index.sync(tz, tpos)
     return work - nk
+
+
+def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: float, vbeta: float, seed: int,
+                  pull_buf, push_buf, slots, overflow, deterministic: bool = False) -> torch.Tensor:
+    """:func:`cgs_sample` (dense sampler, GPU) with the word rows read from the pull
+    payload and the word-row deltas written into the (zeroed) push payload -- no dense
+    local table (``parallel.sparse_ps.SparseRowPS.row_slots`` gives ``slots``). Returns
+    the topic-count delta."""
+    dev = tz.device
+    Kp = ndk.shape[1]
+    if not _lib.use_native(tz) or K > 1024:
+        raise ValueError("fused push-pull rows need the GPU dense sampler (K <= 1024)")
+    poff, pcap, qoff, qcap = slots
+    inv = torch.zeros(Kp, dtype=torch.float32, device=dev)
+    inv[:K] = 1.0 / (nk[:K].float() + vbeta)
+    delta = torch.zeros(Kp, dtype=torch.int32, device=dev)
+    st = _lib.kernels().harp_lda_cgs_ps(
+        tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(), chunks.numel() - 1, ndk.data_ptr(),
+        ndk.stride(0), _bits(ndk), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
+        seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0), pull_buf.data_ptr(),
+        poff.data_ptr(), pcap.data_ptr(), push_buf.data_ptr(), qoff.data_ptr(), qcap.data_ptr(), overflow.data_ptr(),
+        _lib.stream_ptr(dev))
+    _lib.check(st, "lda_cgs_ps")
+    return delta
 
 
 def loglik_terms(counts: torch.Tensor, prior: float, K: int) -> torch.Tensor:

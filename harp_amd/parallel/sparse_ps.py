@@ -156,6 +156,49 @@ class SparseRowPS:
         self._exchange(s, r)
         RC.decode(glob_rows, self.K, r.rows, r.off, r.cap, r.buf, add=True)
 
+    # -- fused rows (the sampler reads pull slots and writes push slots itself) -----------
+    def row_slots(self):
+        """Per LOCAL row: (pull slot offset, pull cap, push slot offset, push cap) device
+        arrays, for kernels that read rows straight from the pull payload and write their
+        deltas straight into the push payload (csrc/lda.hip ``harp_lda_cgs_ps``). Every
+        local row has one owner, so it has exactly one slot per direction."""
+        if getattr(self, "_row_slots", None) is None:
+            n, dev = self.n_rows, self.device
+
+            def inv(side):
+                off = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+                cap = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+                if side.rows.numel():
+                    r = side.rows.long()
+                    off[r] = side.off
+                    cap[r] = side.cap
+                return off, cap
+
+            self._row_slots = inv(self.pull_recv) + inv(self.push_send)
+        return self._row_slots
+
+    def pull_payload(self, glob_rows: torch.Tensor) -> torch.Tensor:
+        """The pull without its decode: owners encode, one all-to-all; returns the received
+        payload (slots per :meth:`row_slots`)."""
+        s, r = self.pull_send, self.pull_recv
+        RC.encode(glob_rows, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
+        self._exchange(s, r)
+        self._pulled = True
+        return r.buf
+
+    def push_payload_buffer(self) -> torch.Tensor:
+        """The push payload, zeroed (empty sparse slots, zero dense slots) for a kernel to fill."""
+        buf = self.push_send.buf
+        buf[:self.push_send.nbytes].zero_()
+        return buf
+
+    def push_payload(self, glob_rows: torch.Tensor) -> None:
+        """The push of a payload a kernel filled (:meth:`push_payload_buffer`): one
+        all-to-all, owners add the slots (repeated topics in a slot add up)."""
+        s, r = self.push_send, self.push_recv
+        self._exchange(s, r)
+        RC.decode(glob_rows, self.K, r.rows, r.off, r.cap, r.buf, add=True)
+
     def check_overflow(self) -> None:
         if int(self.overflow.item()):
             raise RuntimeError("sparse push/pull overflow: a row held more nonzeros than its token bound")

@@ -66,17 +66,25 @@ def main():
     comm.barrier()
     dt = time.perf_counter() - t0
     ll = m.log_likelihood(a.warmup + a.iters)
-    extra = {"comm_mode": getattr(m, "comm_mode", "rotation")}
+    extra = {"comm_mode": getattr(m, "comm_mode", "rotation"), "fused_rows": bool(getattr(m, "fused", False))}
     if getattr(m, "ps", None) is not None:  # sparse push/pull: codec + exchange time per call
         ps = m.ps
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         reps = 10
+        fused = getattr(m, "fused", False)
         ev[0].record()
         for _ in range(reps):
-            ps.pull(m._glob_rows(), m.pull_buf)
+            if fused:
+                ps.pull_payload(m._glob_rows())
+            else:
+                ps.pull(m._glob_rows(), m.pull_buf)
         ev[1].record()
         for _ in range(reps):
-            ps.push(m.pull_buf, m._glob_rows())  # zero deltas: same payload work as a real push
+            if fused:
+                ps.push_payload_buffer()
+                ps.push_payload(m._glob_rows())  # empty deltas
+            else:
+                ps.push(m.pull_buf, m._glob_rows())  # zero deltas: same payload work as a real push
         ev[2].record()
         ev[2].synchronize()
         pb, qb = ps.bytes_per_call(remote_only=False)

@@ -60,13 +60,13 @@ def test_rowcodec_overflow_flag_gpu(cuda):
     assert int(ov.item()) == 1
 
 
-def _lda_pp(cuda, toks, mode, local, seed, det):
+def _lda_pp(cuda, toks, mode, local, seed, det, fused=True):
     from harp_amd.models.lda import LDAConfig, LDAPushPullMapper
     from harp_amd.parallel.comm import Communicator
     from harp_amd.runtime.mapper import KeyValReader
 
     cfg = LDAConfig(num_topics=64, alpha=0.1, beta=0.01, iterations=12, print_interval=6, block_words=512,
-                    sparse_comm=mode, local_server=local, seed=seed, deterministic=det)
+                    sparse_comm=mode, local_server=local, seed=seed, deterministic=det, fused_rows=fused)
     m = LDAPushPullMapper(Communicator(device=cuda), cfg, 3000, 4000, toks)
     m.run(KeyValReader([]))
     return m
@@ -77,7 +77,8 @@ def test_lda_push_pull_sparse_rows_gpu(cuda):
     must carry the SAME model: (1) the exact invariant -- the word-topic counts rebuilt
     from the final (word, z) equal the server table bit for bit, and the topic sums equal
     its column sums -- under the production (racing) sampler, for every layout and seed;
-    (2) with the one-wave deterministic sampler the three layouts take bit-identical
+    (2) with the one-wave deterministic sampler the layouts (and the fused rows mode, which
+    samples straight from the pull payload into the push payload) take bit-identical
     trajectories (the sampler's random stream is keyed by token index, and token order /
     chunking / initial z do not depend on the row layout). The production sampler's
     doc-row races make same-seed runs differ by as much as different seeds (measured:
@@ -88,16 +89,17 @@ def test_lda_push_pull_sparse_rows_gpu(cuda):
     toks = synthetic_corpus(3000, 4000, 20, 50, seed=2)
     n = toks[0].numel()
     for seed in range(2):
-        for mode, local in (("off", False), ("on", False), ("off", True)):
-            m = _lda_pp(cuda, toks, mode, local, seed, det=False)
+        for mode, local, fused in (("off", False, True), ("on", False, True), ("on", False, False), ("off", True, True)):
+            m = _lda_pp(cuda, toks, mode, local, seed, det=False, fused=fused)
             assert m.comm_mode == {("off", False): "dense", ("on", False): "sparse", ("off", True): "local"}[(mode, local)]
+            assert m.result["fused_rows"] == (mode == "on" and fused)
             assert m.check_counts(), (mode, local, seed)
             assert int(m.nk.sum()) == n
             ll = [v for _, v in m.result["loglik"]]
             assert ll[-1] > ll[0]
     ref = None
-    for mode, local in (("off", False), ("on", False), ("off", True)):
-        m = _lda_pp(cuda, toks, mode, local, 3, det=True)
+    for mode, local, fused in (("off", False, True), ("on", False, True), ("on", False, False), ("off", True, True)):
+        m = _lda_pp(cuda, toks, mode, local, 3, det=True, fused=fused)
         assert m.check_counts()
         got = (m.tz.cpu(), m.ndk.cpu(), [v for _, v in m.result["loglik"]])
         if ref is None:
