@@ -1,0 +1,37 @@
+"""LDA push-pull over sparse rows with TWO ranks on one GPU (gloo ranks stage their
+all-to-alls through the host, parallel/comm.py): the fused-rows mode (the sampler reads
+the pull payload and writes the push payload) against the decode / re-encode mode, in the
+deterministic one-wave sampler: identical token topics on every rank, and the exact
+count-rebuild invariant across ranks."""
+import pytest
+import torch
+
+from harp_amd.runtime.launcher import launch
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(comm, fused):
+    from harp_amd.models.lda import LDAConfig, LDAPushPullMapper, synthetic_corpus
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    dev = torch.device("cuda", 0)
+    gcomm = Communicator(None, dev)
+    toks = synthetic_corpus(2000, 3000, 20, 40, seed=5)
+    cfg = LDAConfig(num_topics=64, alpha=0.1, beta=0.01, iterations=6, print_interval=3, block_words=256,
+                    sparse_comm="on", local_server=False, seed=1, deterministic=True, fused_rows=fused)
+    m = LDAPushPullMapper(gcomm, cfg, 2000, 3000, toks)
+    m.run(KeyValReader([]))
+    ok = m.check_counts()
+    return {"tz": m.tz.cpu(), "ok": ok, "fused": m.result["fused_rows"], "ll": [v for _, v in m.result["loglik"]]}
+
+
+def test_fused_rows_two_ranks_match_unfused(cuda):
+    a = launch(_worker, 2, args=(True,), timeout=300)
+    b = launch(_worker, 2, args=(False,), timeout=300)
+    for ra, rb in zip(a, b):
+        assert ra["fused"] and not rb["fused"]
+        assert ra["ok"] and rb["ok"]
+        assert torch.equal(ra["tz"], rb["tz"])
+        assert ra["ll"] == rb["ll"]
