@@ -536,154 +536,6 @@ __global__ __launch_bounds__(256, OCC) void kmeans_assign_wide_kernel(
   }
 }
 
-// The same tile with a 3-deep pipeline: stage f + 2's centroid slice (LDS-DMA) and point
-// slices (registers) are issued once stage f's have landed, so two stages of loads are in
-// flight under each stage's MFMAs (counted vmcnt waits, one barrier per stage).
-template <int G, int DC>
-__global__ __launch_bounds__(256, 1) void kmeans_assign_wide3_kernel(
-    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
-    int nkb, unsigned long long* __restrict__ keys) {
-  using C = KWCfg<G, DC>;
-  constexpr int KS = C::KS;
-  constexpr int OPS = C::DMA / 4 + G * KS;  // vector-memory instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[3 * C::TILE_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int srot = (r >> 3) & 1;
-  const long id = blockIdx.x;
-  const long xcd = id & 7, round = id >> 3;
-  const long pb = (round / nkb) * 8 + xcd;
-  const int kb = (int)(round % nkb);
-  const long npb = (N + C::PTS - 1) / C::PTS;
-  if (pb >= npb) return;
-  const int row0 = kb * KW_CB;
-  const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
-  const long pbase = pb * C::PTS + wave * (G * 32);
-  const int nst = dp / DC;
-  const bf16x8* xrow[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    long p = pbase + g * 32 + r;
-    if (p > N - 1) p = N - 1;
-    xrow[g] = (const bf16x8*)(X + p * ldx);
-  }
-  bf16x8 xf[3][G][KS];
-  floatx16 acc[KW_RG][G];
-#pragma unroll
-  for (int a = 0; a < KW_RG; ++a)
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
-  int aoff[KS];
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int cp = (2 * k + h + wide_rot<C::CPR>(r)) % C::CPR;
-    aoff[k] = (r * C::CPR + cp) * 16;
-  }
-  auto issue = [&](int f, auto btag) {
-    constexpr int b = decltype(btag)::value;
-    stage_dma_wide<C>(Cm2, dp, row0, kp, f, smem + b * C::TILE_BYTES, wave, lane);
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int k = 0; k < KS; ++k) xf[b][g][k] = xrow[g][f * C::CPR + 2 * k + h];
-  };
-  issue(0, std::integral_constant<int, 0>{});
-  if (nst > 1) issue(1, std::integral_constant<int, 1>{});
-  auto stage = [&](int f, auto btag) {
-    constexpr int b = decltype(btag)::value;
-    if (f + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (f + 2 < nst) issue(f + 2, std::integral_constant<int, (b + 2) % 3>{});
-    const char* buf = smem + b * C::TILE_BYTES;
-    bf16x8 af[2][KS];
-#pragma unroll
-    for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
-#pragma unroll
-    for (int rg = 0; rg < KW_RG; ++rg) {
-      if (rg + 1 < KW_RG) {
-        const char* nb = buf + (rg + 1) * 32 * C::CPR * 16;
-#pragma unroll
-        for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
-      }
-      if (rg < live_rg) {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int k = 0; k < KS; ++k)
-            acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[b][g][k], acc[rg][g], 0, 0, 0);
-      }
-    }
-  };
-  for (int f = 0; f < nst; f += 3) {
-    stage(f, std::integral_constant<int, 0>{});
-    if (f + 1 < nst) stage(f + 1, std::integral_constant<int, 1>{});
-    if (f + 2 < nst) stage(f + 2, std::integral_constant<int, 2>{});
-  }
-  float xsg[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float t = 0.f;
-    for (int c = h; c < dp / 8; c += 2) {
-      const bf16x8 v = xrow[g][c];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) t = fmaf((float)v[j], (float)v[j], t);
-    }
-    t += __shfl_xor(t, 32, 64);
-    xsg[g] = t - (float)KM_ONES;
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float best = KM_BIG;
-    int bestt = 0;
-#pragma unroll
-    for (int rg = 0; rg < KW_RG; ++rg) {
-      if (rg >= live_rg) break;
-      float m = keyed(acc[rg][g][0], 0u);
-#pragma unroll
-      for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
-      if (m < best) {
-        best = m;
-        bestt = rg;
-      }
-    }
-    const float ob = __shfl_xor(best, 32, 64);
-    const int obt = __shfl_xor(bestt, 32, 64);
-    const bool take = h ? (ob <= best) : (ob < best);
-    const float bv = take ? ob : best;
-    const int bt = take ? obt : bestt;
-    const int hw = take ? (1 - h) : h;
-    const unsigned reg = __float_as_uint(bv) & 0xFu;
-    const int idx = row0 + bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
-    const long p = pbase + g * 32 + r;
-    if (h == 0 && p < N) {
-      const float dist = fmaxf(bv + xsg[g], 0.f);
-      const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
-      __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <int G, int DC>
-int launch_wide3(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
-                 unsigned long long* keys, hipStream_t s) {
-  using C = KWCfg<G, DC>;
-  if (dp % DC) return HARP_EBADARG;
-  const long npb = (N + C::PTS - 1) / C::PTS;
-  const int nkb = (kswept + KW_CB - 1) / KW_CB;
-  const long rounds = (npb + 7) / 8 * nkb;
-  kmeans_assign_wide3_kernel<G, DC><<<dim3((unsigned)(rounds * 8)), dim3(256), 0, s>>>(
-      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
-  return harp_launch_status();
-}
-
-// Both operands through LDS: the points' 64-feature slices ride LDS-DMA too (a stage's slice
-// of 32 G rows per wave is 1-KiB contiguous pieces, where per-lane 16-B register loads touch
-// 32 rows per instruction), fragments read conflict-free with the same rotation as the
-// centroid slices. G point groups per wave (4 waves), NBUF-deep LDS ring (stage f + NBUF - 1
-// is issued once stage f has landed: counted vmcnt waits, one barrier per stage).
 template <int G, int DC, int NBUF>
 __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
     const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
@@ -820,166 +672,6 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
   }
 }
 
-// Persistent form of the LDS-staged tiling (G = 2, 64-feature stages, 2-deep ring): one
-// workgroup per CU walks its XCD's (point block, centroid block) tiles -- workgroup j of XCD
-// x takes tiles j, j + W, j + 2W, ... of x's tile list (point blocks x, x + 8, ...; centroid
-// blocks minor), so the workgroups resident on an XCD still share their point rows in L2 --
-// and the stage stream runs across tile boundaries: the next tile's first stage is in flight
-// while a tile's argmin epilogue and atomics run (no per-tile launch, prologue or drain).
-__global__ __launch_bounds__(256, 1) void kmeans_assign_wide_persist_kernel(
-    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
-    int nkb, unsigned long long* __restrict__ keys) {
-  constexpr int G = 2, DC = 64;
-  using C = KWCfg<G, DC>;
-  constexpr int KS = C::KS, CPR = C::CPR;
-  constexpr int XROWS = 4 * G * 32;
-  constexpr int XBYTES = XROWS * DC * 2;
-  constexpr int SBYTES = C::TILE_BYTES + XBYTES;
-  constexpr int XDMA = XROWS * CPR / 64;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SBYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int xcd = (int)(blockIdx.x & 7);
-  const int wpx = (int)(gridDim.x >> 3);      // workgroups per XCD
-  const int j = (int)(blockIdx.x >> 3);
-  const long npb = (N + XROWS - 1) / XROWS;
-  const long npb_x = npb > xcd ? (npb - xcd + 7) / 8 : 0;  // point blocks of this XCD
-  const long ntile_x = npb_x * nkb;
-  const long nmine = ntile_x > j ? (ntile_x - j + wpx - 1) / wpx : 0;
-  const int nst = dp / DC;
-  if (nmine == 0) return;
-  auto tile_of = [&](long t, long& p0, int& row0) {  // t-th tile of this workgroup
-    const long q = j + t * wpx;  // index in the XCD's tile list
-    p0 = ((q / nkb) * 8 + xcd) * XROWS;
-    row0 = (int)(q % nkb) * KW_CB;
-  };
-  auto issue = [&](long p0, int row0, int f, int slot) {
-    char* buf = smem + slot * SBYTES;
-    stage_dma_wide<C>(Cm2, dp, row0, kp, f, buf, wave, lane);
-    char* xb = buf + C::TILE_BYTES;
-#pragma unroll
-    for (int j0 = 0; j0 < XDMA; j0 += 4) {
-      const int jj = j0 + wave;
-      const int q = jj * 64 + lane;
-      const int row = q / CPR;
-      int c = q - row * CPR - wide_rot<CPR>(row);
-      if (c < 0) c += CPR;
-      long pr = p0 + row;
-      if (pr > N - 1) pr = N - 1;
-      const __bf16* src = X + pr * ldx + f * DC + c * 8;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                       (void __attribute__((address_space(3)))*)(xb + jj * 1024), 16, 0, 0);
-    }
-  };
-  floatx16 acc[KW_RG][G];
-  int aoff[KS];
-#pragma unroll
-  for (int k = 0; k < KS; ++k) aoff[k] = (r * CPR + (2 * k + h + wide_rot<CPR>(r)) % CPR) * 16;
-  long p0, np0;
-  int row0, nrow0;
-  tile_of(0, p0, row0);
-  issue(p0, row0, 0, 0);
-  int slot = 0;
-  for (long t = 0; t < nmine; ++t) {
-    const bool more = t + 1 < nmine;
-    if (more) tile_of(t + 1, np0, nrow0);
-    const int live_rg = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
-#pragma unroll
-    for (int a = 0; a < KW_RG; ++a)
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
-    float xs[G] = {0.f, 0.f};
-    for (int f = 0; f < nst; ++f) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      // the next stage: this tile's, or the next tile's first (in flight under the epilogue)
-      if (f + 1 < nst) issue(p0, row0, f + 1, slot ^ 1);
-      else if (more) issue(np0, nrow0, 0, slot ^ 1);
-      const char* buf = smem + slot * SBYTES;
-      const char* xb = buf + C::TILE_BYTES + wave * (G * 32) * CPR * 16;
-      bf16x8 xf[G][KS];
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int k = 0; k < KS; ++k) xf[g][k] = *(const bf16x8*)(xb + g * 32 * CPR * 16 + aoff[k]);
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int k = 0; k < KS; ++k)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xs[g] = fmaf((float)xf[g][k][e], (float)xf[g][k][e], xs[g]);
-      bf16x8 af[2][KS];
-#pragma unroll
-      for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(buf + aoff[k]);
-#pragma unroll
-      for (int rg = 0; rg < KW_RG; ++rg) {
-        if (rg + 1 < KW_RG) {
-          const char* nb = buf + (rg + 1) * 32 * CPR * 16;
-#pragma unroll
-          for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
-        }
-        if (rg < live_rg) {
-#pragma unroll
-          for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int k = 0; k < KS; ++k)
-              acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[g][k], acc[rg][g], 0, 0, 0);
-        }
-      }
-      slot ^= 1;
-    }
-    // tile epilogue: keyed argmin over the block's 256 candidates, one 64-bit atomic per point
-    const long pbase = p0 + wave * (G * 32);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float xsg = xs[g] + __shfl_xor(xs[g], 32, 64) - (float)KM_ONES;
-      float best = KM_BIG;
-      int bestt = 0;
-#pragma unroll
-      for (int rg = 0; rg < KW_RG; ++rg) {
-        if (rg >= live_rg) break;
-        float m = keyed(acc[rg][g][0], 0u);
-#pragma unroll
-        for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
-        if (m < best) {
-          best = m;
-          bestt = rg;
-        }
-      }
-      const float ob = __shfl_xor(best, 32, 64);
-      const int obt = __shfl_xor(bestt, 32, 64);
-      const bool take = h ? (ob <= best) : (ob < best);
-      const float bv = take ? ob : best;
-      const int bt = take ? obt : bestt;
-      const int hw = take ? (1 - h) : h;
-      const unsigned reg = __float_as_uint(bv) & 0xFu;
-      const int idx = row0 + bt * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
-      const long p = pbase + g * 32 + r;
-      if (h == 0 && p < N) {
-        const float dist = fmaxf(bv + xsg, 0.f);
-        const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
-        __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    p0 = np0;
-    row0 = nrow0;
-  }
-}
-
-int launch_wide_persist(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
-                        unsigned long long* keys, hipStream_t s) {
-  if (dp % 64 || (ldx * 2) % 16) return HARP_EBADARG;
-  const int nkb = (kswept + KW_CB - 1) / KW_CB;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int wpx = cus / 8 > 0 ? cus / 8 : 1;  // one resident workgroup per CU (LDS + registers)
-  kmeans_assign_wide_persist_kernel<<<dim3((unsigned)(wpx * 8)), dim3(256), 0, s>>>(
-      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
-  return harp_launch_status();
-}
-
 template <int G, int DC, int NBUF>
 int launch_wide_lds(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                     unsigned long long* keys, hipStream_t s) {
@@ -1088,24 +780,24 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, long ldx, const void* Cm2, lon
 
 // Wide rows (dp > 256, dp % 64 == 0): keys (N uint64, filled with ~0 by the caller) take the
 // per-point (distance, index) minimum over all centroid blocks; harp_kmeans_wide_finish then
-// writes labels / distances / objective partials (one per 256 points). variant: 0 = auto,
-// 1 = (2 point groups, 64-feature stages, 1 wave / SIMD), 2 = (2, 128, 1), 3 = (1, 64, 2).
+// writes labels / distances / objective partials (one per 256 points). variant: 0 = 5 (both
+// operands through LDS-DMA, 2 point groups per wave, 64-feature stages, 2-deep ring); 1 / 3 =
+// point fragments loaded straight into registers (2 groups at 1 wave / SIMD, 1 group at 2).
+// Measured at N = 1e7, K = 1e3, d = 1000 (profiles/r4_kwide): 5 at 0.96-0.98 PF useful, 1 / 3
+// at 0.56 / 0.61 (waves parked 52-66 % of their cycles on 32-row-per-instruction point
+// loads); 128-feature stages, a 3-deep register pipeline, 32-feature stages with 3- and
+// 4-deep LDS rings, one group per wave with a 3-deep ring, and a persistent stage stream
+// across tiles all measured 0.44-0.93 PF and were removed.
 HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                                         int d, unsigned long long* keys, int variant, hipStream_t s) {
   if (N <= 0 || d + KM_ONES > dp || dp % 64 || dp <= 0 || kswept <= 0 || kswept % 32 || kp < kswept ||
       ldx < dp || ldx % 8 || !keys)
     return HARP_EBADARG;
-  if (variant == 0) variant = dp % 128 == 0 ? 2 : 1;
+  if (variant == 0) variant = 5;
   switch (variant) {
     case 1: return launch_wide<2, 64, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 2: return launch_wide<2, 128, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 3: return launch_wide<1, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 4: return launch_wide3<2, 64>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 5: return launch_wide_lds<2, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 6: return launch_wide_lds<1, 64, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 7: return launch_wide_lds<2, 32, 4>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 8: return launch_wide_lds<2, 32, 3>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
-    case 9: return launch_wide_persist(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     default: return HARP_EBADARG;
   }
 }

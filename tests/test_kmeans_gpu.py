@@ -225,12 +225,12 @@ def test_kmeans_model_wide_d(cuda):
     assert len(obj) == 3 and obj[2] <= obj[0]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [1, 3, 5])
 def test_assign_wide_variants_agree(cuda, variant, monkeypatch):
     """Every wide-row tiling gives the labels of the torch fp64 argmin (near-ties aside)."""
     monkeypatch.setattr(K, "WIDE_VARIANT", variant)
     torch.manual_seed(2)
-    n, d, k = 9000, (760 if variant == 2 else 700), 600  # variant 2 stages 128 features
+    n, d, k = 9000, 700, 600
     x = torch.rand(n, d, device=cuda) * 1000
     X = K.pack_points(x, cuda)
     c = torch.rand(k, d, device=cuda) * 1000
