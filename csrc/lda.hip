@@ -248,47 +248,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     for (int t = 0; t < TPL; ++t) qw[t] = (nwf[t] + beta) * s_inv[k0 + t];
     int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
                                            // waits on ONE memory round trip, not two
-    // PF (packed uint8 rows, 16 topics per lane = ONE 16-B load): the NEXT token's doc row
-    // is fetched while this token samples (ids two ahead), so the per-token doc-row round
-    // trip leaves the dependent chain; 4 VGPRs (the int16 form cost a wave per SIMD,
-    // profiles/r1_lda/ldapf)
-    constexpr bool PF = sizeof(DT) == 1 && TPL == 16;
-    unsigned rn[4] = {0u, 0u, 0u, 0u};
-    int d_n2 = 0, z_n2 = 0;
-    if constexpr (PF) {
-      const uint4 v = *(const uint4*)((const unsigned char*)ndk + (long)d_next * ldd + k0);
-      rn[0] = v.x; rn[1] = v.y; rn[2] = v.z; rn[3] = v.w;
-      if (a + 1 < b) {
-        d_n2 = tdoc[a + 1];
-        z_n2 = tz[a + 1];
-      }
-    }
     for (long i = a; i < b; ++i) {
       const int d = d_next;
       const int z = z_next;
       DT* drow = ndk + (long)d * ldd;
       float nd[TPL];
-      if constexpr (PF) {
-        const unsigned rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-        d_next = d_n2;
-        z_next = z_n2;
-        if (i + 1 < b) {
-          const uint4 v = *(const uint4*)((const unsigned char*)ndk + (long)d_next * ldd + k0);
-          rn[0] = v.x; rn[1] = v.y; rn[2] = v.z; rn[3] = v.w;
-        }
-        if (i + 2 < b) {
-          d_n2 = tdoc[i + 2];
-          z_n2 = tz[i + 2];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) nd[4 * q + e] = (float)((rc[q] >> (8 * e)) & 0xFFu);
-      } else {
-        if (i + 1 < b) {
-          d_next = tdoc[i + 1];
-          z_next = tz[i + 1];
-        }
+      if (i + 1 < b) {
+        d_next = tdoc[i + 1];
+        z_next = tz[i + 1];
+      }
+      {
         int ndi[TPL];
         DocRow<DT>::template load<TPL>(drow, k0, ndi);
 #pragma unroll
@@ -350,17 +319,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
           DocRow<DT>::add(drow, nz, 1);
           atomicSub(&s_delta[z], 1);
           atomicAdd(&s_delta[nz], 1);
-        }
-      }
-      if constexpr (PF) {
-        // the next token of the same doc: its row was fetched before this token's move
-        if (nz != z && i + 1 < b && d_next == d) {
-          const int zq = (z & 15) >> 2, zs = (z & 3) * 8, nq = (nz & 15) >> 2, ns = (nz & 3) * 8;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (lane == (z >> 4) && q == zq) rn[q] -= 1u << zs;
-            if (lane == (nz >> 4) && q == nq) rn[q] += 1u << ns;
-          }
         }
       }
     }
