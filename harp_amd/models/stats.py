@@ -37,8 +37,9 @@ def _local(comm: Optional[Communicator]) -> Communicator:
 #  * "bf16": the MFMA SYRK fast path -- operands rounded to bf16 ONCE (ops.linalg.FeatureMajor),
 #    fp32 accumulation; n, the column sums and X^T X all come from that one rounded operand
 #    (a row of ones in the Gram), so the finalize never mixes operands. The bf16 rounding
-#    (2^-9 relative per element) bounds the result: tests/test_partial_results.py pins it
-#    (<= 3e-3 relative covariance error on U[0,1) data);
+#    (2^-9 relative per element) bounds the result: 3.5e-5 relative (max-norm) covariance
+#    error measured on 1e6 x 1000 U[0,1) data (tests/test_linalg_gpu.py bounds it by 3e-4,
+#    tests/test_partial_results.py by 3e-3 on the CPU form);
 #  * "fp32": fp32 operands, rocBLAS fp32 GEMMs over row slices of ops.linalg.ATB_CHUNK
 #    rows on data shifted by a per-rank reference row (no cancellation in the centred
 #    sums), slices summed in fp64: <= 1e-6 relative to an fp64 covariance;
