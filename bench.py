@@ -402,7 +402,9 @@ def _lda_run(args, comm, torch, local_server: bool, iters: int) -> dict:
     out = {"tokens_per_sec": round(n / dt, 1), "s_per_iter": round(dt / iters, 6),
            "median_s_per_iter": round(st["median"], 6), "iter_s": st, "iters": iters,
            "sync_bytes_per_iter": int(coll / max(iters, 1)), "loglik_end": ll, "setup_s": round(setup_s, 3),
-           "local_server": bool(getattr(m, "local_server", False)), "tokens_per_iter": int(n) // iters}
+           "local_server": bool(getattr(m, "local_server", False)), "tokens_per_iter": int(n) // iters,
+           "comm_mode": getattr(m, "comm_mode", "rotation"), "fused_rows": bool(getattr(m, "fused", False)),
+           "sampler": "sparse" if getattr(m, "sparse", False) else "dense"}
     del m
     return out
 
