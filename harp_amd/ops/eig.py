@@ -46,16 +46,28 @@ NB_DEFAULT = 32  # workgroups (CUs) of XCD 0
 VARIANT = os.environ.get("HARP_EIG_VARIANT", "fused")
 
 
-def usable(C: torch.Tensor) -> bool:
-    return (C.device.type == "cuda" and C.dtype == torch.float64 and C.dim() == 2 and C.shape[0] == C.shape[1]
-            and _lib.use_native(C) and 0 < C.shape[0] <= int(_lib.kernels().harp_eig_max_n()))
+# crossover to rocSOLVER: the one-XCD reduction costs n steps of ~10-25 us and loses to the
+# blocked dsyevd near n = 1.9k (eigh: n = 1000 11.7 vs 23-27 ms, 1536 29.2 vs 36.3, 1792
+# 40.6 vs 44.1, 2048 57.3 vs 51.7; profiles/r4_eigh/crossover.log, time_barriers10.log)
+NATIVE_MAX_N = int(os.environ.get("HARP_EIG_NATIVE_MAX", "1856"))
 
 
-def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None) -> torch.Tensor:
-    """Ascending eigenvalues of the symmetric matrix ``C`` (fp64 on a GPU: the one-XCD
-    kernels; otherwise, or if the cooperative launch could not claim its workgroups,
-    torch.linalg.eigvalsh)."""
-    if not usable(C):
+def usable(C: torch.Tensor, native: bool | None = None) -> bool:
+    """The native kernels take C: fp64 square on a GPU, within the kernels' size limit and
+    (``native=None``) at most NATIVE_MAX_N; ``native=True`` ignores the crossover (tests),
+    ``native=False`` never takes them."""
+    if native is False:
+        return False
+    ok = (C.device.type == "cuda" and C.dtype == torch.float64 and C.dim() == 2 and C.shape[0] == C.shape[1]
+          and _lib.use_native(C) and 0 < C.shape[0] <= int(_lib.kernels().harp_eig_max_n()))
+    return ok and (native is True or C.shape[0] <= NATIVE_MAX_N)
+
+
+def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None, native: bool | None = None) -> torch.Tensor:
+    """Ascending eigenvalues of the symmetric matrix ``C`` (fp64 on a GPU up to
+    NATIVE_MAX_N: the one-XCD kernels; otherwise, or if the cooperative launch could not
+    claim its workgroups, torch.linalg.eigvalsh). ``native``: see :func:`usable`."""
+    if not usable(C, native if stamps is None else True):
         return torch.linalg.eigvalsh(C)
     n = C.shape[0]
     dev = C.device
@@ -142,11 +154,12 @@ def eigh_tridiag(d: torch.Tensor, e: torch.Tensor):
     return dmod[order], Qt[order].t()
 
 
-def eigh(C: torch.Tensor):
+def eigh(C: torch.Tensor, native: bool | None = None):
     """Eigenvalues (ascending) and eigenvectors (columns) of the symmetric matrix ``C``
-    (fp64 on a GPU: one-XCD reduction + D&C + WY back-transform; otherwise, or if the
-    cooperative launch could not claim its workgroups, torch.linalg.eigh)."""
-    if not usable(C):
+    (fp64 on a GPU up to NATIVE_MAX_N: one-XCD reduction + D&C + WY back-transform;
+    otherwise, or if the cooperative launch could not claim its workgroups,
+    torch.linalg.eigh). ``native``: see :func:`usable`."""
+    if not usable(C, native):
         return torch.linalg.eigh(C)
     n = C.shape[0]
     dev = C.device

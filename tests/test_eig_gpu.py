@@ -19,7 +19,7 @@ def _sym(n, seed, cuda):
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 64, 65, 513, 1000, 2048])
 def test_random_symmetric(cuda, n):
     C = _sym(n, n, cuda)
-    w = EIG.eigvalsh(C)
+    w = EIG.eigvalsh(C, native=True)
     ref = torch.linalg.eigvalsh(C)
     scale = max(1.0, float(ref.abs().max()))
     assert float((w - ref).abs().max()) <= 1e-12 * scale * max(1, n) ** 0.5
@@ -137,3 +137,20 @@ def test_eigh_correlation_matrix(cuda):
         torch.cuda.synchronize()
         ts[name] = (time.perf_counter() - t0) / 5
     print(f"eigh 1000 x 1000 (vectors): harp {ts['harp'] * 1e3:.2f} ms, rocSOLVER {ts['torch'] * 1e3:.2f} ms")
+
+
+def test_eigh_native_above_crossover(cuda):
+    """Above NATIVE_MAX_N the library routes to rocSOLVER; native=True still runs the kernels
+    (n = 2048: reduction + D&C + back-transform) to the same accuracy."""
+    n = 2048
+    assert n > EIG.NATIVE_MAX_N
+    C = _sym(n, 11, cuda)
+    lam, V = EIG.eigh(C, native=True)
+    ref = torch.linalg.eigvalsh(C)
+    nc = float(torch.linalg.matrix_norm(C, 2))
+    I = torch.eye(n, dtype=torch.float64, device=cuda)
+    assert float((lam - ref).abs().max()) <= 1e-12 * nc * n ** 0.5
+    assert float((V.t() @ V - I).abs().max()) <= 1e-12
+    assert float((C @ V - V * lam).abs().max()) <= 1e-11 * nc
+    lam2, _ = EIG.eigh(C)  # crossover path
+    assert float((lam2 - ref).abs().max()) <= 1e-12 * nc
