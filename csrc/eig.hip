@@ -368,7 +368,8 @@ template <int KU>
 __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A, long lda, int n,
                                                          double* __restrict__ dout, double* __restrict__ eout, int NB,
                                                          int* __restrict__ ws, double* __restrict__ wsd,
-                                                         double* __restrict__ vout, double* __restrict__ tauout) {
+                                                         double* __restrict__ vout, double* __restrict__ tauout,
+                                                         long long* __restrict__ stamps) {
   extern __shared__ double smem[];
   double* sv = smem;          // v_k
   double* sw = smem + n;      // w_k
@@ -412,6 +413,16 @@ __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A,
   }
   fused_pass<KU>(A, lda, 1, n - 1, b, NB, false, nullptr, nullptr, tn, sn, wsd, spart);
   if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
+  // diagnostic (stamps != nullptr): workgroup 0 / thread 0 sums the cycles of each phase
+  const bool stamp = stamps != nullptr && b == 0 && tid == 0;
+  long long ph[4] = {0, 0, 0, 0}, t_last = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {
+    if (stamp) {
+      const long long now = (long long)__builtin_amdgcn_s_memtime();
+      ph[i] += now - t_last;
+      t_last = now;
+    }
+  };
   for (int k = 0; k + 2 < n; ++k) {
     const int off = k + 1, m = n - off;
     const double tk = tn;
@@ -461,6 +472,7 @@ __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A,
       }
     }
     __syncthreads();
+    mark(0);
     if (k + 3 < n) {
       tn = house_lds(sn, m - 1, red, &beta);
       if (lead) eout[k + 1] = beta;
@@ -473,10 +485,15 @@ __global__ __launch_bounds__(kT) void sytrd_fused_kernel(double* __restrict__ A,
       if (lead) eout[k + 1] = sn[0];
     }
     if (vout && lead) tauout[k + 1] = tn;
+    mark(1);
     // trailing block of the next step: update by (v_k, w_k) and p_{k+1} in one pass
     fused_pass<KU>(A, lda, off + 1, m - 1, b, NB, tk != 0.0, sv + 1, sw + 1, tn, sn, pn, spart);
+    mark(2);
     if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;
+    mark(3);
   }
+  if (stamp)
+    for (int i = 0; i < 4; ++i) stamps[i] = ph[i];
   if (lead) dout[n - 1] = ld_agent(A + (n - 1) + (long)(n - 1) * lda);
 }
 
@@ -556,6 +573,7 @@ __global__ __launch_bounds__(256) void tridiag_multisect_kernel(const double* __
 }  // namespace
 
 // Fused look-ahead reduction (sytrd_fused_kernel) + multisection; wsd: zeroed 3 n doubles.
+static long long* g_fused_stamps = nullptr;  // diagnostic phase cycles (harp_eig_fused_stamps)
 template <int KU>
 static int launch_fused(double* A, long lda, int n, double* d, double* e, int NB, int* ws, double* wsd, hipStream_t s,
                         double* V = nullptr, double* tau = nullptr) {
@@ -563,7 +581,8 @@ static int launch_fused(double* A, long lda, int n, double* d, double* e, int NB
   if (lds1 > 32 * 1024 && hipFuncSetAttribute((const void*)sytrd_fused_kernel<KU>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess)
     return HARP_ELAUNCH;
-  sytrd_fused_kernel<KU><<<dim3((unsigned)(NB * 8)), dim3(kT), lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, V, tau);
+  sytrd_fused_kernel<KU><<<dim3((unsigned)(NB * 8)), dim3(kT), lds1, s>>>(A, lda, n, d, e, NB, ws, wsd, V, tau,
+                                                                      g_fused_stamps);
   return harp_launch_status();
 }
 
@@ -592,6 +611,9 @@ HARP_EXPORT int harp_sytrd_fused(double* A, long lda, int n, double* d, double* 
   return launch_fused<8>(A, lda, n, d, e, nb_max, ws, wsd, s, V, tau);
 }
 
+// diagnostic: the next fused launches sum workgroup 0's cycles per phase into stamps[0..3]
+// (w + column update, Householder vector, trailing pass, arrival); nullptr turns it off
+HARP_EXPORT void harp_eig_fused_stamps(long long* stamps) { g_fused_stamps = stamps; }
 HARP_EXPORT int harp_eig_ws_ints() { return kWsInts; }
 HARP_EXPORT int harp_eig_max_n() { return kMaxN; }
 // workgroups the reduction uses (all nb_max of XCD 0; the tiles are re-cut every step)
