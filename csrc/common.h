@@ -40,6 +40,32 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// wave64 fp64 sum on the DPP network: quad_perm [1,0,3,2] and [2,3,0,1], row_ror 4 and 8
+// leave every lane of a 16-lane row with the row's sum; the four row sums are then read
+// from lanes 0 / 16 / 32 / 48 (v_readlane) and added in one fixed order, so every lane gets
+// the same bits. Six dependent ds_bpermute round trips become four DPP moves and eight
+// readlanes. Needs the whole wave active (as the __shfl_xor form does).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_d(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum_d_dpp(double v) {
+  v += dpp_mov_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov_d<0x124>(v);  // row_ror:4
+  v += dpp_mov_d<0x128>(v);  // row_ror:8
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
 // wave64 inclusive prefix sum on the DPP network (no LDS round trips): Hillis-Steele within
 // each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 and 3 and
 // row_bcast:31 into rows 2 and 3; lanes without a source add 0.

@@ -70,7 +70,7 @@ __device__ __forceinline__ bool arrive(int* cnt, int target, int* err, int* s_ok
 // block-wide sum, the result in every thread
 template <int T = kT>
 __device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum_d(v);
+  v = wave_sum_d_dpp(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   double s = 0.0;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
         __syncthreads();
       }
       if (wv == 0) {
-        pvp = wave_sum_d(pvp);
+        pvp = wave_sum_d_dpp(pvp);
         if (lane == 0 && pvp != 0.0) atomicAdd(scal + par, pvp);
       }
     }
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(kT) void sytrd_coop_kernel(double* __restrict__ A, 
         sp = fma(a, a, sp);
       }
     }
-    sp = wave_sum_d(sp);
+    sp = wave_sum_d_dpp(sp);
     if (lane == 0 && sp != 0.0) atomicAdd(scal + 2 + (par ^ 1), sp);
     STAMP(4)
     if (!arrive(ws + 1, NB * ++syncs, err, &s_ok)) return;

@@ -43,7 +43,7 @@ __device__ __forceinline__ double wave_prod_d(double v) {
 
 // block reductions (1024 threads), result in every thread
 __device__ __forceinline__ double block_sum_1k(double v, double* red) {
-  v = wave_sum_d(v);
+  v = wave_sum_d_dpp(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__
     const double mid = 0.5 * (dd[i + 1] - dd[i]);
     double f = 0.0;
     for (int j = lane; j < k; j += 64) f += zz[j] * zz[j] / ((dd[j] - dd[i]) - mid);
-    f = wave_sum_d(f) + irho;
+    f = wave_sum_d_dpp(f) + irho;
     if (f >= 0.0) {
       o = i;
       lo_t = 0.0;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__
     for (int j = lane; j < k; j += 64) z2 += zz[j] * zz[j];
     o = i;
     lo_t = 0.0;
-    hi_t = rho * wave_sum_d(z2);
+    hi_t = rho * wave_sum_d_dpp(z2);
   }
   const double dor = dd[o];
   double tau = 0.5 * (lo_t + hi_t);
@@ -312,10 +312,10 @@ __global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__
         dphi = fma(t, r, dphi);
       }
     }
-    psi = wave_sum_d(psi);
-    phi = wave_sum_d(phi);
-    dpsi = wave_sum_d(dpsi);
-    dphi = wave_sum_d(dphi);
+    psi = wave_sum_d_dpp(psi);
+    phi = wave_sum_d_dpp(phi);
+    dpsi = wave_sum_d_dpp(dpsi);
+    dphi = wave_sum_d_dpp(dphi);
     const double f = irho + psi + phi;
     const double erretm = 2.0 * kEps * (irho + fabs(psi) + fabs(phi));
     if (fabs(f) <= erretm || hi_t - lo_t <= 2.0 * kEps * fmax(fabs(lo_t), fabs(hi_t))) break;
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void dc_vectors_kernel(const int* __restrict__
     U[j] = u;
     s2 = fma(u, u, s2);
   }
-  const double inv = 1.0 / sqrt(wave_sum_d(s2));
+  const double inv = 1.0 / sqrt(wave_sum_d_dpp(s2));
   for (int j = lane; j < k; j += 64) U[j] *= inv;
 }
 
