@@ -672,6 +672,181 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_wide_lds_kernel(
   }
 }
 
+// 8 waves (2 per SIMD) on the same 256 x 256 tile: wave w takes centroid half w & 1 and
+// point quarter w >> 1 (4 x 2 accumulators), so each SIMD has a second wave to issue while
+// one waits (the 4-wave form parks 44 % of its cycles on instruction dependencies)
+template <int C_DMA8, class C>
+__device__ __forceinline__ void stage_dma_wide8(const __bf16* __restrict__ cm2, int dp, int row0, int kp, int f,
+                                                char* lds, int wave, int lane) {
+#pragma unroll
+  for (int j0 = 0; j0 < C::DMA; j0 += 8) {
+    const int j = j0 + wave;
+    const int q = j * 64 + lane;
+    const int row = q / C::CPR;
+    int c = q - row * C::CPR - wide_rot<C::CPR>(row);
+    if (c < 0) c += C::CPR;
+    int gr = row0 + row;
+    if (gr > kp - 1) gr = kp - 1;
+    const __bf16* src = cm2 + (size_t)gr * dp + f * (C::CPR * 8) + c * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
+  }
+}
+
+template <int G, int DC, int NBUF>
+__global__ __launch_bounds__(512, 1) void kmeans_assign_wide8_kernel(
+    const __bf16* __restrict__ X, long ldx, const __bf16* __restrict__ Cm2, long N, int dp, int kswept, int kp,
+    int nkb, unsigned long long* __restrict__ keys) {
+  using C = KWCfg<G, DC>;
+  constexpr int KS = C::KS, CPR = C::CPR;
+  constexpr int XROWS = 4 * G * 32;                  // points per workgroup (256 at G = 2)
+  constexpr int RGW = KW_RG / 2, GW = G;             // per wave: 4 centroid groups x G point groups
+  constexpr int XBYTES = XROWS * DC * 2;             // point slice per stage
+  constexpr int SBYTES = C::TILE_BYTES + XBYTES;     // one ring slot
+  constexpr int XDMA = XROWS * CPR / 64;             // 1-KiB pieces of the point slice
+  constexpr int OPS = C::DMA / 8 + XDMA / 8;         // DMA instructions per wave per stage
+  static_assert(C::DMA % 8 == 0 && XDMA % 8 == 0, "whole pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int rgo = (wave & 1) * RGW;                  // first centroid group of this wave
+  const int pwo = (wave >> 1) * (GW * 32);           // first point of this wave in the block
+  const long id = blockIdx.x;
+  const long xcd = id & 7, round = id >> 3;
+  const long pb = (round / nkb) * 8 + xcd;
+  const int kb = (int)(round % nkb);
+  const long npb = (N + XROWS - 1) / XROWS;
+  if (pb >= npb) return;
+  const int row0 = kb * KW_CB;
+  const int live_blk = (kswept - row0) >= KW_CB ? KW_RG : (kswept - row0 + 31) / 32;
+  const int live_rg = live_blk - rgo < 0 ? 0 : (live_blk - rgo > RGW ? RGW : live_blk - rgo);
+  const long p0 = pb * XROWS;  // first point of the workgroup
+  const long pbase = p0 + pwo;
+  const int nst = dp / DC;
+  auto issue = [&](int f, int slot) {
+    char* buf = smem + slot * SBYTES;
+    stage_dma_wide8<0, C>(Cm2, dp, row0, kp, f, buf, wave, lane);
+    char* xb = buf + C::TILE_BYTES;
+#pragma unroll
+    for (int j0 = 0; j0 < XDMA; j0 += 8) {
+      const int j = j0 + wave;
+      const int q = j * 64 + lane;
+      const int row = q / CPR;
+      int c = q - row * CPR - wide_rot<CPR>(row);
+      if (c < 0) c += CPR;
+      long pr = p0 + row;
+      if (pr > N - 1) pr = N - 1;
+      const __bf16* src = X + pr * ldx + f * DC + c * 8;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)(xb + j * 1024), 16, 0, 0);
+    }
+  };
+  floatx16 acc[RGW][G];
+#pragma unroll
+  for (int a = 0; a < RGW; ++a)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][g][q] = 0.f;
+  int aoff[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) aoff[k] = (r * CPR + (2 * k + h + wide_rot<CPR>(r)) % CPR) * 16;
+#pragma unroll
+  for (int q = 0; q < NBUF - 1; ++q)
+    if (q < nst) issue(q, q);
+  float xs[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) xs[g] = 0.f;
+  for (int f = 0; f < nst; ++f) {
+    // stage f landed when at most the younger stages' pieces are outstanding
+    const int younger = (nst - 1 - f) < (NBUF - 2) ? (nst - 1 - f) : (NBUF - 2);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (f + NBUF - 1 < nst) issue(f + NBUF - 1, (f + NBUF - 1) % NBUF);
+    const char* buf = smem + (f % NBUF) * SBYTES;
+    const char* xb = buf + C::TILE_BYTES + pwo * CPR * 16;
+    const char* cb = buf + rgo * 32 * CPR * 16;
+    bf16x8 xf[G][KS];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) xf[g][k] = *(const bf16x8*)(xb + g * 32 * CPR * 16 + aoff[k]);
+    // |x|^2 from the staged fragments (VALU work under the stage's MFMAs)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xs[g] = fmaf((float)xf[g][k][j], (float)xf[g][k][j], xs[g]);
+    bf16x8 af[2][KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) af[0][k] = *(const bf16x8*)(cb + aoff[k]);
+#pragma unroll
+    for (int rg = 0; rg < RGW; ++rg) {
+      if (rg + 1 < RGW) {
+        const char* nb = cb + (rg + 1) * 32 * CPR * 16;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) af[(rg + 1) & 1][k] = *(const bf16x8*)(nb + aoff[k]);
+      }
+      if (rg < live_rg) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int k = 0; k < KS; ++k)
+            acc[rg][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rg & 1][k], xf[g][k], acc[rg][g], 0, 0, 0);
+      }
+    }
+  }
+  float xsg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) xsg[g] = xs[g] + __shfl_xor(xs[g], 32, 64) - (float)KM_ONES;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float best = KM_BIG;
+    int bestt = 0;
+#pragma unroll
+    for (int rg = 0; rg < RGW; ++rg) {
+      if (rg >= live_rg) break;
+      float m = keyed(acc[rg][g][0], 0u);
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = fminf(m, keyed(acc[rg][g][q], (unsigned)q));
+      if (m < best) {
+        best = m;
+        bestt = rg;
+      }
+    }
+    const float ob = __shfl_xor(best, 32, 64);
+    const int obt = __shfl_xor(bestt, 32, 64);
+    const bool take = h ? (ob <= best) : (ob < best);
+    const float bv = take ? ob : best;
+    const int bt = take ? obt : bestt;
+    const int hw = take ? (1 - h) : h;
+    const unsigned reg = __float_as_uint(bv) & 0xFu;
+    const int idx = row0 + (rgo + bt) * 32 + (int)(reg & 3u) + 8 * (int)(reg >> 2) + 4 * hw;
+    const long p = pbase + g * 32 + r;
+    if (h == 0 && p < N && live_rg > 0) {
+      const float dist = fmaxf(bv + xsg[g], 0.f);
+      const unsigned long long key = ((unsigned long long)__float_as_uint(dist) << 32) | (unsigned)idx;
+      __hip_atomic_fetch_min(keys + p, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int G, int DC, int NBUF>
+int launch_wide8(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
+                 unsigned long long* keys, hipStream_t s) {
+  constexpr int XROWS = 4 * G * 32;
+  if (dp % DC || (ldx * 2) % 16) return HARP_EBADARG;
+  const long npb = (N + XROWS - 1) / XROWS;
+  const int nkb = (kswept + KW_CB - 1) / KW_CB;
+  const long rounds = (npb + 7) / 8 * nkb;
+  kmeans_assign_wide8_kernel<G, DC, NBUF><<<dim3((unsigned)(rounds * 8)), dim3(512), 0, s>>>(
+      (const __bf16*)X, ldx, (const __bf16*)Cm2, N, dp, kswept, kp, nkb, keys);
+  return harp_launch_status();
+}
+
 template <int G, int DC, int NBUF>
 int launch_wide_lds(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                     unsigned long long* keys, hipStream_t s) {
@@ -780,24 +955,27 @@ HARP_EXPORT int harp_kmeans_assign(const void* X, long ldx, const void* Cm2, lon
 
 // Wide rows (dp > 256, dp % 64 == 0): keys (N uint64, filled with ~0 by the caller) take the
 // per-point (distance, index) minimum over all centroid blocks; harp_kmeans_wide_finish then
-// writes labels / distances / objective partials (one per 256 points). variant: 0 = 5 (both
-// operands through LDS-DMA, 2 point groups per wave, 64-feature stages, 2-deep ring); 1 / 3 =
+// writes labels / distances / objective partials (one per 256 points). variant: 0 = 6 (both
+// operands through LDS-DMA into a 256 x 256 tile, 8 waves = 2 per SIMD, each 128 centroids x
+// 64 points); 5 = the same tile with 4 waves (256 centroids x 64 points each); 1 / 3 =
 // point fragments loaded straight into registers (2 groups at 1 wave / SIMD, 1 group at 2).
-// Measured at N = 1e7, K = 1e3, d = 1000 (profiles/r4_kwide): 5 at 0.96-0.98 PF useful, 1 / 3
-// at 0.56 / 0.61 (waves parked 52-66 % of their cycles on 32-row-per-instruction point
-// loads); 128-feature stages, a 3-deep register pipeline, 32-feature stages with 3- and
-// 4-deep LDS rings, one group per wave with a 3-deep ring, and a persistent stage stream
-// across tiles all measured 0.44-0.93 PF and were removed.
+// Measured at N = 1e7, K = 1e3 (profiles/r4_kwide): d = 1000 6 and 5 both 0.98 PF useful,
+// d = 512 6 at 0.86 vs 5 at 0.81 PF; 1 / 3 at 0.56 / 0.61 (waves parked 52-66 % of their
+// cycles on 32-row-per-instruction point loads); 128-feature stages, a 3-deep register
+// pipeline, 32-feature stages with 3- and 4-deep LDS rings, one group per wave with a 3-deep
+// ring, a persistent stage stream across tiles and square 128 x 128 per-wave tiles all
+// measured 0.44-0.93 PF and were removed.
 HARP_EXPORT int harp_kmeans_assign_wide(const void* X, long ldx, const void* Cm2, long N, int dp, int kswept, int kp,
                                         int d, unsigned long long* keys, int variant, hipStream_t s) {
   if (N <= 0 || d + KM_ONES > dp || dp % 64 || dp <= 0 || kswept <= 0 || kswept % 32 || kp < kswept ||
       ldx < dp || ldx % 8 || !keys)
     return HARP_EBADARG;
-  if (variant == 0) variant = 5;
+  if (variant == 0) variant = 6;
   switch (variant) {
     case 1: return launch_wide<2, 64, 1>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 3: return launch_wide<1, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     case 5: return launch_wide_lds<2, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
+    case 6: return launch_wide8<2, 64, 2>(X, ldx, Cm2, N, dp, kswept, kp, keys, s);
     default: return HARP_EBADARG;
   }
 }

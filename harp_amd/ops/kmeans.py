@@ -35,7 +35,7 @@ DEFAULT_VARIANT = 15
 
 NARROW_MAX_DP = 256  # the register-resident assign kernel (X fragments live for the sweep)
 WIDE_ALIGN = 64      # wider rows: the feature-staged kernel's stage width
-WIDE_VARIANT = int(os.environ.get("HARP_KMEANS_WIDE_VARIANT", "0"))  # 0: the kernel default (LDS-staged, 5)
+WIDE_VARIANT = int(os.environ.get("HARP_KMEANS_WIDE_VARIANT", "0"))  # 0: the kernel default (LDS-staged, 8 waves: 6)
 
 
 def padded_dim(d: int) -> int:

@@ -225,7 +225,7 @@ def test_kmeans_model_wide_d(cuda):
     assert len(obj) == 3 and obj[2] <= obj[0]
 
 
-@pytest.mark.parametrize("variant", [1, 3, 5])
+@pytest.mark.parametrize("variant", [1, 3, 5, 6])
 def test_assign_wide_variants_agree(cuda, variant, monkeypatch):
     """Every wide-row tiling gives the labels of the torch fp64 argmin (near-ties aside)."""
     monkeypatch.setattr(K, "WIDE_VARIANT", variant)
