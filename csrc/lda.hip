@@ -766,13 +766,11 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
   const int ldelta = Kp <= 4096;  // LDS topic-sum deltas while they cost at most 16 KB
   const int wdelta = sparse_wdelta(Kp);
   const size_t lds = sparse_lds_bytes(Kp, WAVES);
-  static size_t lds_set = 0;  // raise the dynamic-LDS cap past 64 KB once per instantiation
-  if (lds > 65536 && lds > lds_set) {
-    if (hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return HARP_ELAUNCH;
-    lds_set = lds;
-  }
+  // raise the dynamic-LDS cap past 64 KB (per launch: no process-wide cache that a second
+  // device or a concurrent caller could skip past)
+  if (lds > 65536 && hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return HARP_ELAUNCH;
   // grid = resident workgroups (LDS- or wave-slot-bound), striding over the chunks
   long per_cu = 163840 / (long)(lds + 1100);
   if (per_cu > 32 / WAVES) per_cu = 32 / WAVES;

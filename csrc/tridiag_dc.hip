@@ -545,7 +545,6 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
   w.kcnt = ip + 2 * n;
   w.rotp = ip + 3 * n;
   w.rotq = ip + 4 * n;
-  static size_t lds_set = 0;
   for (int l = 0; l < nlevels; ++l) {
     const int m0 = level_off[l], nm = level_off[l + 1] - m0;
     const int smax = level_smax[l];
@@ -554,12 +553,10 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
     w.ldu = smax;
     const int* mg = merges + 3 * m0;
     const size_t lds = prep_lds(smax);
-    if (lds > 65536 && lds > lds_set) {
-      if (hipFuncSetAttribute((const void*)dc_prep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-          hipSuccess)
-        return HARP_ELAUNCH;
-      lds_set = lds;
-    }
+    // set per launch (a host-side attribute call, no process-wide cache to race on)
+    if (lds > 65536 && hipFuncSetAttribute((const void*)dc_prep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds) != hipSuccess)
+      return HARP_ELAUNCH;
     const int threads = smax >= 512 ? 1024 : smax >= 128 ? 256 : 64;
     dc_prep_kernel<<<dim3((unsigned)nm), dim3(threads), lds, st>>>(Q, n, dmod, e, mg, w);
     const unsigned wg = (unsigned)((n + 3) / 4);
