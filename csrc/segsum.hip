@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void bucket_kernel(const int* __restrict__ lab
 // bucket-sorted permutation (so work is balanced whatever the bucket sizes), keeps the
 // running row sum in registers, and flushes it with one contiguous fp32 atomic row segment
 // whenever it crosses a bucket boundary (~1 flush per slot for buckets >> RUN).
-template <int LPR, int RUN>
+template <int LPR, int RUN, int ROWS = 4>
 __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restrict__ X, int dp, long ldx,
                                                           const int* __restrict__ perm,
                                                           const int* __restrict__ start, int K, long n,
@@ -173,17 +173,19 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restri
       kend = start[k + 1];
     }
     long stop = kend < j1 ? kend : j1;
-    // 4 rows in flight per slot inside one bucket
-    for (; j + 4 <= stop; j += 4) {
-      bf16x8 v0{}, v1{}, v2{}, v3{};
-      if (active) {
-        v0 = *(const bf16x8*)(X + (long)perm[j] * ldx + sl * 8);
-        v1 = *(const bf16x8*)(X + (long)perm[j + 1] * ldx + sl * 8);
-        v2 = *(const bf16x8*)(X + (long)perm[j + 2] * ldx + sl * 8);
-        v3 = *(const bf16x8*)(X + (long)perm[j + 3] * ldx + sl * 8);
-      }
+    // ROWS rows in flight per slot inside one bucket
+    for (; j + ROWS <= stop; j += ROWS) {
+      bf16x8 v[ROWS];
+      int pj[ROWS];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += ((float)v0[e] + (float)v1[e]) + ((float)v2[e] + (float)v3[e]);
+      for (int q = 0; q < ROWS; ++q) pj[q] = perm[j + q];
+#pragma unroll
+      for (int q = 0; q < ROWS; ++q) v[q] = active ? *(const bf16x8*)(X + (long)pj[q] * ldx + sl * 8) : bf16x8{};
+#pragma unroll
+      for (int q = 0; q < ROWS; q += 4)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          acc[e] += ((float)v[q][e] + (float)v[q + 1][e]) + ((float)v[q + 2][e] + (float)v[q + 3][e]);
     }
     for (; j < stop; ++j) {
       if (active) {
@@ -251,7 +253,9 @@ HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, long ldx, const i
   constexpr int RUN = 256;
   auto grid = [&](int lpr) { return dim3((unsigned)(((n + RUN - 1) / RUN * lpr + 255) / 256)); };
   if (lpr_min <= 8) rowsum_bf16_kernel<8, RUN><<<grid(8), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
-  else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN><<<grid(16), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
+  // 8 rows in flight at 16 lanes per row (dp 72..128, the K-means headline's 112): 5.13 ->
+  // 5.00 ms at N = 1e8, K = 1e4 (profiles/r4_endstate/rowsum_rows.log)
+  else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN, 8><<<grid(16), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
   else rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
   return harp_launch_status();
 }
