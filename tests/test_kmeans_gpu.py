@@ -225,6 +225,22 @@ def test_kmeans_model_wide_d(cuda):
     assert len(obj) == 3 and obj[2] <= obj[0]
 
 
+@pytest.mark.parametrize("strategy", ["allreduce", "regroup_allgather", "bcast_reduce", "push_pull", "rotation"])
+def test_kmeans_strategies_wide_d_agree(cuda, strategy):
+    """Every sync strategy runs the wide-row path (d = 300 > 256 padded features) and gives
+    the allreduce trajectory (one worker: the strategies differ only in their collectives)."""
+    from harp_amd.models.kmeans import KMeansConfig, run_kmeans
+    from harp_amd.parallel.comm import Communicator
+
+    def obj(st):
+        cfg = KMeansConfig(num_points=12000, num_centroids=70, dim=300, iterations=3, strategy=st, seed=5)
+        return run_kmeans(Communicator(None, cuda), cfg)["objective"]
+
+    ref, got = obj("allreduce"), obj(strategy)
+    assert len(got) == 3 and got[2] <= got[0]
+    assert all(abs(a - b) <= 1e-4 * abs(a) for a, b in zip(ref, got)), (ref, got)
+
+
 @pytest.mark.parametrize("variant", [1, 3, 5, 6])
 def test_assign_wide_variants_agree(cuda, variant, monkeypatch):
     """Every wide-row tiling gives the labels of the torch fp64 argmin (near-ties aside)."""
