@@ -368,10 +368,10 @@ def _lda_run(args, comm, torch, local_server: bool, iters: int) -> dict:
     cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=1 + iters, local_server=local_server)
     cls = LDAPushPullMapper if args.lda_strategy == "push_pull" else LDACollectiveMapper
     m = cls(comm, cfg, nd, V, toks)
+    del toks  # init_model keeps only the mapper's own (int32, word-sorted) token arrays
     _trace(comm, "lda mapper", t0)
     m.init_model(KeyValReader([]))
     _trace(comm, "lda init_model", t0)
-    del toks
     setup_s = time.perf_counter() - t0
     m.iterate(0)
     if hasattr(m, "rot"):

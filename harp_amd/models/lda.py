@@ -25,6 +25,7 @@ import torch
 from ..ops import lda as L
 from ..runtime.dymoro import BudgetTuner, DeviceRotator, RotationSchedule, StepBudget, ring_strides
 from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
+from ..ops.sorting import SORT_CHUNK, argsort_small_keys
 from .common import reduce_partials
 
 
@@ -66,10 +67,16 @@ def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, s
     dtop = torch.randint(0, true_topics, (n_docs, 3), generator=g, device=device)
     pick = torch.randint(0, 3, (n,), generator=g, device=device)
     topic = dtop[doc, pick]
+    del pick  # (in-place steps below: a clueweb1-share corpus has 3.7e9 tokens)
     per = max(vocab // true_topics, 1)
-    rank = (torch.rand(n, generator=g, device=device) ** 3 * per).long().clamp_max(per - 1)
+    u = torch.rand(n, generator=g, device=device)
+    idx = u.pow_(3).mul_(per).long().clamp_max_(per - 1)  # Zipf-like rank within the topic's words
+    del u
+    idx += topic.mul_(per)
+    del topic
+    idx.remainder_(vocab)
     perm = torch.randperm(vocab, generator=g, device=device)
-    word = perm[(topic * per + rank) % vocab]
+    word = perm[idx]
     return doc, word
 
 
@@ -98,24 +105,33 @@ class LDACollectiveMapper(CollectiveMapper):
         # per-word setup does not pay at a few tokens per word: 8-GPU share, 12.5M tokens over
         # 1M words, dense 10.0 vs sparse 14.0 ms per sweep, profiles/r4_lda_share)
         self.sparse = L.use_sparse(K, doc.numel() // P)
-        mine = (doc % P) == me
-        doc, word = doc[mine].to(dev), word[mine].to(dev)
+        self._tokens = None  # the mapper keeps only its own token arrays (int32, word-sorted)
+        if P > 1:
+            mine = (doc % P) == me
+            doc, word = doc[mine].to(dev), word[mine].to(dev)
+            del mine
+        else:
+            doc, word = doc.to(dev), word.to(dev)
         self.ndoc_local = (self.n_docs - me + P - 1) // P
         ldoc = (doc // P).to(torch.int32)
+        del doc
         # word -> (slice, row in slice): seeded permutation, equal slice sizes
         gperm = torch.Generator().manual_seed(cfg.seed + 99)
         perm = torch.randperm(self.vocab, generator=gperm)
         self.vps = math.ceil(self.vocab / ns)
-        pos = torch.empty(self.vocab, dtype=torch.int64)
-        pos[perm] = torch.arange(self.vocab)
-        pos = pos.to(dev)
-        gslice = pos[word] // self.vps
-        wrow = (pos[word] % self.vps).to(torch.int32)
-        order = torch.argsort(gslice * self.vps + wrow.long())
+        pos = torch.empty(self.vocab, dtype=torch.int32)
+        pos[perm] = torch.arange(self.vocab, dtype=torch.int32)
+        key = pos.to(dev)[word]  # = slice * vps + row in slice
+        del word
+        if key.numel() <= SORT_CHUNK:
+            order = torch.argsort(key.long())
+        else:  # an 8-GPU share of clueweb1 (3.7e9 tokens) is past torch's per-call sort limit
+            order = argsort_small_keys(key, ns * self.vps)
         self.tdoc = ldoc[order].contiguous()
-        self.tword = wrow[order].contiguous()
-        gs = gslice[order]
-        counts = torch.bincount(gs, minlength=ns).cpu()
+        del ldoc
+        counts = torch.bincount(key // self.vps, minlength=ns).cpu()
+        self.tword = (key[order] % self.vps).contiguous()
+        del key, order
         self.offsets = [0] + torch.cumsum(counts, 0).tolist()
         self.chunks = []
         for s in range(ns):
@@ -127,8 +143,7 @@ class LDACollectiveMapper(CollectiveMapper):
         self.orders = [L.chunk_order(c) for c in self.chunks] if self.doc_index is not None else [None] * ns
         # counts: doc-topic local; word-topic global (allreduced once), then each worker keeps
         # the slices of its initial placement
-        maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
-        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(dev, maxlen), device=dev)
+        self.ndk = self._doc_topic_table()
         nwk_full = torch.zeros((ns * self.vps, self.Kp), dtype=torch.int32, device=dev)
         nk = torch.zeros(self.Kp, dtype=torch.int32, device=dev)
         for s in range(ns):
@@ -145,13 +160,33 @@ class LDACollectiveMapper(CollectiveMapper):
         self.schedules = [RotationSchedule(P, None, stride=st) for st in ring_strides(P, S)]
         self.schedule = self.schedules[0]
         block = self.schedule.block_at(me, 0, 0)
-        slabs = [nwk_full[(block * S + k) * self.vps:(block * S + k + 1) * self.vps].clone() for k in range(S)]
+        # (one worker: the slabs ARE the table, no copy -- 41 GB at clueweb1's K = 10,000)
+        slabs = [nwk_full[(block * S + k) * self.vps:(block * S + k + 1) * self.vps] for k in range(S)]
+        if P > 1:
+            slabs = [t.clone() for t in slabs]
         self.codec = self._rotation_codec(nwk_full, ns) if P > 1 else None
         del nwk_full
         self.rot = DeviceRotator(self.comm, slabs, name="lda-w", metrics=self.metrics, codec=self.codec)
         self.vbeta = self.vocab * cfg.beta
         self.word_perm = perm  # slice s holds words perm[s*vps:(s+1)*vps]
         self._init_budget()
+
+    def _doc_topic_table(self) -> Optional[torch.Tensor]:
+        """Dense doc-topic counts, or None for the sparse sampler on the GPU: it samples from
+        the doc-order topic lists (DocIndex) alone, and a dense table would cost ndocs x K_pad
+        counts (20 KB per document at K = 10,000; the reference's SparseLDA keeps doc rows
+        sparse too)."""
+        if self.sparse and self.tz.device.type == "cuda" and L._lib.use_native(self.tz):
+            return None
+        maxlen = int(torch.bincount(self.tdoc, minlength=1).max()) if self.tdoc.numel() else 0
+        return torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(self.device, maxlen),
+                           device=self.device)
+
+    def _doc_loglik(self) -> torch.Tensor:
+        K = self.cfg.num_topics
+        if self.ndk is None:
+            return L.doc_loglik_terms(self.doc_index, self.cfg.alpha, K)
+        return L.loglik_terms(self.ndk, self.cfg.alpha, K)
 
     def _init_budget(self) -> None:
         cfg = self.cfg
@@ -264,7 +299,7 @@ class LDACollectiveMapper(CollectiveMapper):
         wp = torch.zeros(2, dtype=torch.float64, device=self.device)
         for k in range(cfg.num_slices):
             wp += L.loglik_terms(self.rot.slabs[k], cfg.beta, K)
-        dp = L.loglik_terms(self.ndk, cfg.alpha, K)
+        dp = self._doc_loglik()
         tot = reduce_partials(self.comm, {"w": wp[:1], "d": dp})
         nk = self.nk[:K].double()
         topic = (torch.lgamma(torch.tensor(self.vbeta, dtype=torch.float64)) - torch.lgamma(nk + self.vbeta)).sum()
@@ -325,7 +360,9 @@ class LDACollectiveMapper(CollectiveMapper):
         from ..utils.checkpoint import blob_table, tensor_table
 
         self.rot.wait_all()
-        tabs = {"tz": blob_table(self.tz), "ndk": blob_table(self.ndk), "nk": blob_table(self.nk)}
+        tabs = {"tz": blob_table(self.tz), "nk": blob_table(self.nk)}
+        if self.ndk is not None:
+            tabs["ndk"] = blob_table(self.ndk)
         for k, words in self._resident_words(it + 1):
             tabs[f"W{k}"] = tensor_table(self.rot.slabs[k][: words.numel()], words)
         return tabs
@@ -341,7 +378,12 @@ class LDACollectiveMapper(CollectiveMapper):
             raise ValueError(f"LDA resume needs the checkpoint's world size {man['world']} "
                              f"(token topics are per-rank state), got {self.get_num_workers()}")
         self.tz.copy_(tabs["tz"][0].to(self.device))
-        self.ndk.copy_(tabs["ndk"][0].to(self.device))
+        if self.ndk is not None:
+            if "ndk" in tabs:
+                self.ndk.copy_(tabs["ndk"][0].to(self.device))
+            else:  # written by a run without the dense table: recount from the topics
+                self.ndk.zero_()
+                L.count(self.tdoc, None, self.tz, self.ndk)
         self.nk.copy_(tabs["nk"][0].to(self.device))
         if self.doc_index is not None:
             self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local)
@@ -404,14 +446,17 @@ class LDAPushPullMapper(LDACollectiveMapper):
         self.Kp = L.padded_topics(K)
         B = self.B = int(getattr(cfg, "block_words", 0) or 4096)
         doc, word = self._tokens
+        self._tokens = None
         # same choice on every worker, by the tokens ONE worker samples (the sparse sampler's
         # per-word setup does not pay at a few tokens per word: 8-GPU share, 12.5M tokens over
         # 1M words, dense 10.0 vs sparse 14.0 ms per sweep, profiles/r4_lda_share)
         self.sparse = L.use_sparse(K, doc.numel() // P)
         mine = (doc % P) == me
         doc, word = doc[mine].to(dev), word[mine].to(dev)
+        del mine
         self.ndoc_local = (self.n_docs - me + P - 1) // P
         ldoc = (doc // P).to(torch.int32)
+        del doc
         blocks = torch.unique(word // B)
         self.need = blocks.cpu().tolist()
         nblocks = math.ceil(self.vocab / B)
@@ -437,8 +482,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
         self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local) if self.sparse else None
-        maxlen = int(torch.bincount(self.tdoc.long(), minlength=1).max()) if self.tdoc.numel() else 0
-        self.ndk = torch.zeros((self.ndoc_local, self.Kp), dtype=L.doc_topic_dtype(dev, maxlen), device=dev)
+        self.ndk = self._doc_topic_table()
         nrows = self.touched.numel() if self.ps is not None else len(self.need) * B
         slab = torch.zeros((nrows, self.Kp), dtype=torch.int32, device=dev)
         nk = torch.zeros(self.Kp, dtype=torch.int32, device=dev)
@@ -623,7 +667,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         wp = torch.zeros(2, dtype=torch.float64, device=self.device)
         for p in self.glob.get_partitions():  # each block counted once, at its owner
             wp += L.loglik_terms(p.get(), cfg.beta, K)
-        dp = L.loglik_terms(self.ndk, cfg.alpha, K)
+        dp = self._doc_loglik()
         tot = reduce_partials(self.comm, {"w": wp[:1], "d": dp})
         nk = self.nk[:K].double()
         topic = (torch.lgamma(torch.tensor(self.vbeta, dtype=torch.float64)) - torch.lgamma(nk + self.vbeta)).sum()
@@ -650,7 +694,9 @@ class LDAPushPullMapper(LDACollectiveMapper):
     def _state_tables(self, it: int) -> dict:
         from ..utils.checkpoint import blob_table, tensor_table
 
-        tabs = {"tz": blob_table(self.tz), "ndk": blob_table(self.ndk), "nk": blob_table(self.nk)}
+        tabs = {"tz": blob_table(self.tz), "nk": blob_table(self.nk)}
+        if self.ndk is not None:
+            tabs["ndk"] = blob_table(self.ndk)
         ids = self.glob.sorted_ids()
         if ids:
             tabs["glob"] = tensor_table(torch.stack([self.glob[b] for b in ids]), ids)

@@ -82,12 +82,15 @@ class DocIndex:
 
     @staticmethod
     def build(tdoc: torch.Tensor, tz: torch.Tensor, n_docs: int) -> "DocIndex":
-        order = torch.sort(tdoc.long(), stable=True).indices
+        from .sorting import argsort_small_keys
+
+        order = argsort_small_keys(tdoc, n_docs)  # any length (chunked past INT_MAX tokens)
+        zdoc = tz[order].to(torch.int16)
         tpos = torch.empty_like(order)
         tpos[order] = torch.arange(order.numel(), device=order.device)
+        del order
         off = torch.zeros(n_docs + 1, dtype=torch.int64, device=tdoc.device)
-        off[1:] = torch.cumsum(torch.bincount(tdoc.long(), minlength=n_docs)[:n_docs], 0)
-        zdoc = tz[order].to(torch.int16)
+        off[1:] = torch.cumsum(torch.bincount(tdoc, minlength=n_docs)[:n_docs], 0)
         return DocIndex(zdoc, off, tpos)
 
     def sync(self, tz: torch.Tensor, tpos: Optional[torch.Tensor] = None) -> None:
@@ -181,7 +184,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
     GPU, ONE wave samples every chunk in order -- bit-reproducible and independent of the
     word-row numbering (a test mode; the CPU sampler is always sequential)."""
     dev = tz.device
-    Kp = ndk.shape[1]
+    Kp = nwk.shape[1]  # ndk may be None (sparse sampler on the GPU: no dense doc-topic table)
     if doc_index is None and use_sparse(K):
         raise ValueError(f"K={K} needs the sparse sampler: pass doc_index (DocIndex.build)")
     if doc_index is not None and tpos is None:
@@ -250,6 +253,32 @@ def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: 
         _lib.stream_ptr(dev))
     _lib.check(st, "lda_cgs_ps")
     return delta
+
+
+def doc_loglik_terms(doc_index: DocIndex, prior: float, K: int, block_tokens: int = 1 << 26) -> torch.Tensor:
+    """:func:`loglik_terms` of the doc-topic counts, from the sparse sampler's doc-order
+    topic lists instead of a dense [docs, K_pad] table (which at K = 10,000 would take
+    20 KB per document): each doc block's (doc, topic) pairs are counted by ``unique``."""
+    off, z = doc_index.doc_off, doc_index.zdoc
+    dev = z.device
+    n_docs = off.numel() - 1
+    lg_p = torch.lgamma(torch.tensor(prior, dtype=torch.float64))
+    lg_kp = torch.lgamma(torch.tensor(K * prior, dtype=torch.float64))
+    out = torch.zeros(2, dtype=torch.float64, device=dev)
+    lens = off[1:] - off[:-1]
+    out[1] = (lg_kp - torch.lgamma(lens.double() + K * prior)).sum()
+    # doc blocks of ~block_tokens tokens (at least one doc each)
+    cuts = torch.searchsorted(off, torch.arange(0, int(off[-1]) + 1, block_tokens, device=dev)).cpu().tolist()
+    edges = sorted(set([0, n_docs] + [min(c, n_docs) for c in cuts]))
+    for d0, d1 in zip(edges[:-1], edges[1:]):
+        a, b = int(off[d0]), int(off[d1])
+        if b == a:
+            continue
+        doc = torch.repeat_interleave(torch.arange(d1 - d0, device=dev), lens[d0:d1])
+        key = doc * 65536 + (z[a:b].long() & 0xFFFF)
+        c = torch.unique(key, return_counts=True)[1].double()
+        out[0] += (torch.lgamma(c + prior) - lg_p).sum()
+    return out
 
 
 def loglik_terms(counts: torch.Tensor, prior: float, K: int) -> torch.Tensor:

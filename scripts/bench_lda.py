@@ -45,6 +45,7 @@ def main():
         cfg.max_chunk = a.max_chunk
     cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper
     m = cls(comm, cfg, nd, V, toks)
+    del toks
     t0 = time.perf_counter()
     m.init_model(KeyValReader([]))
     torch.cuda.synchronize()
@@ -96,7 +97,8 @@ def main():
     if comm.world_size > 1:
         comm.all_reduce(tot)
     if comm.rank == 0:
-        print(json.dumps({"metric": f"LDA-CGS sampled tokens/sec ({a.strategy})", "value": float(tot.item()) / dt,
+        print(json.dumps({"peak_hbm_gb": torch.cuda.max_memory_allocated() / 2**30, "dense_doc_topic": m.ndk is not None,
+                          "metric": f"LDA-CGS sampled tokens/sec ({a.strategy})", "value": float(tot.item()) / dt,
                           "unit": "tokens/s", "s_per_iter": dt / a.iters, "n_gpus": comm.world_size,
                           "docs": nd, "vocab": V, "topics": a.topics, "tokens": int(tot.item()) // a.iters,
                           "sampler": "sparse" if m.doc_index is not None else "dense",

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One 8-GPU rank's share of the reference's published clueweb runs (BASELINE rows 1-6), on
+# one MI355X: MF-SGD rank 2000 and MF-CCD rank 120 on the clueweb2 shape (76,163,963 x
+# 999,933; a rank holds 1/8 of the users), LDA-CGS K = 10,000 on the clueweb1 shape
+# (999,933 words, 392 tokens per document): the full SGD share (2.0e9 ratings), half the
+# CCD and LDA shares; a step that ends in an exception (e.g. out of memory) does not stop
+# the next one (profiles/r4_published/README.md).
+set -o pipefail
+out=gpurun_out/r4pub_full
+mkdir -p $out
+# progress marker for the box's idle detector (every step below has its own time limit)
+(while sleep 45; do date +%T >> $out/heartbeat.txt; done) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
+timeout -k 10 600 python -u scripts/bench_sgd.py --users 9520495 --items 999933 --ratings 2000000000 --rank 2000 \
+  --epochs 2 --warmup 1 --lr 0.001 --lam 0.01 > $out/sgd_r2000.log 2>&1
+rc=$?; echo "sgd rc=$rc" >> $out/status.txt; [ $rc -le 1 ] || exit $rc
+
+timeout -k 10 300 python -u scripts/bench_ccd.py --users 9520495 --items 999933 --ratings 1e9 --rank 120 \
+  --iters 2 > $out/ccd_r120.log 2>&1
+rc=$?; echo "ccd rc=$rc" >> $out/status.txt; [ $rc -le 1 ] || exit $rc
+
+timeout -k 10 360 python -u scripts/bench_lda.py --docs 4.76e6 --vocab 999933 --topics 10000 --len 392 --iters 2 \
+  --warmup 1 --strategy rotation > $out/lda_k10000.log 2>&1
+rc=$?
+echo "rc=$rc" >> $out/status.txt
+exit $rc

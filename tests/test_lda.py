@@ -99,6 +99,32 @@ def test_doc_index_build_and_sync():
     assert torch.equal(di.zdoc[di.tpos[:100]].int(), tz[:100])
 
 
+@pytest.mark.parametrize("n,keys,chunk", [(5000, 37, 700), (4096, 4096, 1000), (300, 5, 1 << 30), (1001, 2, 1000)])
+def test_argsort_small_keys_chunked_is_the_stable_order(n, keys, chunk):
+    """Past torch's per-call sort limit (an 8-GPU clueweb1 share has 3.7e9 tokens) keys are
+    sorted in chunks and merged by key runs: the result must be the global stable order."""
+    from harp_amd.ops.sorting import argsort_small_keys
+
+    x = torch.randint(0, keys, (n,), generator=torch.Generator().manual_seed(n), dtype=torch.int32)
+    assert torch.equal(argsort_small_keys(x, keys, chunk=chunk), torch.sort(x, stable=True).indices)
+
+
+def test_doc_loglik_from_doc_lists_equals_dense_table():
+    """The sparse sampler keeps no dense doc-topic table on the GPU; the doc part of the
+    log-likelihood then comes from the doc-order topic lists and must equal the dense form."""
+    g = torch.Generator().manual_seed(3)
+    nd, K = 40, 10000
+    tdoc = torch.randint(0, nd - 2, (3000,), generator=g, dtype=torch.int32)  # two empty docs
+    tz = torch.randint(0, 60, (3000,), generator=g, dtype=torch.int32) * 160 + 7  # topics up to 9447
+    di = L.DocIndex.build(tdoc, tz, nd)
+    ndk = torch.zeros((nd, L.padded_topics(K)), dtype=torch.int32)
+    L.count(tdoc, None, tz, ndk)
+    dense = L.loglik_terms(ndk, 0.005, K)
+    for block in (1 << 26, 97):  # one block, and many doc blocks
+        sparse = L.doc_loglik_terms(di, 0.005, K, block_tokens=block)
+        assert torch.allclose(sparse, dense, rtol=1e-12, atol=1e-6), (sparse, dense)
+
+
 def test_padded_topics_large_k():
     assert L.padded_topics(1000) == 1024
     assert L.padded_topics(1025) == 1152 and L.padded_topics(10000) == 10112

@@ -19,6 +19,33 @@ def test_lda_gpu_matches_cpu_quality(cuda, K):
     assert abs(lg - lc) / n < 0.1, (lg, lc)
 
 
+@pytest.mark.parametrize("strategy", ["rotation", "push_pull"])
+def test_sparse_sampler_keeps_no_dense_doc_table(cuda, strategy):
+    """K > 1024 on the GPU: the sparse sampler runs from the doc-order topic lists alone (no
+    [docs, K_pad] table, 20 KB per doc at K = 10,000); the doc-order lists stay equal to the
+    token topics and the model's log-likelihood equals the one from a dense recount."""
+    from harp_amd.models.lda import LDAPushPullMapper
+    from harp_amd.models.lda import LDACollectiveMapper
+    from harp_amd.ops import lda as L
+    from harp_amd.runtime.mapper import KeyValReader
+
+    toks = synthetic_corpus(1500, 3000, 20, 60, seed=6)
+    K = 2000
+    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=3, print_interval=3, block_words=512)
+    cls = LDACollectiveMapper if strategy == "rotation" else LDAPushPullMapper
+    m = cls(Communicator(device=cuda), cfg, 1500, 3000, toks)
+    m.run(KeyValReader([]))
+    assert m.sparse and m.ndk is None and m._tokens is None
+    di = m.doc_index
+    assert torch.equal(di.zdoc[di.tpos].int() & 0xFFFF, m.tz)
+    ndk = torch.zeros((m.ndoc_local, m.Kp), dtype=torch.int32, device=cuda)
+    L.count(m.tdoc, None, m.tz, ndk)
+    dense = L.loglik_terms(ndk, cfg.alpha, K)
+    assert torch.allclose(m._doc_loglik(), dense, rtol=1e-12, atol=1e-6)
+    ll = [v for _, v in m.result["loglik"]]
+    assert len(ll) == 1 and ll[0] < 0
+
+
 def test_lda_push_pull_gpu(cuda):
     from harp_amd.models.lda import LDAConfig, LDAPushPullMapper, synthetic_corpus
     from harp_amd.parallel.comm import Communicator
