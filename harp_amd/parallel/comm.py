@@ -117,6 +117,21 @@ def parse_nodes_file(text: str) -> List[List[str]]:
     return racks
 
 
+# dtypes RCCL has no wire type for (ShortArray tables, reference ShortArray): data movement
+# sends their bits as a same-width type; reductions run on an int32 / int64 copy
+_NCCL_BITS = {torch.int16: torch.float16}
+for _n, _w in (("uint16", torch.float16), ("uint32", torch.int32), ("uint64", torch.int64)):
+    if hasattr(torch, _n):
+        _NCCL_BITS[getattr(torch, _n)] = _w
+_NCCL_WIDE = {torch.int16: torch.int32}
+
+
+def nccl_wire(t: torch.Tensor) -> torch.Tensor:
+    """``t`` itself, or a same-width view RCCL can move (bit-exact: no arithmetic)."""
+    w = _NCCL_BITS.get(t.dtype)
+    return t if w is None else t.view(w)
+
+
 class Communicator:
     """A torch.distributed group plus the device its buffers live on."""
 
@@ -208,6 +223,15 @@ class Communicator:
         fn(d)
         t.copy_(d.cpu())
 
+    def _wire(self, t: torch.Tensor) -> torch.Tensor:
+        return nccl_wire(t) if self.dev_stage else t
+
+    def _widened(self, t: torch.Tensor, fn) -> None:
+        """A reduction of a dtype RCCL cannot reduce (int16) on a widened copy."""
+        w = t.to(_NCCL_WIDE[t.dtype])
+        fn(w)
+        t.copy_(w)
+
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
         self._hook("all_reduce")
         if self.world_size > 1:
@@ -215,6 +239,8 @@ class Communicator:
                 return self._host(t, lambda h: dist.all_reduce(h, op=op, group=self.group))
             if self._on_host(t):
                 return self._dev(t, lambda d: dist.all_reduce(d, op=op, group=self.group))
+            if self.dev_stage and t.dtype in _NCCL_WIDE:
+                return self._widened(t, lambda w: dist.all_reduce(w, op=op, group=self.group))
             return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
         return None
 
@@ -225,7 +251,7 @@ class Communicator:
                 return self._host(t, lambda h: dist.broadcast(h, src=self.global_rank(root), group=self.group))
             if self._on_host(t):
                 return self._dev(t, lambda d: dist.broadcast(d, src=self.global_rank(root), group=self.group))
-            return dist.broadcast(t, src=self.global_rank(root), group=self.group, async_op=async_op)
+            return dist.broadcast(self._wire(t), src=self.global_rank(root), group=self.group, async_op=async_op)
         return None
 
     def reduce(self, t: torch.Tensor, root: int, op=dist.ReduceOp.SUM):
@@ -235,6 +261,8 @@ class Communicator:
                 return self._host(t, lambda h: dist.reduce(h, dst=self.global_rank(root), op=op, group=self.group))
             if self._on_host(t):
                 return self._dev(t, lambda d: dist.reduce(d, dst=self.global_rank(root), op=op, group=self.group))
+            if self.dev_stage and t.dtype in _NCCL_WIDE:
+                return self._widened(t, lambda w: dist.reduce(w, dst=self.global_rank(root), op=op, group=self.group))
             dist.reduce(t, dst=self.global_rank(root), op=op, group=self.group)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
@@ -250,7 +278,7 @@ class Communicator:
                 dist.all_gather_into_tensor(do, inp.to(self.device), group=self.group)
                 out.copy_(do)
                 return None
-            return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
+            return dist.all_gather_into_tensor(self._wire(out), self._wire(inp), group=self.group, async_op=async_op)
         out.copy_(inp.reshape(out.shape))
         return None
 
@@ -267,6 +295,11 @@ class Communicator:
                 do = torch.empty(out.shape, dtype=out.dtype, device=self.device)
                 dist.reduce_scatter_tensor(do, inp.to(self.device), op=op, group=self.group)
                 out.copy_(do)
+                return None
+            if self.dev_stage and out.dtype in _NCCL_WIDE:
+                w = torch.empty(out.shape, dtype=_NCCL_WIDE[out.dtype], device=out.device)
+                dist.reduce_scatter_tensor(w, inp.to(w.dtype), op=op, group=self.group)
+                out.copy_(w)
                 return None
             return dist.reduce_scatter_tensor(out, inp, op=op, group=self.group, async_op=async_op)
         out.copy_(inp.reshape(out.shape))
@@ -286,7 +319,7 @@ class Communicator:
                 dist.all_to_all_single(do, inp.to(self.device), out_splits, in_splits, group=self.group)
                 out.copy_(do)
                 return
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            dist.all_to_all_single(self._wire(out), self._wire(inp), out_splits, in_splits, group=self.group)
         else:
             out.copy_(inp)
 
@@ -299,9 +332,9 @@ class Communicator:
             return self._device_p2p({d: [t] for d, t in sends.items()}, {s: [t] for s, t in recvs.items()})
         ops = []
         for dst, t in sends.items():
-            ops.append(dist.P2POp(dist.isend, t, self.global_rank(dst), self.group))
+            ops.append(dist.P2POp(dist.isend, self._wire(t), self.global_rank(dst), self.group))
         for src, t in recvs.items():
-            ops.append(dist.P2POp(dist.irecv, t, self.global_rank(src), self.group))
+            ops.append(dist.P2POp(dist.irecv, self._wire(t), self.global_rank(src), self.group))
         if not ops:
             return []
         works = dist.batch_isend_irecv(ops)
@@ -361,10 +394,10 @@ class Communicator:
         ops = []
         for dst, ts in sends.items():
             for t in ts:
-                ops.append(dist.P2POp(dist.isend, t, self.global_rank(dst), self.group))
+                ops.append(dist.P2POp(dist.isend, self._wire(t), self.global_rank(dst), self.group))
         for src, ts in recvs.items():
             for t in ts:
-                ops.append(dist.P2POp(dist.irecv, t, self.global_rank(src), self.group))
+                ops.append(dist.P2POp(dist.irecv, self._wire(t), self.global_rank(src), self.group))
         if not ops:
             return []
         works = dist.batch_isend_irecv(ops)

@@ -329,9 +329,10 @@ def _alltoall_rows(comm: Communicator, send: torch.Tensor, send_counts, recv_cou
     recv = torch.empty((sum(recv_counts),) + shape, dtype=like.dtype, device=dev)
     if sum(send_counts) or sum(recv_counts):
         s = send.contiguous().to(dev)
-        if s.dtype == torch.bool:
+        if s.dtype == torch.bool:  # both sides as uint8 bytes (same width)
             s = s.to(torch.uint8)
-        comm.all_to_all_single(recv, s, list(recv_counts), list(send_counts))
+        comm.all_to_all_single(recv.view(torch.uint8) if recv.dtype == torch.bool else recv, s,
+                               list(recv_counts), list(send_counts))
     return recv if recv.device == like.device else recv.to(like.device)
 
 

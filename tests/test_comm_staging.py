@@ -67,3 +67,50 @@ def _dev_stage_worker(comm):
 def test_nccl_host_tensor_staging_matches_direct():
     for o in launch(_dev_stage_worker, 3, timeout=300):
         assert o[False] == o[True]
+
+
+def _int16_wire_worker(comm):
+    """RCCL has no int16 type (ShortArray tables): under nccl, data movement sends the bits
+    as float16 and reductions run on an int32 copy. Forced here on gloo CPU ranks (the
+    device-copy path switched off, so the wire-type path itself runs)."""
+    comm.dev_stage = True
+    comm._on_host = lambda *ts: False
+    P, r = comm.world_size, comm.rank
+    res = {}
+    t = torch.tensor([30000, -30000, 7 + r, -1], dtype=torch.int16)
+    a = t.clone()
+    comm.all_reduce(a, op=torch.distributed.ReduceOp.MAX)
+    res["max"] = a.tolist()
+    s = torch.tensor([1000 * (r + 1), -5], dtype=torch.int16)
+    comm.all_reduce(s)
+    res["sum"] = s.tolist()
+    b = torch.tensor([-32768, 32767, r, 0x7C01 - 65536 * 0], dtype=torch.int16)  # NaN bit pattern in fp16
+    comm.broadcast(b, 1)
+    res["bcast"] = b.tolist()
+    g = torch.empty(2 * P, dtype=torch.int16)
+    comm.all_gather_into(g, torch.tensor([-r - 1, 0x7E00 + r], dtype=torch.int16))
+    res["gather"] = g.tolist()
+    o = torch.empty(2, dtype=torch.int16)
+    comm.reduce_scatter(o, torch.arange(2 * P, dtype=torch.int16) * (r + 1))
+    res["rs"] = o.tolist()
+    x = torch.empty(P, dtype=torch.int16)
+    comm.all_to_all_single(x, (torch.arange(P, dtype=torch.int16) - 100 * r))
+    res["a2a"] = x.tolist()
+    rv = torch.empty(3, dtype=torch.int16)
+    comm.sendrecv({(r + 1) % P: torch.tensor([r, -r, 0x7C01], dtype=torch.int16)}, {(r - 1) % P: rv})
+    res["ring"] = rv.tolist()
+    return res
+
+
+def test_int16_tables_travel_bit_exact_on_the_rccl_wire_path():
+    P = 2
+    out = launch(_int16_wire_worker, P, timeout=300)
+    for r, o in enumerate(out):
+        assert o["max"] == [30000, -30000, 7 + P - 1, -1]
+        assert o["sum"] == [1000 * P * (P + 1) // 2, -5 * P]
+        assert o["bcast"] == [-32768, 32767, 1, 0x7C01]
+        assert o["gather"] == [v for q in range(P) for v in (-q - 1, 0x7E00 + q)]
+        assert o["rs"] == [(2 * r + j) * P * (P + 1) // 2 for j in range(2)]
+        assert o["a2a"] == [r - 100 * q for q in range(P)]
+        q = (r - 1) % P
+        assert o["ring"] == [q, -q, 0x7C01]
