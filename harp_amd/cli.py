@@ -16,6 +16,8 @@ same parameters as named flags (which win when both are given):
   subgraph  <maps> <useLocalMultiThread> <template> <graphDir> <outDir> <threads> <cores>
             <affinity> <tpc> <memMB> <sendArrayLimit> <rotationPipeline> <iters>
             (ml/java subgraph/SCLauncher.java:76-88)                       [--strategy]
+  ldacvb    <inputDir> <metafile> <outputDir> <numTerms> <numTopics> <numDocs> <maps> <iters>
+            <threads> <mode>                 (contrib lda/LdaMapCollective.java, ldacvb.sh)
   pagerank  <inputDir> <numUrls> <iters> <maps>   (contrib simplepagerank)
   daal      <algo> <maps> <threads> <memMB> <iters> <inputDir> <workDir> [algo args]
             (harp-daal-interface data_aux/Initialize.java:97-130 common prefix)
@@ -59,6 +61,9 @@ SPECS: Dict[str, List[Tuple[str, type, Any]]] = {
                  ("out_dir", str, "harp-work/subgraph"), ("threads", int, 1), ("cores", int, 1), ("affinity", str, ""),
                  ("tpc", int, 1), ("mem", int, 0), ("send_array_limit", int, 0), ("rotation_pipeline", str, "false"),
                  ("iterations", int, 1)],
+    "ldacvb": [("input_dir", str, ""), ("metafile", str, ""), ("output_dir", str, "harp-work/ldacvb"),
+               ("num_terms", int, 0), ("num_topics", int, 10), ("num_docs", int, 0), ("maps", int, 2),
+               ("iterations", int, 5), ("threads", int, 1), ("mode", int, 1)],
     "pagerank": [("input_dir", str, ""), ("num_urls", int, 0), ("iterations", int, 10), ("maps", int, 2)],
     "daal": [("algo", str, "pca"), ("maps", int, 2), ("threads", int, 1), ("mem", int, 0), ("iterations", int, 10),
              ("input_dir", str, ""), ("work_dir", str, "harp-work/daal")],
@@ -67,6 +72,8 @@ EXTRA = {  # named-only flags
     "kmeans": [("strategy", str, "regroup_allgather")],
     "subgraph": [("strategy", str, "allgather"), ("seed", int, 0)],
     "lda": [("vocab", int, 0)],
+    "ldacvb": [("strategy", str, "allreduce"), ("init", str, "random"), ("alpha", float, 1e-3), ("eta", float, 0.0),
+               ("gamma_iters", int, 29)],
     "sgd": [("num_users", int, 0), ("num_items", int, 0)],
     "ccd": [("num_users", int, 0), ("num_items", int, 0)],
     "daal": [("k", int, 0), ("method", str, ""), ("label_cols", int, 1)],
@@ -249,6 +256,36 @@ def _run_lda(comm, cfg):
     if comm.rank == 0:
         _write(os.path.join(cfg["work_dir"], "likelihood"), "\n".join(f"{i} {v}" for i, v in res["loglik"]) + "\n")
     return res
+
+
+def _run_ldacvb(comm, cfg):
+    """Variational LDA on term-count documents (contrib LdaMapCollective: input dir, HDFS
+    metafile of ``<file> <first doc>`` lines, output dir, terms, topics, docs, maps,
+    iterations, threads, mode). Writes ``likelihood`` (iteration, bound, seconds) and
+    ``alpha`` to the output dir."""
+    from .models.lda_vb import LDAVBConfig, train_lda_vb
+    from .utils.datasets import load_term_count_docs
+
+    meta = cfg["metafile"]
+    if meta and not os.path.isabs(meta) and not os.path.exists(meta):
+        meta = os.path.join(cfg["input_dir"], meta)
+    meta_name = os.path.basename(meta) if meta else ""
+    files = [f for f in _my_files(comm, cfg["input_dir"]) if os.path.basename(f) != meta_name]
+    doc, word, cnt = load_term_count_docs(sorted(files), meta if meta and os.path.exists(meta) else None)
+    docs, local = torch.unique(doc, return_inverse=True)
+    vocab = cfg["num_terms"] or _allmax(comm, int(word.max()) + 1 if word.numel() else 0)
+    # the reference's settings: alpha 1e-3 (LDAMapper.java:99-106), maximum-likelihood beta
+    # (no smoothing), 29 gamma passes per document (Constants.MAX_GAMMA_ITERATIONS = 30);
+    # --init uniform also starts from its uniform beta (which keeps every topic identical)
+    vc = LDAVBConfig(num_topics=cfg["num_topics"], iterations=cfg["iterations"], strategy=cfg["strategy"],
+                     alpha=cfg["alpha"], eta=cfg["eta"], gamma_iters=cfg["gamma_iters"], gamma_tol=0.0,
+                     init=cfg["init"])
+    res = train_lda_vb(comm, local, word, cnt, docs.numel(), vocab, vc)
+    if comm.rank == 0:
+        _write(os.path.join(cfg["output_dir"], "likelihood"),
+               "".join(f"{h['iter']} {h['elbo']} {h['time_s']}\n" for h in res["history"]))
+        _write(os.path.join(cfg["output_dir"], "alpha"), " ".join(f"{a:.9g}" for a in res["alpha"].tolist()) + "\n")
+    return {"history": res["history"], "num_docs": int(docs.numel()), "vocab": vocab}
 
 
 def load_mds_block(folder: str, prefix: str, ids_file: str):

@@ -46,6 +46,9 @@ class LDAVBConfig:
     strategy: str = "allreduce"  # or "push_pull"
     block: int = 256             # words per push/pull partition
     seed: int = 0
+    init: str = "random"         # "uniform": the reference's start (every log beta 0.1, then
+                                 # normalised: LDAMapper.java:113-130), which keeps the topics
+                                 # symmetric for good
 
 
 def _estep(doc, word, cnt, n_docs, log_beta, alpha, cfg):
@@ -67,6 +70,21 @@ def _estep(doc, word, cnt, n_docs, log_beta, alpha, cfg):
     logz = torch.logsumexp(lphi, 1)
     phi = torch.exp(lphi - logz[:, None])
     return gamma, phi, logz
+
+
+def _elbo_terms(doc, cnt, gamma, logz, alpha, n_docs):
+    """The variational bound of this worker's documents as (doc part, word part): the doc
+    part from gamma, the word part sum_w n_w sum_k phi (log beta + E log theta - log phi) =
+    n_w (logz_w - digamma(sum_k gamma_dk)), logz over log beta + digamma(gamma). At the gamma
+    fixed point it equals the reference's per-document likelihood (LDAMapper.java:239-344,
+    updatePhi :679-717: lnG(sum alpha) - sum lnG(alpha) + sum lnG(gamma) - lnG(sum gamma)
+    + sum_w n_w sum_k phi (log beta - log phi))."""
+    dsum = torch.digamma(gamma.sum(1, keepdim=True))
+    lg = (torch.lgamma(alpha.sum()) - torch.lgamma(alpha).sum()) * n_docs
+    lg = lg + ((alpha - gamma) * (torch.digamma(gamma) - dsum)).sum()
+    lg = lg + (torch.lgamma(gamma).sum() - torch.lgamma(gamma.sum(1)).sum())
+    lw = (cnt * (logz - dsum[:, 0][doc])).sum()
+    return lg, lw
 
 
 def _alpha_newton(alpha, ss, D, iters=20):
@@ -96,7 +114,10 @@ def train_lda_vb(comm: Communicator, doc: torch.Tensor, word: torch.Tensor, cnt:
     K = cfg.num_topics
     doc, word, cnt = doc.to(dev), word.to(dev), cnt.to(dev, dt)
     g = torch.Generator().manual_seed(cfg.seed)
-    beta = torch.rand((K, vocab), generator=g, dtype=dt) + 1.0
+    if cfg.init == "uniform":
+        beta = torch.ones((K, vocab), dtype=dt)
+    else:
+        beta = torch.rand((K, vocab), generator=g, dtype=dt) + 1.0
     log_beta = (beta / beta.sum(1, keepdim=True)).log().to(dev)
     alpha = torch.full((K,), cfg.alpha, dtype=dt, device=dev)
     D = float(reduce_partials(comm, {"d": torch.tensor([float(n_docs_local)])})["d"][0])
@@ -109,11 +130,7 @@ def train_lda_vb(comm: Communicator, doc: torch.Tensor, word: torch.Tensor, cnt:
         S = torch.zeros((K, vocab), dtype=dt, device=dev)
         S.index_add_(1, word, (cnt[:, None] * phi).t())
         ss = (torch.digamma(gamma) - torch.digamma(gamma.sum(1, keepdim=True))).sum(0)
-        # ELBO pieces (word part; doc part from gamma)
-        lg = (torch.lgamma(alpha.sum()) - torch.lgamma(alpha).sum()) * n_docs_local
-        lg = lg + ((alpha - gamma) * (torch.digamma(gamma) - torch.digamma(gamma.sum(1, keepdim=True)))).sum()
-        lg = lg + (torch.lgamma(gamma).sum() - torch.lgamma(gamma.sum(1)).sum())
-        lw = (cnt * logz).sum()
+        lg, lw = _elbo_terms(doc, cnt, gamma, logz, alpha, n_docs_local)
         if cfg.strategy == "push_pull" and comm.world_size > 1:
             # normaliser = global row sums (allreduce of K values), statistics by push/pull
             red = reduce_partials(comm, {"ss": ss, "ll": (lg + lw).reshape(1), "norm": S.sum(1)})

@@ -209,6 +209,42 @@ def load_libsvm(path: str, n_features: Optional[int] = None, threads: int = 8) -
     return X, torch.tensor(ys)
 
 
+def load_term_count_docs(files: List[str], metadata: Optional[str] = None):
+    """Contrib LDA-CVB input (datasets/tutorial/lda-cvb, contrib lda/LDAMapper.java): one
+    document per line as ``termId:count`` pairs; the metadata file's lines
+    ``<file name> <first doc index>`` place each file's documents in the global numbering
+    (files it does not name keep the order given). Returns global (doc, term, count)."""
+    import os
+
+    start = {}
+    if metadata:
+        with open(metadata) as f:
+            for ln in f:
+                t = ln.split()
+                if len(t) >= 2:
+                    start[t[0]] = int(t[1])
+    docs, terms, cnts = [], [], []
+    nxt = 0
+    for path in files:
+        d0 = start.get(os.path.basename(path), nxt)
+        n = 0
+        with open(path) as f:
+            for ln in f:
+                t = ln.split()
+                if not t:
+                    continue
+                for pair in t:
+                    w, c = pair.split(":")
+                    if int(c) > 0:
+                        docs.append(d0 + n)
+                        terms.append(int(w))
+                        cnts.append(float(c))
+                n += 1
+        nxt = max(nxt, d0 + n)
+    return (torch.tensor(docs, dtype=torch.long), torch.tensor(terms, dtype=torch.long),
+            torch.tensor(cnts, dtype=torch.float64))
+
+
 def shard(n: int, rank: int, world: int) -> slice:
     """Contiguous row block of this worker."""
     return slice(rank * n // world, (rank + 1) * n // world)

@@ -50,3 +50,28 @@ def test_lda_vb_distributed_strategies_agree():
         assert torch.allclose(ga, gp, atol=1e-9)
         assert abs(ea - single["history"][-1]["elbo"]) < 1e-6 * abs(ea)
         assert torch.allclose(ga, single["gamma"][r::2], atol=1e-8)
+
+
+def test_bound_is_the_reference_likelihood_at_the_gamma_fixed_point():
+    """The per-iteration bound equals the reference's document likelihood (contrib
+    LDAMapper.java:239-344: lnG(sum a) - sum lnG(a) + sum lnG(g) - lnG(sum g) + sum_w n_w
+    sum_k phi (log beta - log phi)) once gamma has converged, and is a proper (negative)
+    log-likelihood bound."""
+    import torch
+
+    g = torch.Generator().manual_seed(2)
+    nd, V_, K = 30, 50, 4
+    doc = torch.randint(0, nd, (400,), generator=g)
+    word = torch.randint(0, V_, (400,), generator=g)
+    cnt = torch.randint(1, 4, (400,), generator=g).double()
+    beta = torch.rand((K, V_), generator=g, dtype=torch.float64) + 0.5
+    log_beta = (beta / beta.sum(1, keepdim=True)).log()
+    alpha = torch.full((K,), 0.3, dtype=torch.float64)
+    cfg = V.LDAVBConfig(num_topics=K, gamma_iters=2000, gamma_tol=1e-14)
+    gamma, phi, logz = V._estep(doc, word, cnt, nd, log_beta, alpha, cfg)
+    lg, lw = V._elbo_terms(doc, cnt, gamma, logz, alpha, nd)
+    ref = nd * (torch.lgamma(alpha.sum()) - torch.lgamma(alpha).sum())
+    ref = ref + torch.lgamma(gamma).sum() - torch.lgamma(gamma.sum(1)).sum()
+    ref = ref + (cnt[:, None] * phi * (log_beta[:, word].t() - phi.log())).sum()
+    assert abs(float(lg + lw) - float(ref)) < 1e-9 * abs(float(ref))
+    assert float(lg + lw) < 0

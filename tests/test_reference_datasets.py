@@ -188,3 +188,23 @@ def test_random_forest_airline_fixture():
     assert len(forests[0].trees) == len(forests[1].trees) == 16
     acc = float((forests[0].predict(Xte) == yte).float().mean())
     assert acc > 0.97, acc
+
+
+def test_lda_cvb_reference_sample_through_cli(tmp_path):
+    """contrib LDA-CVB's own test input (ldacvb.sh 'sample': 12 docs over 11 terms in two
+    files placed by a metadata file) through the reference's positional command line
+    (``<in> <meta> <out> 11 2 12 2 5 4 1``, two workers): every doc and count is loaded,
+    and the bound (the reference's likelihood) is negative and rises over the 5 iterations."""
+    from harp_amd import cli
+    from harp_amd.utils.datasets import load_term_count_docs
+
+    d = os.path.join(ROOT, "tutorial", "lda-cvb", "sample-sparse-data")
+    files = sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".txt"))
+    doc, word, cnt = load_term_count_docs(files, os.path.join(d, "sample-sparse-metadata"))
+    assert int(doc.max()) + 1 == 12 and int(word.max()) + 1 == 11 and int(cnt.sum()) == 260
+    out = tmp_path / "out"
+    assert cli.main(["ldacvb", d, os.path.join(d, "sample-sparse-metadata"), str(out), "11", "2", "12", "2", "5", "4",
+                     "1", "--backend", "gloo"]) == 0
+    rows = [ln.split() for ln in (out / "likelihood").read_text().splitlines()]
+    ll = [float(r[1]) for r in rows]
+    assert len(ll) == 5 and all(v < 0 for v in ll) and ll[-1] > ll[0]
