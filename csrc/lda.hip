@@ -559,13 +559,36 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         int f = z;
         if (lane == src) {
           float pre = inclb - sb;
-          for (long j = lo + lane; j < hi; j += 64) {
+          bool done = false;
+          for (int q = 0; q < 2 && !done; ++q) {  // the two entries held in registers
+            const long j = lo + lane + 64 * q;
+            if (j >= hi) break;
             if (j == p) continue;
-            const long o = j - lo - lane;  // 0, 64, 128, ...: registers for the first two
-            const int zj = o == 0 ? zv0 : o == 64 ? zv1 : (int)__builtin_nontemporal_load(zdoc + j);
+            const int zj = q == 0 ? zv0 : zv1;
             f = zj;
             pre += zj == z ? qz : s_qw[zj];
-            if (pre > u) break;
+            done = pre > u;
+          }
+          long j = lo + lane + 128;
+          for (; !done && j + 192 < hi; j += 256) {  // then four loads per round trip
+            int zq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) zq[q] = __builtin_nontemporal_load(zdoc + j + 64 * q);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (!done && j + 64 * q != p) {
+                f = zq[q];
+                pre += zq[q] == z ? qz : s_qw[zq[q]];
+                done = pre > u;
+              }
+            }
+          }
+          for (; !done && j < hi; j += 64) {
+            if (j == p) continue;
+            const int zj = __builtin_nontemporal_load(zdoc + j);
+            f = zj;
+            pre += zj == z ? qz : s_qw[zj];
+            done = pre > u;
           }
         }
         nz = __builtin_amdgcn_readlane(f, src);
