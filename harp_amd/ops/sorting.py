@@ -13,8 +13,10 @@ import torch
 SORT_CHUNK = 1 << 30
 
 
-def argsort_small_keys(keys: torch.Tensor, nkeys: int, chunk: int = SORT_CHUNK) -> torch.Tensor:
-    """int64 permutation ``order`` with ``keys[order]`` ascending and ties in input order."""
+def argsort_small_keys(keys: torch.Tensor, nkeys: int, chunk: int = 0) -> torch.Tensor:
+    """int64 permutation ``order`` with ``keys[order]`` ascending and ties in input order
+    (``chunk``: elements per sort call, default SORT_CHUNK)."""
+    chunk = chunk if chunk > 0 else SORT_CHUNK
     E = keys.numel()
     dev = keys.device
     if E <= chunk:

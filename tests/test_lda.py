@@ -170,3 +170,30 @@ def test_lda_large_k_rotation_two_workers(corpus):
         assert ok and sparse and tot == corpus[0].numel()
     ll = [v for _, v in res[0][0]["loglik"]]
     assert ll[-1] > ll[0] and res[1][0]["loglik"] == res[0][0]["loglik"]
+
+
+def test_lda_init_past_the_sort_limit(corpus, monkeypatch):
+    """Model init on the chunked-sort path (forced with a 1000-element 'sort limit'): the
+    token order is the stable word order, the doc index the stable doc order, and the
+    counts are complete."""
+    from harp_amd.models import lda as LM
+    from harp_amd.ops import sorting
+    from harp_amd.parallel.comm import Communicator
+    from harp_amd.runtime.mapper import KeyValReader
+
+    cfg = LDAConfig(num_topics=2000, alpha=0.01, beta=0.01, iterations=1)
+    ref = LM.LDACollectiveMapper(Communicator(), cfg, 300, 400, corpus)
+    ref.init_model(KeyValReader([]))
+    monkeypatch.setattr(sorting, "SORT_CHUNK", 1000)
+    monkeypatch.setattr(LM, "SORT_CHUNK", 1000)
+    m = LM.LDACollectiveMapper(Communicator(), cfg, 300, 400, corpus)
+    m.init_model(KeyValReader([]))
+    assert m.tdoc.numel() == corpus[0].numel() > 1000
+    key = m.tword.long() + torch.repeat_interleave(torch.arange(len(m.offsets) - 1),
+                                                   torch.tensor(m.offsets).diff()) * m.vps
+    assert bool((key[1:] >= key[:-1]).all())  # word-sorted
+    assert torch.equal(torch.sort(m.tword + 0, stable=True)[0], torch.sort(ref.tword + 0, stable=True)[0])
+    assert m.offsets == ref.offsets and int(m.nk.sum()) == corpus[0].numel()
+    di = m.doc_index
+    assert torch.equal(di.doc_off, ref.doc_index.doc_off)
+    assert torch.equal(di.zdoc[di.tpos].int(), m.tz)
