@@ -199,6 +199,90 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const __bf16* __restri
   (void)SPW;
 }
 
+// Rows wider than 256 columns (the wide-row K-means, d up to 1024 per call): one wave per
+// slot, each lane VEC 16-B chunks of the row (chunk c of lane l at column 8 * (64 c + l), so
+// each chunk index is one contiguous 1 KB read per wave), ROWS rows in flight; one pass over
+// the permutation instead of one per 256-column slice.
+template <int VEC, int RUN, int ROWS = 4>
+__global__ __launch_bounds__(256) void rowsum_wide_bf16_kernel(const __bf16* __restrict__ X, int dp, long ldx,
+                                                               const int* __restrict__ perm,
+                                                               const int* __restrict__ start, int K, long n,
+                                                               float* __restrict__ sums, int ld) {
+  const int lane = threadIdx.x & 63;
+  const long slot = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long j0 = slot * RUN;
+  if (j0 >= n) return;
+  long j1 = j0 + RUN;
+  if (j1 > n) j1 = n;
+  bool active[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) active[c] = (64 * c + lane) * 8 < dp;
+  int lo = 0, hi = K;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (start[mid] <= j0) lo = mid; else hi = mid;
+  }
+  int k = lo;
+  long kend = start[k + 1];
+  float acc[VEC][8];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[c][e] = 0.f;
+  auto flush = [&](int kk) {
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) {
+      if (active[c]) {
+        float* o = sums + (long)kk * ld + (64 * c + lane) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (acc[c][e] != 0.f) atomicAdd(o + e, acc[c][e]);
+          acc[c][e] = 0.f;
+        }
+      }
+    }
+  };
+  long j = j0;
+  while (j < j1) {
+    while (j >= kend) {
+      flush(k);
+      ++k;
+      kend = start[k + 1];
+    }
+    const long stop = kend < j1 ? kend : j1;
+    for (; j + ROWS <= stop; j += ROWS) {
+      int pj[ROWS];
+#pragma unroll
+      for (int q = 0; q < ROWS; ++q) pj[q] = perm[j + q];
+      bf16x8 v[ROWS][VEC];
+#pragma unroll
+      for (int q = 0; q < ROWS; ++q)
+#pragma unroll
+        for (int c = 0; c < VEC; ++c)
+          v[q][c] = active[c] ? *(const bf16x8*)(X + (long)pj[q] * ldx + (64 * c + lane) * 8) : bf16x8{};
+#pragma unroll
+      for (int c = 0; c < VEC; ++c)
+#pragma unroll
+        for (int q = 0; q < ROWS; q += 4)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            acc[c][e] += ((float)v[q][c][e] + (float)v[q + 1][c][e]) + ((float)v[q + 2][c][e] + (float)v[q + 3][c][e]);
+    }
+    for (; j < stop; ++j) {
+      const long r = perm[j];
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) {
+        if (active[c]) {
+          const bf16x8 v = *(const bf16x8*)(X + r * ldx + (64 * c + lane) * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[c][e] += (float)v[e];
+        }
+      }
+    }
+  }
+  flush(k);
+}
+
 }  // namespace
 
 // Labels per histogram chunk: 65536 for large n; smaller for small n so the histogram and
@@ -247,7 +331,7 @@ HARP_EXPORT int harp_bucket_labels(const int* lab, long n, int K, int* ws, long*
 // X rows of dp elements at a row stride of ldx >= dp (ldx % 8 == 0).
 HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, long ldx, const int* perm, const int* start, int K,
                                         long n, float* sums, int ld, hipStream_t s) {
-  if (dp % 8 || dp > 256 || ld < dp || ldx < dp || ldx % 8 || n <= 0) return n == 0 ? HARP_OK : HARP_EBADARG;
+  if (dp % 8 || dp > 1024 || ld < dp || ldx < dp || ldx % 8 || n <= 0) return n == 0 ? HARP_OK : HARP_EBADARG;
   const int lpr_min = dp / 8;
   const __bf16* Xb = (const __bf16*)X;
   constexpr int RUN = 256;
@@ -256,6 +340,8 @@ HARP_EXPORT int harp_bucket_rowsum_bf16(const void* X, int dp, long ldx, const i
   // 8 rows in flight at 16 lanes per row (dp 72..128, the K-means headline's 112): 5.13 ->
   // 5.00 ms at N = 1e8, K = 1e4 (profiles/r4_endstate/rowsum_rows.log)
   else if (lpr_min <= 16) rowsum_bf16_kernel<16, RUN, 8><<<grid(16), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
-  else rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
+  else if (lpr_min <= 32) rowsum_bf16_kernel<32, RUN><<<grid(32), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
+  else if (dp <= 512) rowsum_wide_bf16_kernel<1, RUN><<<grid(64), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
+  else rowsum_wide_bf16_kernel<2, RUN><<<grid(64), dim3(256), 0, s>>>(Xb, dp, ldx, perm, start, K, n, sums, ld);
   return harp_launch_status();
 }

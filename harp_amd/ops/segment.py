@@ -7,6 +7,7 @@ See csrc/segsum.hip for why this beats float atomics on gfx950.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Tuple
 
 import torch
@@ -55,6 +56,9 @@ def bucket_labels(labels: torch.Tensor, K: int) -> Tuple[torch.Tensor, torch.Ten
     return ws[po.value:po.value + n], ws[so.value:so.value + K + 1]
 
 
+SUM_SLICE = int(os.environ.get("HARP_ROWSUM_SLICE", "1024"))  # 256: the per-slice form before round 4
+
+
 def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """out[k] += sum of the bucket's rows (zero ``out`` first for a plain sum)."""
     K = start.numel() - 1
@@ -63,9 +67,10 @@ def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out:
         out[:K, : X.shape[1]].index_add_(0, idx, X[perm.long()].float())
         return out
     assert X.dtype == torch.bfloat16 and X.stride(1) == 1 and out.dtype == torch.float32 and out.is_contiguous()
-    # the kernel sums rows of up to 256 columns; wider rows go as 256-column slices
-    for c0 in range(0, X.shape[1], 256):
-        w = min(256, X.shape[1] - c0)
+    # the kernel sums rows of up to SUM_SLICE columns in one pass (one wave per slot past 256
+    # columns); wider rows go as slices
+    for c0 in range(0, X.shape[1], SUM_SLICE):
+        w = min(SUM_SLICE, X.shape[1] - c0)
         st = _lib.kernels().harp_bucket_rowsum_bf16(X[:, c0:].data_ptr(), w, X.stride(0), perm.data_ptr(),
                                                     start.data_ptr(), K, perm.numel(), out[:, c0:].data_ptr(),
                                                     out.stride(0), _lib.stream_ptr(X.device))

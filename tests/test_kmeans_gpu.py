@@ -118,6 +118,26 @@ def test_bucket_labels_and_rowsum(cuda):
     assert torch.allclose(out.double(), ref, rtol=1e-5, atol=1e-2)
 
 
+@pytest.mark.parametrize("dp,slice_", [(264, 1024), (512, 1024), (1000, 1024), (1024, 1024), (2048, 1024), (1000, 256)])
+def test_bucket_rowsum_wide_rows(cuda, monkeypatch, dp, slice_):
+    """Rows wider than 256 columns: the one-pass wave-per-slot gather-sum (slices of up to
+    1024 columns) and the former 256-column slices both equal an fp64 index_add, with a
+    heavy bucket, an empty one, and a row stride wider than the row."""
+    from harp_amd.ops import segment
+
+    monkeypatch.setattr(segment, "SUM_SLICE", slice_)
+    n, K = 40000, 700
+    lab = torch.randint(0, K, (n,), device=cuda, dtype=torch.int32)
+    lab[:9000] = 3
+    lab[lab == 5] = 6
+    perm, start = segment.bucket_labels(lab, K)
+    X = (torch.rand(n, dp + 8, device=cuda) * 10).to(torch.bfloat16)[:, :dp]
+    out = torch.zeros(K, dp, device=cuda)
+    segment.bucket_rowsum(X, perm, start, out)
+    ref = torch.zeros(K, dp, dtype=torch.float64, device=cuda).index_add_(0, lab.long(), X.double())
+    assert torch.allclose(out.double(), ref, rtol=1e-5, atol=1e-2)
+
+
 def test_kmeans_hip_graph_iterations_match_eager(cuda):
     """Iterations replayed from HIP graphs give the same centroids as eager launches."""
     from harp_amd.models.kmeans import KMeansCollectiveMapper, KMeansConfig
