@@ -419,9 +419,11 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 //  * word-row moves go straight to the global n_wk row (two atomics) so chunks of one
 //    word on different workgroups stay exact; doc-topic counts (when kept) and topic-sum
 //    deltas are updated with atomics as in the dense kernel.
-template <int WAVES, class DT>
+// SPAN: tspan[i] = doc_off[doc of token i] | (doc length << 40), precomputed per token, so the
+// next token's doc range needs no dependent doc_off load (no doc-topic table, no doc ids)
+template <int WAVES, class DT, bool SPAN = false>
 __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
-    const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
+    const int* __restrict__ tdoc, const long* __restrict__ tspan, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, const int* __restrict__ order, int* __restrict__ work,
     const long* __restrict__ tpos, const long* __restrict__ doc_off, unsigned short* __restrict__ zdoc,
     DT* __restrict__ ndk, int ldd,
@@ -495,11 +497,17 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     // lo + 64 + lane), loaded one token ahead; the (rare) rest is read in the loop
     int zv0 = 0, zv1 = 0;
     if (i < b) {
-      d = tdoc[i];
       z = tz[i];
       p = tpos[i];
-      lo = doc_off[d];
-      hi = doc_off[d + 1];
+      if constexpr (SPAN) {
+        const long sp = tspan[i];
+        lo = sp & ((1L << 40) - 1);
+        hi = lo + (sp >> 40);
+      } else {
+        d = tdoc[i];
+        lo = doc_off[d];
+        hi = doc_off[d + 1];
+      }
       inv_z = inv_nk[z];
       if (lo + lane < hi) zv0 = __builtin_nontemporal_load(zdoc + lo + lane);
       if (lo + 64 + lane < hi) zv1 = __builtin_nontemporal_load(zdoc + lo + 64 + lane);
@@ -507,9 +515,10 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     for (; i < b; i += WAVES) {
       const long inx = i + WAVES;
       int dn = 0, zn = 0;
-      long pn = 0;
+      long pn = 0, spn = 0;
       if (inx < b) {
-        dn = tdoc[inx];
+        if constexpr (SPAN) spn = tspan[inx];
+        else dn = tdoc[inx];
         zn = tz[inx];
         pn = tpos[inx];
       }
@@ -545,8 +554,13 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       float invn = 0.f;
       int zn0 = 0, zn1 = 0;
       if (inx < b) {
-        lon = doc_off[dn];
-        hin = doc_off[dn + 1];
+        if constexpr (SPAN) {
+          lon = spn & ((1L << 40) - 1);
+          hin = lon + (spn >> 40);
+        } else {
+          lon = doc_off[dn];
+          hin = doc_off[dn + 1];
+        }
         invn = inv_nk[zn];
         // the next token's doc list, in flight while this token samples
         if (lon + lane < hin) zn0 = __builtin_nontemporal_load(zdoc + lon + lane);
@@ -627,7 +641,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         tz[i] = nz;
         if (nz != z) {
           zdoc[p] = (unsigned short)nz;
-          if (ndk) {
+          if (!SPAN && ndk) {
             DocRow<DT>::add(ndk + (long)d * ldd, z, -1);
             DocRow<DT>::add(ndk + (long)d * ldd, nz, 1);
           }
@@ -664,7 +678,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
       }
       // the next token of the same document: its prefetched list missed this token's move
-      if (dn == d && nz != z && inx < b) {
+      if ((SPAN ? lon == lo : dn == d) && nz != z && inx < b) {
         if (lon + lane == p) zn0 = nz;
         if (lon + 64 + lane == p) zn1 = nz;
       }
@@ -793,8 +807,9 @@ size_t sparse_lds_bytes(int Kp, int waves) {
   return (Kp <= 4096 ? 8 : 4) * (size_t)Kp + (wd == 1 ? 4 * (size_t)Kp * waves : wd == 2 ? 4 * (size_t)Kp : 0);
 }
 
-template <int WAVES, class DT>
-int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, const int* order,
+template <int WAVES, class DT, bool SPAN = false>
+int launch_sparse(const int* tdoc, const long* tspan, const int* tword, int* tz, const long* chunk_start, long nchunks,
+                  const int* order,
                   int* work, const long* tpos,
                   const long* doc_off, unsigned short* zdoc, DT* ndk, int ldd, int* nwk, int ldw, const float* inv_nk,
                   int* nk_delta, int K, float alpha, float beta, unsigned long long seed, int det, hipStream_t s) {
@@ -804,7 +819,7 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
   const size_t lds = sparse_lds_bytes(Kp, WAVES);
   // raise the dynamic-LDS cap past 64 KB (per launch: no process-wide cache that a second
   // device or a concurrent caller could skip past)
-  if (lds > 65536 && hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT>,
+  if (lds > 65536 && hipFuncSetAttribute((const void*)lda_cgs_sparse_kernel<WAVES, DT, SPAN>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return HARP_ELAUNCH;
   // grid = resident workgroups (LDS- or wave-slot-bound), striding over the chunks
@@ -814,8 +829,8 @@ int launch_sparse(const int* tdoc, const int* tword, int* tz, const long* chunk_
   long blocks = nchunks;
   if (blocks > 256 * per_cu) blocks = 256 * per_cu;
   if (det) blocks = 1;
-  lda_cgs_sparse_kernel<WAVES, DT><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
-      tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
+  lda_cgs_sparse_kernel<WAVES, DT, SPAN><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
+      tdoc, tspan, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
       beta, seed, ldelta, wdelta);
   return harp_launch_status();
 }
@@ -844,7 +859,7 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
       }
     }
   }
-#define SP_ARGS tdoc, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc
+#define SP_ARGS tdoc, nullptr, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc
 #define SP_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, s
   if (ndk_bits == 16) {
     if (ldd % 2) return HARP_EBADARG;
@@ -873,6 +888,39 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
                        : launch_sparse<8>(SP_ARGS, n32, ldd, SP_TAIL);
 #undef SP_ARGS
 #undef SP_TAIL
+}
+
+// The same sampler with per-token doc spans (tspan[i] = doc_off[d_i] | (len_i << 40)) in place
+// of doc ids, and no doc-topic table: the next token's doc range is one independent load.
+HARP_EXPORT int harp_lda_cgs_sparse_span(const long* tspan, const int* tword, int* tz, const long* chunk_start,
+                                         long nchunks, const int* order, int* work, const long* tpos,
+                                         unsigned short* zdoc, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
+                                         int K, float alpha, float beta, unsigned long long seed, int waves,
+                                         hipStream_t s) {
+  if (nchunks <= 0) return HARP_OK;
+  if (K <= 0 || K > 16384 || ldw < K || !tspan || !tpos || !zdoc || !work) return HARP_EBADARG;
+  const int det = waves < 0 ? 1 : 0;
+  if (det) waves = 1;
+  if (waves == 0) {
+    const int Kp = (K + 63) / 64 * 64;
+    waves = 16;
+    for (int w = 4; w <= 8; w *= 2) {
+      const long per_cu = 163840 / ((long)sparse_lds_bytes(Kp, w) + 1100);
+      if (per_cu * w >= 24) {
+        waves = w;
+        break;
+      }
+    }
+  }
+#define SS_ARGS nullptr, tspan, tword, tz, chunk_start, nchunks, order, work, tpos, nullptr, zdoc, (int*)nullptr, 0
+#define SS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, s
+  return waves == 1    ? launch_sparse<1, int, true>(SS_ARGS, SS_TAIL)
+         : waves == 2  ? launch_sparse<2, int, true>(SS_ARGS, SS_TAIL)
+         : waves == 4  ? launch_sparse<4, int, true>(SS_ARGS, SS_TAIL)
+         : waves == 16 ? launch_sparse<16, int, true>(SS_ARGS, SS_TAIL)
+                       : launch_sparse<8, int, true>(SS_ARGS, SS_TAIL);
+#undef SS_ARGS
+#undef SS_TAIL
 }
 
 HARP_EXPORT int harp_lda_count(const int* tdoc, const int* tword, const int* tz, long n, void* ndk, int ldd,

@@ -14,6 +14,11 @@ _lib.register({
     "harp_lda_cgs": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int,
                      _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
                      _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
+    # tspan, tword, tz, chunks, nchunks, order, work, tpos, zdoc, nwk, ldw, inv_nk, nk_delta, K, alpha, beta,
+    # seed, waves, stream
+    "harp_lda_cgs_sparse_span": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 5 + [
+        _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_ulonglong,
+        _lib.c_int, _lib.c_void_p],
     "harp_lda_cgs_sparse": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 6 + [
         _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
         _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
@@ -79,6 +84,7 @@ class DocIndex:
     zdoc: torch.Tensor     # [n] int16
     doc_off: torch.Tensor  # [n_docs + 1] int64
     tpos: torch.Tensor     # [n] int64
+    span: Optional[torch.Tensor] = None  # [n] int64: doc_off[doc] | (doc length << 40), token order
 
     @staticmethod
     def build(tdoc: torch.Tensor, tz: torch.Tensor, n_docs: int) -> "DocIndex":
@@ -91,11 +97,29 @@ class DocIndex:
         del order
         off = torch.zeros(n_docs + 1, dtype=torch.int64, device=tdoc.device)
         off[1:] = torch.cumsum(torch.bincount(tdoc, minlength=n_docs)[:n_docs], 0)
-        return DocIndex(zdoc, off, tpos)
+        span = None
+        if tdoc.device.type == "cuda" and SPAN:
+            d = tdoc.long()
+            span = off[d] | ((off[d + 1] - off[d]) << 40)
+            del d
+        return DocIndex(zdoc, off, tpos, span)
 
     def sync(self, tz: torch.Tensor, tpos: Optional[torch.Tensor] = None) -> None:
         """Copy assignments ``tz`` (tokens ``tpos``, default all) into the doc-order view."""
         self.zdoc[self.tpos if tpos is None else tpos] = tz.to(torch.int16)
+
+
+def _span_slice(doc_index: "DocIndex", tdoc: torch.Tensor, tpos: torch.Tensor) -> torch.Tensor:
+    """The per-token doc spans of the tokens ``tpos`` (a slice of ``doc_index.tpos``: the
+    matching slice of ``doc_index.span``; otherwise computed from ``tdoc``)."""
+    full = doc_index.tpos
+    o = (tpos.data_ptr() - full.data_ptr()) // full.element_size()
+    if (doc_index.span is not None and tpos.untyped_storage().data_ptr() == full.untyped_storage().data_ptr()
+            and tpos.is_contiguous() and 0 <= o and o + tpos.numel() <= full.numel()):
+        return doc_index.span[o:o + tpos.numel()]
+    d = tdoc.long()
+    off = doc_index.doc_off
+    return (off[d] | ((off[d + 1] - off[d]) << 40)).contiguous()
 
 
 def build_chunks(words: torch.Tensor, max_chunk: int = 2048) -> torch.Tensor:
@@ -135,6 +159,9 @@ def chunk_order(chunks: torch.Tensor) -> torch.Tensor:
 
 
 DOC_TOPIC_8BIT = os.environ.get("HARP_LDA_NDK8", "1") != "0"
+# sparse sampler without a doc-topic table: per-token doc spans instead of doc ids (one
+# independent load for the next token's doc range instead of ids -> doc_off)
+SPAN = os.environ.get("HARP_LDA_SPAN", "1") != "0"
 
 
 def doc_topic_dtype(device, max_doc_len: int) -> torch.dtype:
@@ -199,6 +226,15 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
                 order = chunk_order(chunks)
             assert order.dtype == torch.int32 and order.numel() == chunks.numel() - 1
             work = torch.zeros(1, dtype=torch.int32, device=dev)
+            if ndk is None and SPAN:  # doc ranges from per-token spans: no dependent doc_off load
+                span = _span_slice(doc_index, tdoc, tpos)
+                st = _lib.kernels().harp_lda_cgs_sparse_span(
+                    span.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(), chunks.numel() - 1,
+                    order.data_ptr(), work.data_ptr(), tpos.data_ptr(), doc_index.zdoc.data_ptr(), nwk.data_ptr(),
+                    nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
+                    seed & 0xFFFFFFFFFFFFFFFF, -1 if deterministic else SPARSE_WAVES, _lib.stream_ptr(dev))
+                _lib.check(st, "lda_cgs_sparse_span")
+                return delta
             st = _lib.kernels().harp_lda_cgs_sparse(
                 tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(), chunks.numel() - 1,
                 order.data_ptr(), work.data_ptr(), tpos.data_ptr(), doc_index.doc_off.data_ptr(), doc_index.zdoc.data_ptr(), _lib.ptr(ndk),

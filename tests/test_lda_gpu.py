@@ -46,6 +46,27 @@ def test_sparse_sampler_keeps_no_dense_doc_table(cuda, strategy):
     assert len(ll) == 1 and ll[0] < 0
 
 
+def test_sparse_sampler_doc_spans_match_doc_ids(cuda, monkeypatch):
+    """The span form of the sparse sampler (per-token doc_off | length << 40 instead of doc
+    ids -> doc_off) takes the same trajectory as the id form in the one-wave deterministic
+    mode, on the model path (token slices of the rotation)."""
+    from harp_amd.models.lda import LDACollectiveMapper
+    from harp_amd.ops import lda as L
+    from harp_amd.runtime.mapper import KeyValReader
+
+    toks = synthetic_corpus(800, 2000, 20, 60, seed=8)
+    out = {}
+    for span in (True, False):
+        monkeypatch.setattr(L, "SPAN", span)
+        cfg = LDAConfig(num_topics=1500, alpha=0.03, beta=0.01, iterations=2, print_interval=2, deterministic=True)
+        m = LDACollectiveMapper(Communicator(device=cuda), cfg, 800, 2000, toks)
+        m.run(KeyValReader([]))
+        assert m.sparse and m.ndk is None and (m.doc_index.span is not None) == span
+        out[span] = (m.tz.cpu(), m.result["loglik"])
+    assert torch.equal(out[True][0], out[False][0])
+    assert out[True][1] == out[False][1]
+
+
 def test_lda_push_pull_gpu(cuda):
     from harp_amd.models.lda import LDAConfig, LDAPushPullMapper, synthetic_corpus
     from harp_amd.parallel.comm import Communicator
