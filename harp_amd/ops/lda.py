@@ -98,10 +98,13 @@ class DocIndex:
         off = torch.zeros(n_docs + 1, dtype=torch.int64, device=tdoc.device)
         off[1:] = torch.cumsum(torch.bincount(tdoc, minlength=n_docs)[:n_docs], 0)
         span = None
-        if tdoc.device.type == "cuda" and SPAN:
-            d = tdoc.long()
-            span = off[d] | ((off[d + 1] - off[d]) << 40)
-            del d
+        if tdoc.device.type == "cuda" and SPAN:  # built in pieces: no int64 temporaries of n
+            span = torch.empty(tdoc.numel(), dtype=torch.int64, device=tdoc.device)
+            for a in range(0, tdoc.numel(), 1 << 27):
+                d = tdoc[a:a + (1 << 27)].long()
+                lo = off[d]
+                span[a:a + d.numel()] = lo | ((off[d + 1] - lo) << 40)
+                del d, lo
         return DocIndex(zdoc, off, tpos, span)
 
     def sync(self, tz: torch.Tensor, tpos: Optional[torch.Tensor] = None) -> None:
