@@ -217,7 +217,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (cap < 0) {
         const int4* s4 = (const int4*)slot;
-        for (int q = lane; q < K / 4; q += 64) ((int4*)lrow)[q] = s4[q];
+        // a dense slot holds the whole padded row (the PS is built with K_pad = KP ints,
+        // models/lda.py): copy all of it, so topics K - K % 4 .. K - 1 are not left at 0
+        for (int q = lane; q < KP / 4; q += 64) ((int4*)lrow)[q] = s4[q];
       } else {
         int nnz = *(const int*)slot;
         nnz = nnz < 0 ? 0 : (nnz > cap ? cap : nnz);

@@ -160,6 +160,8 @@ def _assign_wide(X, op, sums, labels, want_objective, obj_partial, min_dist):
         from . import segment
 
         assert sums.dtype == torch.float32 and sums.shape[1] >= op.d + 1 and sums.is_contiguous()
+        assert sums.shape[0] >= op.Cm2.shape[0], "sums needs Kp (padded) rows"
+        assert sums.device == dev
         perm, start = segment.bucket_labels(labels, op.Cm2.shape[0])
         segment.bucket_rowsum(X, perm, start, sums)
     obj = obj_partial[:nblk].double().sum() if want_objective else None
@@ -185,6 +187,9 @@ def assign(X: torch.Tensor, op: CentroidOperand, sums: Optional[torch.Tensor] = 
     if _lib.use_native(X):
         lib = _lib.kernels()
         if dp > NARROW_MAX_DP:
+            if accumulate == "atomic":
+                raise ValueError("accumulate='atomic' is only fused into the narrow kernel (dp <= "
+                                 f"{NARROW_MAX_DP}); the wide path (dp = {dp}) accumulates by bucket")
             return _assign_wide(X, op, sums, labels, want_objective, obj_partial, min_dist)
         if dp > 128:
             variant = 4  # the only instantiation for 9..16 k-steps

@@ -56,7 +56,8 @@ def bucket_labels(labels: torch.Tensor, K: int) -> Tuple[torch.Tensor, torch.Ten
     return ws[po.value:po.value + n], ws[so.value:so.value + K + 1]
 
 
-SUM_SLICE = int(os.environ.get("HARP_ROWSUM_SLICE", "1024"))  # 256: the per-slice form before round 4
+# 256: the per-slice form before round 4. The kernel takes multiples of 8 in [8, 1024]
+SUM_SLICE = min(1024, max(8, int(os.environ.get("HARP_ROWSUM_SLICE", "1024")) // 8 * 8))
 
 
 def bucket_rowsum(X: torch.Tensor, perm: torch.Tensor, start: torch.Tensor, out: torch.Tensor) -> torch.Tensor:

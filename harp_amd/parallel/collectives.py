@@ -554,8 +554,13 @@ def _ring_rows(comm: Communicator, table: PackedTable, dst_of: Sequence[int]) ->
     read here) rotated by a derangement (each rank sends to one other rank and receives from
     one other) lets every rank track all P row counts locally: one all-gather of the counts
     at the first rotate, then counts[dst_of[r]] <- counts[r] per rotation. Later rotates
-    send the payload with no header round trip and no host sync (the reference's Rotator
-    re-sends the partition headers on every hop, dymoro/Rotator.java)."""
+    skip the point-to-point header round trip, but :func:`rotate` still runs one 2-element
+    agreement all-reduce (and a host read of it) per rotate, so that a rank that resized the
+    table or lost the packed layout makes EVERY rank raise or fall back instead of leaving
+    its peers in a mismatched send/recv. The saving is therefore one send/recv pair, not
+    the host sync (the reference's Rotator re-sends the partition headers on every hop,
+    dymoro/Rotator.java). Device-resident rotation without any per-hop sync is
+    :class:`~harp_amd.runtime.dymoro.DeviceRotator`."""
     P = comm.world_size
     if not getattr(table, "ring_rows", False) or not _derangement(dst_of):
         return None
