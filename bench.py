@@ -92,6 +92,8 @@ def parse_args(argv=None):
                          "pull / delta / push passes (with auto, a 1-rank run also records the off case)")
     ap.add_argument("--extras-timeout", type=float, default=180.0, help="wall-clock bound (s) per nested record")
     ap.add_argument("--metrics-jsonl", default="", help="per-iteration phase/bytes records (JSONL)")
+    ap.add_argument("--preflight-timeout", type=float, default=120.0,
+                    help="wall-clock bound (s) on the RCCL pre-flight (world / devices / battery / bandwidth)")
     return ap.parse_args(argv)
 
 
@@ -127,6 +129,139 @@ def spawn(args, argv) -> int:
         for p in procs:
             p.kill()
     return rc
+
+
+# ----------------------------------------------------------------------------- RCCL pre-flight
+PREFLIGHT_BYTES = 64 << 20
+
+
+def _now(comm, torch) -> float:
+    if comm.device.type == "cuda":
+        torch.cuda.synchronize()
+    return time.perf_counter()
+
+
+def rccl_preflight(args, comm, torch) -> dict:
+    """A short self-diagnosis before any timed record (the reference's
+    standalone collective harness, core/harp-collective/.../AllreduceCollective.java:53-138,
+    and BenchmarkMapper.java:64-152): the world size every rank sees, every rank's device /
+    PCI address (distinct on a real node), a mini battery of the collectives the records use
+    (each checked against known values; a failure is reported here and never costs the
+    headline), the bus bandwidth of a 64 MB all-reduce, and one ring send/recv per MF-SGD
+    rotation channel (the same keyed channels the rotation then reuses) with its GB/s."""
+    import torch.distributed as dist
+
+    from harp_amd.runtime.dymoro import ring_strides
+
+    P, me, dev = comm.world_size, comm.rank, comm.device
+    ident = [me, -1, -1, -1, -1]
+    name = "cpu"
+    if dev.type == "cuda":
+        pr = torch.cuda.get_device_properties(dev)
+        ident = [me, dev.index, int(getattr(pr, "pci_domain_id", -1)), int(getattr(pr, "pci_bus_id", -1)),
+                 int(getattr(pr, "pci_device_id", -1))]
+        name = pr.name
+    out = {"world": P, "backend": comm.backend, "device": {"index": ident[1], "name": name,
+                                                          "pci": "%04x:%02x:%02x" % tuple(max(0, x) for x in ident[2:])}}
+    if P == 1:
+        return out
+    battery = {}
+
+    def item(key, fn):
+        t0 = _now(comm, torch)
+        try:
+            ok = fn()
+            battery[key] = {"ok": bool(ok), "ms": round((_now(comm, torch) - t0) * 1e3, 3)}
+        except Exception as e:  # noqa: BLE001
+            battery[key] = {"ok": False, "error": f"{type(e).__name__}: {e}"[:200]}
+
+    seen = {}
+
+    def world():
+        g = comm.all_gather_ints([P] + ident)
+        seen["rows"] = g.tolist()
+        return all(r[0] == P for r in seen["rows"]) and [r[1] for r in seen["rows"]] == list(range(P))
+
+    item("all_gather_ints", world)
+    rows = seen.get("rows", [])
+    out["world_seen"] = [r[0] for r in rows]
+    out["ranks"] = [{"rank": r[1], "device": r[2], "pci": "%04x:%02x:%02x" % tuple(max(0, x) for x in r[3:])}
+                    for r in rows]
+    out["distinct_devices"] = len({(r[2], r[3], r[4], r[5]) for r in rows}) == P if rows else False
+    f32 = dict(dtype=torch.float32, device=dev)
+
+    def all_reduce():
+        t = torch.full((1024,), float(me + 1), **f32)
+        comm.all_reduce(t)
+        return bool((t == P * (P + 1) / 2).all())
+
+    def broadcast():
+        t = torch.full((1024,), float(me), **f32)
+        comm.broadcast(t, P - 1)
+        return bool((t == P - 1).all())
+
+    def all_gather():
+        o = torch.empty(P * 4, **f32)
+        comm.all_gather_into(o, torch.full((4,), float(me), **f32))
+        return torch.equal(o.cpu(), torch.arange(P, dtype=torch.float32).repeat_interleave(4))
+
+    def reduce_scatter():
+        o = torch.empty(4, **f32)
+        comm.reduce_scatter(o, torch.arange(P * 4, **f32))
+        return torch.equal(o.cpu(), P * torch.arange(me * 4, me * 4 + 4, dtype=torch.float32))
+
+    def all_to_all():
+        inp = torch.tensor([me * 100 + j for j in range(P)], dtype=torch.int64, device=dev)
+        o = torch.empty(P, dtype=torch.int64, device=dev)
+        comm.all_to_all_single(o, inp)
+        return o.cpu().tolist() == [j * 100 + me for j in range(P)]
+
+    def ring():
+        o = torch.empty(1024, **f32)
+        comm.sendrecv({(me + 1) % P: torch.full((1024,), float(me), **f32)}, {(me - 1) % P: o})
+        return bool((o == (me - 1) % P).all())
+
+    for key, fn in (("all_reduce", all_reduce), ("broadcast", broadcast), ("all_gather", all_gather),
+                    ("reduce_scatter", reduce_scatter), ("all_to_all", all_to_all), ("ring_sendrecv", ring),
+                    ("barrier", lambda: comm.barrier() or True)):
+        item(key, fn)
+    out["battery"] = battery
+    out["battery_ok"] = all(v["ok"] for v in battery.values())
+
+    def busbw():
+        t = torch.ones(PREFLIGHT_BYTES // 4, **f32)
+        comm.all_reduce(t)  # warm-up (RCCL communicator / channel setup)
+        reps = 5
+        t0 = _now(comm, torch)
+        for _ in range(reps):
+            comm.all_reduce(t)
+        dt = (_now(comm, torch) - t0) / reps
+        # ring all-reduce moves 2 (P - 1) / P of the buffer over every link (nccl-tests busbw)
+        seen["busbw"] = 2 * (P - 1) / P * PREFLIGHT_BYTES / dt / 1e9
+        seen["ar_ms"] = dt * 1e3
+        return True
+
+    item("all_reduce_64MB", busbw)
+    out["all_reduce_64MB"] = {"ms": round(seen.get("ar_ms", 0.0), 3), "busbw_GBps": round(seen.get("busbw", 0.0), 2)}
+    S = args.sgd_slices or 2
+    chans = []
+    for k, st in enumerate(ring_strides(P, S)):
+        rec = {"channel": f"sgd-h-{k}", "stride": st}
+        try:
+            ch = comm.channel(f"sgd-h-{k}")  # the DeviceRotator's channel key (models/sgd_mf.py)
+            n = (16 << 20) // 4
+            snd, rcv = torch.ones(n, **f32), torch.empty(n, **f32)
+            ch.sendrecv({(me + st) % P: snd}, {(me - st) % P: rcv})
+            t0 = _now(comm, torch)
+            for _ in range(3):
+                ch.sendrecv({(me + st) % P: snd}, {(me - st) % P: rcv})
+            dt = (_now(comm, torch) - t0) / 3
+            rec.update(ok=bool((rcv == 1).all()), MB=16, GBps=round((n * 4) / dt / 1e9, 2))
+        except Exception as e:  # noqa: BLE001
+            rec.update(ok=False, error=f"{type(e).__name__}: {e}"[:200])
+        chans.append(rec)
+    out["rotation_channels"] = chans
+    return out
 
 
 # ----------------------------------------------------------------------------- K-means
@@ -249,6 +384,11 @@ def bench_sgd(args, comm, torch):
     n = float(nt.item())
     train_rmse, _ = m._eval_ring(args.sgd_warmup + args.sgd_epochs - 1)
     st = step_stats(ep_s)
+    placement = None
+    if dev.type == "cuda":
+        from harp_amd.ops import mf as MF
+
+        placement = MF.check_placement(dev)  # residue -> XCC check of every timed launch
     return {
         "metric": "MF-SGD updates/sec (Netflix-shape synthetic, model rotation)",
         "updates_per_sec": round(n / dt, 1),
@@ -261,6 +401,7 @@ def bench_sgd(args, comm, torch):
         "sync_bytes_per_iter": int(rot_bytes / max(args.sgd_epochs, 1)),
         "rotation_exposed_s_per_epoch": round(rot_exposed / max(args.sgd_epochs, 1), 6),
         "rotation_strides": [s.stride for s in m.schedules],
+        "xcd_placement": placement,
         "train_rmse": round(train_rmse, 6),
         "users": args.sgd_users, "items": args.sgd_items, "ratings": args.sgd_ratings, "rank": args.sgd_rank,
         "slices_per_rank": cfg.num_slices,
@@ -597,7 +738,12 @@ def run(args) -> int:
         raise RuntimeError(f"world size {comm.world_size} != --gpus {args.gpus}")
     if world > 1:
         comm.barrier()  # rank 0's (rare) build finishes before any rank loads the library
+    # self-diagnosis before any timed record; bounded like the nested records (a guard that
+    # fires prints what exists and exits 124 instead of hanging the node)
+    pre = {}
+    _nested(pre, "rccl", rccl_preflight, args.preflight_timeout, args, comm, torch)
     rec = bench_kmeans(args, comm, torch)
+    rec["rccl"] = pre["rccl"]
     if comm.device.type == "cuda":
         torch.cuda.empty_cache()
     want_sgd = args.sgd == "on" or (args.sgd == "auto" and comm.device.type == "cuda")

@@ -352,15 +352,51 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
 // 16-lane subgroup runs one stream. `win` (optional, 2 x 64 int64): cell c trains only the
 // window of win[64 + c] ratings starting at win[c], wrapping around the cell — the
 // fixed-fraction mode standing in for the reference's timer-bounded rotation steps.
+//
+// Placement check (chk != NULL): the schedule is only conflict-free if every block of residue
+// x runs on ONE XCD and the 8 residues on 8 different XCDs. Thread 0 of each block reads
+// HW_REG_XCC_ID and tags, for launch number `gen` (host counter, > 0), residue -> XCC and
+// XCC -> residue in a 64-bit word each ((gen << 8) | id + 1; the first block of a launch to
+// see an older generation installs its own pair, so no reset launch is needed). A block
+// whose pair disagrees with the installed one raises chk[kChkErr] (sticky; the host reads it
+// once per epoch, ops.mf.check_placement, and switches to the placed kernel below).
+constexpr int kChkWords = 32;  // [0, 8) residue map | [8, 24) XCC map | [24] error
+constexpr int kChkErr = 24;
+
+__device__ __forceinline__ unsigned tag_once(unsigned long long* p, unsigned long long gen, unsigned val) {
+  unsigned long long cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long mine = (gen << 8) | val;
+  while ((cur >> 8) != gen) {
+    if (__hip_atomic_compare_exchange_strong(p, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return val;
+  }
+  return (unsigned)(cur & 0xff);
+}
+
+__device__ __forceinline__ int hw_xcc_id() {
+  return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;  // HW_REG_XCC_ID
+}
+
+__device__ __forceinline__ void placement_check(unsigned long long* chk, unsigned long long gen, int x) {
+  if (chk == nullptr || threadIdx.x != 0) return;
+  const int hw = hw_xcc_id();
+  const bool bad = tag_once(chk + x, gen, (unsigned)hw + 1) != (unsigned)hw + 1 ||
+                   tag_once(chk + 8 + hw, gen, (unsigned)x + 1) != (unsigned)x + 1;
+  if (bad) __hip_atomic_store(chk + kChkErr, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int R, int CH>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
                                                          const long* __restrict__ win, int step,
                                                          float* __restrict__ W, int ldw, float* __restrict__ H, int ldh,
-                                                         float lr, float lam) {
+                                                         float lr, float lam, unsigned long long* chk,
+                                                         unsigned long long gen) {
   __shared__ int sR[16 * CH], sC[16 * CH];
   __shared__ float sV[16 * CH];
   const int x = blockIdx.x % XCDS;
+  placement_check(chk, gen, x);
   const long j = blockIdx.x / XCDS;
   const long per_xcd = gridDim.x / XCDS;
   const int cell = x * XCDS + (x + step) % XCDS;
@@ -389,6 +425,90 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
       sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
                              (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
+}
+
+// Placement-independent sub-step (the fallback when placement_check fires): a block trains
+// the cell of the XCD it RUNS on (row x = HW_REG_XCC_ID), not the one its blockIdx.x
+// names, so one XCD per cell holds by construction whatever the dispatcher does. Blocks
+// of an XCD claim rounds of the cell from a counter (ws[x]); a cell whose XCD received no
+// block at all (every block of the grid landed elsewhere) is left fully unclaimed -- its
+// rows were touched by nobody in this launch -- and the LAST block to leave trains it
+// alone (ws[9] counts such drains), then zeroes the counters for the next launch on this
+// stream. Every round of every cell is trained exactly once.
+// ws layout (int32): claim[8] | exit | drained
+constexpr int kPlacedWs = 10;
+
+template <int R, int CH>
+__device__ __forceinline__ void xcd_round(const int* __restrict__ rows, const int* __restrict__ cols,
+                                          const float* __restrict__ vals, long a, long w0, long ncell, long n, long rd,
+                                          int* sR, int* sC, float* sV, float* __restrict__ W, int ldw,
+                                          float* __restrict__ H, int ldh, float lr, float lam) {
+  const int sl = threadIdx.x & 15;
+  const int sub = threadIdx.x >> 4;
+  const long r0 = rd * 16 * CH;
+  __syncthreads();  // the previous round is done with the LDS triples
+  for (int k = threadIdx.x; k < 16 * CH; k += 256) {
+    if (r0 + k < n) {
+      long q = w0 + r0 + k;
+      if (q >= ncell) q -= ncell;
+      sR[k] = rows[a + q];
+      sC[k] = cols[a + q];
+      sV[k] = vals[a + q];
+    }
+  }
+  __syncthreads();
+  const long left = n - (r0 + (long)sub * CH);
+  if (left > 0)
+    sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, left < CH ? (int)left : CH, sl, W, (unsigned)ldw, H,
+                      (unsigned)ldh, lr, lam);
+}
+
+template <int R, int CH>
+__global__ __launch_bounds__(256) void mf_sgd_xcd_placed_kernel(const int* __restrict__ rows,
+                                                                const int* __restrict__ cols,
+                                                                const float* __restrict__ vals,
+                                                                const long* __restrict__ off,
+                                                                const long* __restrict__ win, int step,
+                                                                float* __restrict__ W, int ldw, float* __restrict__ H,
+                                                                int ldh, float lr, float lam, int* __restrict__ ws) {
+  __shared__ int sR[16 * CH], sC[16 * CH];
+  __shared__ float sV[16 * CH];
+  __shared__ int s_round, s_last;
+  const int x = hw_xcc_id() & (XCDS - 1);
+  auto cell_of = [&](int xx, long& a, long& w0, long& ncell, long& n) {
+    const int cell = xx * XCDS + (xx + step) % XCDS;
+    a = off[cell];
+    ncell = off[cell + 1] - a;
+    w0 = win ? win[cell] : 0;
+    n = win ? win[XCDS * XCDS + cell] : ncell;
+  };
+  long a, w0, ncell, n;
+  cell_of(x, a, w0, ncell, n);
+  const long rounds = (n + 16 * CH - 1) / (16 * CH);
+  for (;;) {
+    if (threadIdx.x == 0)
+      s_round = __hip_atomic_fetch_add(ws + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const long rd = s_round;
+    __syncthreads();  // everyone read s_round before it is rewritten
+    if (rd >= rounds) break;
+    xcd_round<R, CH>(rows, cols, vals, a, w0, ncell, n, rd, sR, sC, sV, W, ldw, H, ldh, lr, lam);
+  }
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ws + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int xx = 0; xx < XCDS; ++xx) {
+    if (__hip_atomic_load(ws + xx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) continue;
+    cell_of(xx, a, w0, ncell, n);
+    const long rr = (n + 16 * CH - 1) / (16 * CH);
+    for (long rd = 0; rd < rr; ++rd)
+      xcd_round<R, CH>(rows, cols, vals, a, w0, ncell, n, rd, sR, sC, sV, W, ldw, H, ldh, lr, lam);
+    if (threadIdx.x == 0 && rr > 0) __hip_atomic_fetch_add(ws + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 9; ++k) __hip_atomic_store(ws + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Persistent XCD-blocked pass: all `steps` sub-steps of one slice in ONE launch, ordered by
@@ -591,12 +711,19 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
+// variant 0: blockIdx-placed sub-steps (+ placement check when chk != NULL; `gen` is the
+// first launch's generation, one per sub-step); 2: mf_sgd_xcd_placed_kernel (pws)
 template <int R, int CH>
 int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win, int steps,
-                   int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, hipStream_t s) {
+                   int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, int variant,
+                   unsigned long long* chk, unsigned long long gen, int* pws, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
-    mf_sgd_xcd_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-        rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam);
+    if (variant == 2)
+      mf_sgd_xcd_placed_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam, pws);
+    else
+      mf_sgd_xcd_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
+          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam, chk, gen + (unsigned long long)step);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -725,8 +852,10 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_wide_kernel(const int* __restr
                                                               const long* __restrict__ off,
                                                               const long* __restrict__ win, int step, int R,
                                                               float* __restrict__ W, int ldw, float* __restrict__ H,
-                                                              int ldh, float lr, float lam) {
+                                                              int ldh, float lr, float lam,
+                                                              unsigned long long* chk, unsigned long long gen) {
   const int x = blockIdx.x % XCDS;
+  placement_check(chk, gen, x);
   const long j = blockIdx.x / XCDS;
   const long per_xcd = gridDim.x / XCDS;
   const int cell = x * XCDS + (x + step) % XCDS;
@@ -795,17 +924,18 @@ int launch_sgd_wide(const int* rows, const int* cols, const float* vals, long n,
 template <int Q>
 int launch_sgd_xcd_wide(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
                         int steps, int chunk, int blocks_per_xcd, int r, float* W, int ldw, float* H, int ldh,
-                        float lr, float lam, hipStream_t s) {
+                        float lr, float lam, unsigned long long* chk, unsigned long long gen0, hipStream_t s) {
   for (int step = 0; step < steps; ++step) {
+    const unsigned long long gen = gen0 + (unsigned long long)step;
     if (chunk == 32)
       mf_sgd_xcd_wide_kernel<Q, 32><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam);
+          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam, chk, gen);
     else if (chunk == 128)
       mf_sgd_xcd_wide_kernel<Q, 128><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam);
+          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam, chk, gen);
     else
       mf_sgd_xcd_wide_kernel<Q, 64><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam);
+          rows, cols, vals, off, win, step, r, W, ldw, H, ldh, lr, lam, chk, gen);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -851,22 +981,31 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 // All `steps` (= 8) sub-steps of the XCD-blocked schedule over one resident slice: `off`
 // is a DEVICE array of 65 int64 cell offsets into rows/cols/vals (every cell < 2^31 ratings).
 // `chunk` (ratings per stream and round) is 8, 16, 32, 64 or 128 (32..128 for wide ranks);
-// `variant` must be 0 (non-temporal H stores, 23 % slower, and forced 6 / 7 / 8 waves per
-// SIMD were measured in round 1 and are no longer built).
+// `variant`: 0 = blockIdx-placed sub-steps, checked when `chk` (harp_mf_chk_words() zeroed
+// uint64 per stream) is given: launch generations gen .. gen + steps - 1 (> 0, never reused
+// on that chk); 2 = the placement-independent kernel (`pws`: harp_mf_placed_ws_ints()
+// zeroed int32, left zeroed; ranks <= 256). Non-temporal H stores (23 % slower) and forced
+// 6 / 7 / 8 waves per SIMD were measured in round 1 and are no longer built.
 // `win`: optional DEVICE array [2 x 64] of per-cell window starts and lengths (NULL = all).
+HARP_EXPORT int harp_mf_chk_words() { return kChkWords; }
+HARP_EXPORT int harp_mf_placed_ws_ints() { return kPlacedWs; }
+
 HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win,
                                 int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
-                                float* H, int ldh, float lr, float lam, hipStream_t s) {
-  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || variant != 0)
+                                float* H, int ldh, float lr, float lam, unsigned long long* chk,
+                                unsigned long long gen, int* pws, hipStream_t s) {
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || (variant != 0 && variant != 2))
     return HARP_EBADARG;
-  if (wide_ok(r)) {  // wide ranks: one wave per stream, variants do not apply
+  if ((chk && gen == 0) || (variant == 2 && (!pws || wide_ok(r)))) return HARP_EBADARG;
+  if (wide_ok(r)) {  // wide ranks: one wave per stream
     if (chunk != 32 && chunk != 64 && chunk != 128) return HARP_EBADARG;
 #define SGDXW_CALL(QQ) \
-  launch_sgd_xcd_wide<QQ>(rows, cols, vals, off, win, steps, chunk, blocks_per_xcd, r, W, ldw, H, ldh, lr, lam, s)
+  launch_sgd_xcd_wide<QQ>(rows, cols, vals, off, win, steps, chunk, blocks_per_xcd, r, W, ldw, H, ldh, lr, lam, chk, \
+                          gen, s)
     WIDE_DISPATCH(r, SGDXW_CALL)
 #undef SGDXW_CALL
   }
-#define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, s
+#define SGDX_ARGS rows, cols, vals, off, win, steps, blocks_per_xcd, W, ldw, H, ldh, lr, lam, variant, chk, gen, pws, s
 #define SGDX_CALL(RR)                                                             \
   (chunk == 8 ? launch_sgd_xcd<RR, 8>(SGDX_ARGS)                                    \
    : chunk == 16 ? launch_sgd_xcd<RR, 16>(SGDX_ARGS)                                \

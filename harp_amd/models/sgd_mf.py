@@ -50,6 +50,8 @@ class SGDConfig:
     test_every: int = 5        # rmseIteInterval
     seed: int = 0
     init_scale: float = -1.0   # <0: sqrt(mean_rating / r) (E[w.h] = mean rating)
+    init: str = "mean"         # "mean": U(0, 2 init_scale); "reference": U(0, 1) / sqrt(r), the reference's
+                               # SGDUtil.randomize (ml/java/.../sgd/SGDUtil.java:72-82)
     checkpoint_dir: str = ""   # .hpt checkpoints (W rows + resident H slices); resume on restart
     checkpoint_every: int = 0  # epochs between checkpoints (0: never)
     model_dir: str = ""        # final text dump: W-<worker>, H-<worker>, evaluation
@@ -166,6 +168,7 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.n_users, self.n_items = n_users, n_items
         self._train, self._test = train, test
         self.rmse_history: List[Tuple[int, float, float]] = []
+        self.placement_events: list = []
         self.epoch_times: List[float] = []
 
     # -- partitioning -------------------------------------------------------------------
@@ -211,6 +214,8 @@ class SGDCollectiveMapper(CollectiveMapper):
             self.test = None
         # model: W local, H slices of the blocks initially placed here
         r = cfg.rank
+        # GPU factors carry zero columns up to the next kernel rank (exact: ops.mf.kernel_rank)
+        self.rs = MF.storage_rank(r, dev)
         mean = float(v.mean().item()) if v.numel() else 3.0
         trace("local mean")
         tot = torch.tensor([mean * v.numel(), float(v.numel())], dtype=torch.float64, device=dev)
@@ -218,9 +223,12 @@ class SGDCollectiveMapper(CollectiveMapper):
             self.comm.all_reduce(tot)
         mean = float(tot[0] / max(tot[1], 1))
         trace("mean allreduce")
-        scale = cfg.init_scale if cfg.init_scale > 0 else math.sqrt(mean / r)
+        if cfg.init == "reference":
+            scale = 0.5 / math.sqrt(r)
+        else:
+            scale = cfg.init_scale if cfg.init_scale > 0 else math.sqrt(mean / r)
         gw = torch.Generator().manual_seed(cfg.seed * 31 + 7 + me)
-        self.W = (torch.rand((self.users.numel(), r), generator=gw) * 2 * scale).to(dev)
+        self.W = self._padded(torch.rand((self.users.numel(), r), generator=gw) * 2 * scale)
         trace("W init")
         orders = get_rotation_sequences(self, cfg.epochs + 2, cfg.seed) if cfg.random_order else None
         # ring mode: slice k rotates on its own stride so the slices use different xGMI links
@@ -233,7 +241,7 @@ class SGDCollectiveMapper(CollectiveMapper):
         for k in range(S):
             gs = block * S + k
             gh = torch.Generator().manual_seed(cfg.seed * 1009 + gs)
-            slabs.append((torch.rand((self.ips, r), generator=gh) * 2 * scale).to(dev))
+            slabs.append(self._padded(torch.rand((self.ips, r), generator=gh) * 2 * scale))
         self.rot = DeviceRotator(self.comm, slabs, name="sgd-h", metrics=self.metrics)
         trace("H slabs + rotator")
         self.trained = 0
@@ -242,6 +250,12 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.budget = StepBudget(cfg.time_budget_ms / 1e3, dev) if cfg.time_budget_ms > 0 else None
         self.budget_history = [self.budget.budget_s] if self.budget is not None else []
         self._cursor = {}
+
+    def _padded(self, M: torch.Tensor) -> torch.Tensor:
+        """``M`` [n, r] on the device with zero columns up to the storage rank."""
+        out = torch.zeros((M.shape[0], self.rs), dtype=torch.float32, device=self.device)
+        out[:, : M.shape[1]] = M.to(self.device)
+        return out
 
     def _all_users_of(self, me: int) -> torch.Tensor:
         allu = torch.arange(self.n_users, device=self._train[0].device)
@@ -334,6 +348,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             self.epoch_times.append(time.perf_counter() - t0)
             if self.cfg.kernel_variant == MF.FLOW_VARIANT and self.device.type == "cuda":
                 MF.check_flow_errors(self.device)  # a timed-out wait / foreign XCD invalidates the epoch
+            self._check_placement(ep)
             self.metrics.end_iteration("sgd", ep, trained=n, epoch_s=self.epoch_times[-1],
                                        updates_per_s=n / max(self.epoch_times[-1], 1e-12))
             if self.cfg.test_every and ((ep + 1) % self.cfg.test_every == 0 or ep == self.cfg.epochs - 1):
@@ -344,7 +359,32 @@ class SGDCollectiveMapper(CollectiveMapper):
         if self.cfg.model_dir:
             self.save_models(self.cfg.model_dir)
         self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained,
-                       "start_epoch": start}
+                       "start_epoch": start, "placement": self.placement_events}
+
+    def _check_placement(self, ep: int) -> None:
+        """Once per epoch (the epoch is already synchronised): did a default XCD-blocked
+        launch run blocks of one residue on two XCDs (csrc/mf_sgd.hip placement_check)?
+        Then that epoch ran Hogwild across L2s (every rating still trained once) and the
+        remaining epochs use a schedule that does not depend on the dispatcher's placement:
+        the placed kernel (ranks <= 256) or the flat kernel (wide ranks)."""
+        if self.device.type != "cuda" or not self.cfg.xcd_blocks:
+            return
+        got = MF.check_placement(self.device)
+        if got["drained"]:
+            self.placement_events.append((ep, "drained", got["drained"]))
+        if not got["violation"] or self.cfg.kernel_variant == MF.PLACED_VARIANT:
+            return
+        import warnings
+
+        if MF.storage_rank(self.cfg.rank, self.device) <= 256:
+            self.cfg.kernel_variant = MF.PLACED_VARIANT
+            what = "placed"
+        else:
+            self.cfg.xcd_blocks = False
+            what = "flat"
+        self.placement_events.append((ep, "violation", what))
+        warnings.warn(f"MF-SGD epoch {ep}: XCD placement check fired (blocks of one residue on two XCDs); "
+                      f"switching to the {what} kernel")
 
     # -- checkpoint / resume / model output --------------------------------------------------
     def _ckpt(self):
@@ -370,9 +410,10 @@ class SGDCollectiveMapper(CollectiveMapper):
         from ..utils.checkpoint import tensor_table
 
         self.rot.wait_all()
-        tabs = {"W": tensor_table(self.W, self.users)}
+        r = self.cfg.rank
+        tabs = {"W": tensor_table(self.W[:, :r].contiguous(), self.users)}
         for k, gs, items in self._resident(ep + 1):
-            tabs[f"H{k}"] = tensor_table(self.rot.slabs[k][: items.numel()], items)
+            tabs[f"H{k}"] = tensor_table(self.rot.slabs[k][: items.numel(), :r].contiguous(), items)
         extra = {"rmse": [list(x) for x in self.rmse_history], "trained": int(self.trained)}
         return self._ckpt().save(ep, tabs, extra=extra)
 
@@ -390,7 +431,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             full[ids] = tab.buffer.to(self.device, torch.float32)
             return full
 
-        self.W.copy_(scatter(tabs["W"], self.n_users)[self.users.to(self.device)])
+        self.W[:, :r].copy_(scatter(tabs["W"], self.n_users)[self.users.to(self.device)])
         H = torch.zeros((self.n_items, r), dtype=torch.float32, device=self.device)
         for name, tab in tabs.items():
             if name.startswith("H") and len(tab):
@@ -399,7 +440,7 @@ class SGDCollectiveMapper(CollectiveMapper):
         for k, gs, items in self._resident(ep):
             slab = self.rot.slabs[k]
             slab.zero_()
-            slab[: items.numel()] = H[items.to(self.device)]
+            slab[: items.numel(), :r] = H[items.to(self.device)]
         self.rmse_history = [tuple(x) for x in man["extra"].get("rmse", [])]
         self.trained = int(man["extra"].get("trained", 0))
         return ep
@@ -416,9 +457,9 @@ class SGDCollectiveMapper(CollectiveMapper):
         items, rows = [], []
         for k, gs, it_ids in self._resident(ep):
             items.append(it_ids)
-            rows.append(self.rot.slabs[k][: it_ids.numel()])
+            rows.append(self.rot.slabs[k][: it_ids.numel(), : self.cfg.rank])
         write_factor_rows(f"{folder}/H-{me}", torch.cat(items), torch.cat(rows))
-        write_factor_rows(f"{folder}/W-{me}", self.users, self.W)
+        write_factor_rows(f"{folder}/W-{me}", self.users, self.W[:, : self.cfg.rank])
         if self.is_master():
             last = self.rmse_history[-1][2] if self.rmse_history else float("nan")
             write_scalar(f"{folder}/evaluation", last)

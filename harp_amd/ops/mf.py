@@ -23,18 +23,62 @@ def supported_rank(r: int) -> bool:
     return r in SUPPORTED_RANKS or (256 < r <= MAX_WIDE_RANK and r % 4 == 0)
 
 
-def _require_rank(r: int) -> None:
-    if not supported_rank(r):
-        raise NotImplementedError(f"native MF-SGD supports ranks {SUPPORTED_RANKS} and multiples of 4 in "
-                                  f"(256, {MAX_WIDE_RANK}], got {r}")
+def kernel_rank(r: int) -> int:
+    """The smallest rank >= ``r`` the GPU kernels instantiate. Factors of any rank <=
+    :data:`MAX_WIDE_RANK` train EXACTLY at that rank with zero-padded columns: under the
+    update rule (SGDMPTask.java:46-77) e = v - w.h ignores zero columns, and a zero column
+    of w and h receives lr * (e * 0 - lam * 0) = 0, so padded columns stay zero."""
+    if r <= 0:
+        raise ValueError(f"rank must be positive, got {r}")
+    for s in SUPPORTED_RANKS:
+        if s >= r:
+            return s
+    if r <= MAX_WIDE_RANK:
+        return (r + 3) // 4 * 4
+    raise NotImplementedError(f"native MF-SGD ranks go up to {MAX_WIDE_RANK}, got {r}")
+
+
+def storage_rank(r: int, device) -> int:
+    """Columns a model should allocate for rank-``r`` factors on ``device`` (zero-padded
+    to :func:`kernel_rank` on a GPU, so the hot loop needs no per-call padding)."""
+    dev = torch.device(device)
+    return kernel_rank(r) if dev.type == "cuda" else r
+
+
+class _Padded:
+    """Native call on factors whose rank has no kernel instantiation: zero-padded copies
+    at :func:`kernel_rank`, the trained columns copied back on exit (exact, see
+    :func:`kernel_rank`; costs a copy of W and H per call -- models allocate padded
+    storage with :func:`storage_rank` instead)."""
+
+    def __init__(self, W: torch.Tensor, H: torch.Tensor, write_back: bool = True):
+        self.W, self.H, self.wb = W, H, write_back
+        r = W.shape[1]
+        rk = kernel_rank(r)
+        self.Wp = torch.nn.functional.pad(W, (0, rk - r)).contiguous()
+        self.Hp = torch.nn.functional.pad(H, (0, rk - r)).contiguous()
+
+    def __enter__(self):
+        return self.Wp, self.Hp
+
+    def __exit__(self, *exc):
+        if self.wb and exc[0] is None:
+            r = self.W.shape[1]
+            self.W.copy_(self.Wp[:, :r])
+            self.H.copy_(self.Hp[:, :r])
+        return False
 
 _lib.register({
     "harp_mf_sgd": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_int, _lib.c_void_p,
                     _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_void_p],
     "harp_mf_xcds": [],
-    # rows, cols, vals, off, win, r, steps, chunk, blocks_per_xcd, variant, W, ldw, H, ldh, lr, lam, stream
+    # rows, cols, vals, off, win, r, steps, chunk, blocks_per_xcd, variant, W, ldw, H, ldh, lr, lam, chk, gen, pws,
+    # stream
     "harp_mf_sgd_xcd": [_lib.c_void_p] * 5 + [_lib.c_int] * 5 + [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
-                                                                 _lib.c_float, _lib.c_float, _lib.c_void_p],
+                                                                 _lib.c_float, _lib.c_float, _lib.c_void_p,
+                                                                 ctypes.c_uint64, _lib.c_void_p, _lib.c_void_p],
+    "harp_mf_chk_words": [],
+    "harp_mf_placed_ws_ints": [],
     # rows, cols, vals, off, win, r, steps, chunk, blocks_per_xcd, W, ldw, H, ldh, lr, lam, ws, stream
     "harp_mf_sgd_xcd_flow": [_lib.c_void_p] * 5 + [_lib.c_int] * 4 + [_lib.c_void_p, _lib.c_int, _lib.c_void_p,
                                                                     _lib.c_int, _lib.c_float, _lib.c_float,
@@ -92,6 +136,58 @@ def check_flow_errors(device: torch.device) -> None:
             raise RuntimeError("MF-SGD flow kernel: a cross-XCD wait timed out (results of that pass are invalid)")
 
 
+# variant 2 = mf_sgd_xcd_placed_kernel: each block trains the cell of the XCD it runs on
+# (HW_REG_XCC_ID), so one XCD per cell holds whatever the dispatcher does; the fallback
+# the models switch to when the placement check of the default kernel fires
+PLACED_VARIANT = 2
+CHECK_PLACEMENT = True  # default kernel: tag residue <-> XCC per launch, raise an error word on a mismatch
+_CHK: dict = {}
+
+
+class _Chk:
+    """Per (device, stream) placement-check words of the default XCD kernel plus the
+    launch-generation counter (a generation is never reused on the same words) and the
+    placed kernel's zeroed claim workspace."""
+
+    def __init__(self, device: torch.device):
+        lib = _lib.kernels()
+        self.words = torch.zeros(int(lib.harp_mf_chk_words()), dtype=torch.int64, device=device)
+        self.pws = torch.zeros(int(lib.harp_mf_placed_ws_ints()), dtype=torch.int32, device=device)
+        self.gen = 1
+
+    def next_gen(self, steps: int) -> int:
+        g = self.gen
+        self.gen += steps
+        return g
+
+
+def _chk(device: torch.device) -> _Chk:
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
+    c = _CHK.get(key)
+    if c is None:
+        c = _CHK[key] = _Chk(device)
+    return c
+
+
+def check_placement(device: torch.device) -> dict:
+    """Read (host sync) and clear the placement words of every stream on ``device``:
+    ``{"violation": bool, "drained": n}`` -- a violation means a default-kernel launch had
+    blocks of one residue on two XCDs, or two residues on one XCD (that pass ran Hogwild
+    across L2s: every rating was still trained once); ``drained`` counts cells the placed
+    kernel trained in its last block because their XCD received no block."""
+    out = {"violation": False, "drained": 0}
+    for (idx, _), c in _CHK.items():
+        if idx != device.index:
+            continue
+        if int(c.words[24].item()):
+            out["violation"] = True
+            c.words[24].zero_()
+        out["drained"] += int(c.pws[9].item())
+        c.pws[9].zero_()
+    return out
+
+
 def _check(rows, cols, vals, W, H):
     assert rows.dtype == torch.int32 and cols.dtype == torch.int32 and vals.dtype == torch.float32
     assert rows.is_contiguous() and cols.is_contiguous() and vals.is_contiguous()
@@ -109,7 +205,9 @@ def sgd_update(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: to
     r = W.shape[1]
     chunk = chunk if chunk > 0 else 64
     if _lib.use_native(W):
-        _require_rank(r)
+        if not supported_rank(r):
+            with _Padded(W, H) as (Wp, Hp):
+                return sgd_update(rows, cols, vals, Wp, Hp, lr, lam, chunk)
         st = _lib.kernels().harp_mf_sgd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), n, r, chunk, W.data_ptr(),
                                         W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam),
                                         _lib.stream_ptr(W.device))
@@ -177,8 +275,10 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     (csrc/mf_sgd.hip, mf_sgd_xcd_kernel); on the CPU the same cells in the same order.
     ``host_off``: the offsets as a Python list (saves a device->host copy on the CPU path).
     ``chunk``: ratings per stream (8, 16, 32, 64 or 128 on the GPU; <= 0 = :func:`auto_chunk`);
-    ``variant``: 0 = one launch per sub-step; 1 (:data:`FLOW_VARIANT`, ranks <= 256) = the
-    whole pass in one persistent launch ordered by per-XCD completion flags.
+    ``variant``: 0 = one launch per sub-step (placement-checked, :func:`check_placement`);
+    1 (:data:`FLOW_VARIANT`, ranks <= 256) = the whole pass in one persistent launch
+    ordered by per-XCD completion flags; 2 (:data:`PLACED_VARIANT`, ranks <= 256) = one
+    launch per sub-step whose blocks pick their cell by the XCD they run on.
     ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
     ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
     CPU only: ``threads > 1`` or a ``time_budget`` (s) run the cells through the 2-D
@@ -193,7 +293,10 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     assert cell_off.numel() == nb * nb + 1 and cell_off.dtype == torch.int64
     trained = n if window is None else int(sum(window[1]))
     if _lib.use_native(W):
-        _require_rank(r)
+        if not supported_rank(r):
+            with _Padded(W, H) as (Wp, Hp):
+                return sgd_update_blocked(rows, cols, vals, cell_off, Wp, Hp, lr, lam, chunk, blocks_per_xcd,
+                                          host_off, variant, window)
         assert cell_off.device == W.device and cell_off.is_contiguous()
         win = None
         if window is not None:
@@ -209,9 +312,14 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
                                           _flow_ws(W.device).data_ptr(), _lib.stream_ptr(W.device))
             _lib.check(st, "mf_sgd_xcd_flow")
         else:
+            placed = variant == PLACED_VARIANT and r <= 256
+            ck = _chk(W.device)
+            words = ck.words if (CHECK_PLACEMENT and not placed) else None
+            gen = ck.next_gen(nb) if words is not None else 0
             st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
-                                     _lib.ptr(win), r, nb, chunk, blocks_per_xcd, 0, W.data_ptr(), W.stride(0),
-                                     H.data_ptr(), H.stride(0), float(lr), float(lam), _lib.stream_ptr(W.device))
+                                     _lib.ptr(win), r, nb, chunk, blocks_per_xcd, PLACED_VARIANT if placed else 0,
+                                     W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam),
+                                     _lib.ptr(words), gen, ck.pws.data_ptr(), _lib.stream_ptr(W.device))
             _lib.check(st, "mf_sgd_xcd")
         if win is not None:
             win.record_stream(torch.cuda.current_stream(W.device))
@@ -272,6 +380,9 @@ def sse(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, W: torch.Ten
         return torch.zeros((), dtype=torch.float64, device=W.device)
     r = W.shape[1]
     if _lib.use_native(W):
+        if not supported_rank(r):
+            with _Padded(W, H, write_back=False) as (Wp, Hp):
+                return sse(rows, cols, vals, Wp, Hp)
         lib = _lib.kernels()
         nb = lib.harp_mf_rmse_blocks()
         part = torch.empty(nb, dtype=torch.float64, device=W.device)

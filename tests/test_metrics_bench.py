@@ -125,6 +125,25 @@ def test_bench_self_spawns_ranks():
     assert "sgd" not in rec  # auto: CPU ranks skip the SGD record
 
 
+def test_bench_rccl_preflight_three_ranks():
+    """The self-diagnosing pre-flight at P=3 over gloo: world size seen by
+    every rank, per-rank device records, a passing collective battery, a 64 MB all-reduce
+    bus bandwidth and one ring send/recv per rotation channel (distinct strides at P=3)."""
+    rec = _run_bench(["--gpus", "3", "--points", "3e4", "--centroids", "128", "--backend", "gloo", "--steps", "2",
+                      "--warmup", "1"])
+    r = rec["rccl"]
+    assert r["world"] == 3 and r["world_seen"] == [3, 3, 3] and r["backend"] == "gloo"
+    assert [x["rank"] for x in r["ranks"]] == [0, 1, 2]
+    assert r["distinct_devices"] is False  # CPU ranks share no device
+    assert set(r["battery"]) == {"all_gather_ints", "all_reduce", "broadcast", "all_gather", "reduce_scatter",
+                                 "all_to_all", "ring_sendrecv", "barrier", "all_reduce_64MB"}
+    assert r["battery_ok"], r["battery"]
+    assert r["all_reduce_64MB"]["busbw_GBps"] > 0 and r["all_reduce_64MB"]["ms"] > 0
+    ch = r["rotation_channels"]
+    assert [c["channel"] for c in ch] == ["sgd-h-0", "sgd-h-1"] and [c["stride"] for c in ch] == [1, 2]
+    assert all(c["ok"] and c["GBps"] > 0 for c in ch), ch
+
+
 def test_bench_single_rank_with_sgd_record():
     rec = _run_bench(["--gpus", "1", "--points", "1e4", "--centroids", "128", "--steps", "2", "--warmup", "1",
                       "--sgd", "on", "--sgd-users", "2000", "--sgd-items", "300", "--sgd-ratings", "20000",
@@ -132,6 +151,7 @@ def test_bench_single_rank_with_sgd_record():
     assert rec["n_gpus"] == 1 and rec["metric"].startswith("sec/iteration K-means")
     s = rec["sgd"]
     assert s["updates_per_sec"] > 0 and s["epochs"] == 2 and 0 < s["train_rmse"] < 2
+    assert rec["rccl"]["world"] == 1 and "battery" not in rec["rccl"]
 
 
 def test_bench_sgd_guard_keeps_headline_line():
