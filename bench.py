@@ -73,6 +73,8 @@ def parse_args(argv=None):
                          "100M-rating epoch, profiles/r3_sgd_slices), 2 at P > 1 so every slice's transfer to "
                          "the ring neighbour overlaps the other slice's compute (the reference's numModelSlices "
                          "default, MJ/dymoro/Rotator.java:30-86)")
+    ap.add_argument("--sgd-atomic", type=int, default=-1,
+                    help="1/0: atomic (no-lost-update) write-back of the blocked SGD kernel; -1 = SGDConfig default")
     ap.add_argument("--sgd-timeout", type=float, default=240.0,
                     help="wall-clock bound (s) on the nested MF-SGD record; past it rank 0 prints the "
                          "K-means line with an sgd error and every rank exits")
@@ -352,6 +354,8 @@ def bench_sgd(args, comm, torch):
     u, i, v = synthetic_ratings(args.sgd_users, args.sgd_items, args.sgd_ratings, seed=7, device=dev)
     cfg = SGDConfig(rank=args.sgd_rank, epochs=args.sgd_warmup + args.sgd_epochs, test_every=0,
                     xcd_blocks=dev.type == "cuda", num_slices=args.sgd_slices or (1 if P == 1 else 2))
+    if args.sgd_atomic >= 0:
+        cfg.atomic = bool(args.sgd_atomic)
     m = SGDCollectiveMapper(comm, cfg, args.sgd_users, args.sgd_items, (u, i, v), None)
     m.init_model(_Reader())
     del u, i, v
@@ -402,6 +406,7 @@ def bench_sgd(args, comm, torch):
         "rotation_exposed_s_per_epoch": round(rot_exposed / max(args.sgd_epochs, 1), 6),
         "rotation_strides": [s.stride for s in m.schedules],
         "xcd_placement": placement,
+        "atomic_writeback": cfg.atomic,
         "train_rmse": round(train_rmse, 6),
         "users": args.sgd_users, "items": args.sgd_items, "ratings": args.sgd_ratings, "rank": args.sgd_rank,
         "slices_per_rank": cfg.num_slices,

@@ -88,6 +88,26 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&x
   }
 }
 
+// Delta write-back for conflicting concurrent streams (ATOM kernels): x is ADDED to the row
+// with L2 float atomics (no return) instead of overwriting it, so two streams that update
+// one row at the same time both keep their contribution (a plain store keeps only the last
+// writer's). Workgroup scope: all global atomics execute in the XCD's L2, which every CU of
+// the XCD shares -- the only agents that touch a cell's rows inside a launch.
+template <int EPL>
+__device__ __forceinline__ void add_row(float* __restrict__ p, const float (&x)[EPL]) {
+  if constexpr (EPL % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_fetch_add(p + 16 * k + j, x[k + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      __hip_atomic_fetch_add(p + 16 * k, x[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
 // W rows: L1-cached loads, or (persistent flow kernel, where rows written earlier in the
 // same launch by other CUs of the XCD must be seen) loads from L2 like the H rows
 template <int EPL, bool L2>
@@ -266,26 +286,54 @@ constexpr int XCDS = 8;
 // store waits changed nothing, while ablating the H stores (+66 %) or the H loads (+32 %)
 // and uniform instead of skewed item popularity (+30 %) did: the kernel is bound by L2
 // traffic on hot H rows.
-template <int R, bool WL2 = false>
+//
+// ATOM: conflict-preserving write-back. Concurrent streams of an XCD share hot H rows and
+// the rows of users whose ratings straddle two streams; a plain store keeps one writer's
+// update (measured on the reference's ML-10M gate: 0.855 test RMSE after 200 epochs on the
+// GPU vs 0.834 sequential). With ATOM the H write of a rating is an L2 atomic add of that
+// rating's change, and a W row is written back as the atomic add of the stream's total
+// change to it (w - w at load), so no update is lost -- concurrent updates are merely stale.
+template <int R, bool WL2 = false, bool ATOM = false>
 __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, const float* sV, int n, int sl,
                                                float* __restrict__ W, unsigned ldw, float* __restrict__ H,
                                                unsigned ldh, float lr, float lam) {
   constexpr int EPL = R / 16;
   constexpr int PAIRS = EPL / 2;
+  constexpr int W0 = ATOM ? EPL : 1;
   const float decay = 1.0f - lr * lam;
   const unsigned lo = lane_off<EPL>(sl);
   float w[EPL], h[EPL], hp[EPL], hA[EPL], hB[EPL];
+  float w0[W0];  // ATOM: the W row as loaded (its write-back is w - w0)
+  auto keep_w0 = [&]() {
+    if constexpr (ATOM) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) w0[k] = w[k];
+    }
+  };
+  auto put_w = [&](float* p) {
+    if constexpr (ATOM) {
+      float dw[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) dw[k] = w[k] - w0[k];
+      add_row<EPL>(p, dw);
+    } else {
+      store_row<EPL>(p, w);
+    }
+  };
   unsigned cur = (unsigned)sR[0], col0 = (unsigned)sC[0], colp = 0xffffffffu;
   float v0 = sV[0];
   const int i1c = n > 1 ? 1 : 0;
   unsigned row1 = (unsigned)sR[i1c], col1 = (unsigned)sC[i1c];
   float v1 = sV[i1c];
   load_w<EPL, WL2>(W + (cur * ldw + lo), w);
+  keep_w0();
   load_row_l2<EPL>(H + (col0 * ldh + lo), h);
   load_row_l2<EPL>(H + (col1 * ldh + lo), hB);
 #pragma unroll
   for (int k = 0; k < EPL; ++k) hp[k] = 0.f;
   int i = 0;
+  float dh[ATOM ? EPL : 1];  // ATOM: this rating's change of its H row
+  const float dm1 = -lr * lam;
   auto step = [&](float(&hl)[EPL], float(&hx)[EPL]) -> bool {
     floatx2 d2 = {0.f, 0.f};
 #pragma unroll
@@ -299,28 +347,45 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     for (int p = 0; p < PAIRS; ++p) {
       const floatx2 wk = {w[2 * p], w[2 * p + 1]}, hk = {h[2 * p], h[2 * p + 1]};
       const floatx2 wn = __builtin_elementwise_fma(g, hk, dc * wk);
-      const floatx2 hn = __builtin_elementwise_fma(g, wk, dc * hk);
+      if constexpr (ATOM) {
+        const floatx2 d = __builtin_elementwise_fma(g, wk, floatx2{dm1, dm1} * hk);
+        dh[2 * p] = d[0];
+        dh[2 * p + 1] = d[1];
+        h[2 * p] += d[0];
+        h[2 * p + 1] += d[1];
+      } else {
+        const floatx2 hn = __builtin_elementwise_fma(g, wk, dc * hk);
+        h[2 * p] = hn[0];
+        h[2 * p + 1] = hn[1];
+      }
       w[2 * p] = wn[0];
       w[2 * p + 1] = wn[1];
-      h[2 * p] = hn[0];
-      h[2 * p + 1] = hn[1];
     }
     if constexpr (EPL % 2) {
       const float wk = w[EPL - 1], hk = h[EPL - 1];
       w[EPL - 1] = fmaf(ge, hk, decay * wk);
-      h[EPL - 1] = fmaf(ge, wk, decay * hk);
+      if constexpr (ATOM) {
+        dh[EPL - 1] = fmaf(ge, wk, dm1 * hk);
+        h[EPL - 1] = hk + dh[EPL - 1];
+      } else {
+        h[EPL - 1] = fmaf(ge, wk, decay * hk);
+      }
     }
     const bool last = i + 1 >= n;
     if (!last && row1 != cur) {
-      store_row<EPL>(W + (cur * ldw + lo), w);
+      put_w(W + (cur * ldw + lo));
       cur = row1;
       load_w<EPL, WL2>(W + (cur * ldw + lo), w);
+      keep_w0();
     }
     const int i2 = i + 2 < n ? i + 2 : n - 1;  // clamped: the last prefetch is a harmless re-read
     const unsigned row2 = (unsigned)sR[i2], col2 = (unsigned)sC[i2];
     const float v2 = sV[i2];
     load_row_l2<EPL>(H + (col2 * ldh + lo), hl);
-    store_row<EPL>(H + (col0 * ldh + lo), h);
+    if constexpr (ATOM)
+      add_row<EPL>(H + (col0 * ldh + lo), dh);
+    else
+      store_row<EPL>(H + (col0 * ldh + lo), h);
     if (last) return false;
     // row of rating i+1: just updated (same item as i), updated one rating ago (same item as
     // i-1, its store was issued after the prefetch), or the prefetched copy
@@ -342,7 +407,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
   };
   while (step(hA, hB) && step(hB, hA)) {
   }
-  store_row<EPL>(W + (cur * ldw + lo), w);
+  put_w(W + (cur * ldw + lo));
 }
 
 // Sub-step `step` of the XCD-blocked schedule. off[c] .. off[c + 1] are the ratings of cell
@@ -386,7 +451,7 @@ __device__ __forceinline__ void placement_check(unsigned long long* chk, unsigne
   if (bad) __hip_atomic_store(chk + kChkErr, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int R, int CH>
+template <int R, int CH, bool ATOM>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
                                                          const long* __restrict__ win, int step,
@@ -422,7 +487,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
     __syncthreads();
     const long mine = n - (r0 + (long)sub * CH);
     if (mine > 0)
-      sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
+      sgd_stream_lds<R, false, ATOM>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
                              (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
 }
@@ -438,7 +503,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
 // ws layout (int32): claim[8] | exit | drained
 constexpr int kPlacedWs = 10;
 
-template <int R, int CH>
+template <int R, int CH, bool ATOM>
 __device__ __forceinline__ void xcd_round(const int* __restrict__ rows, const int* __restrict__ cols,
                                           const float* __restrict__ vals, long a, long w0, long ncell, long n, long rd,
                                           int* sR, int* sC, float* sV, float* __restrict__ W, int ldw,
@@ -459,11 +524,12 @@ __device__ __forceinline__ void xcd_round(const int* __restrict__ rows, const in
   __syncthreads();
   const long left = n - (r0 + (long)sub * CH);
   if (left > 0)
-    sgd_stream_lds<R>(sR + sub * CH, sC + sub * CH, sV + sub * CH, left < CH ? (int)left : CH, sl, W, (unsigned)ldw, H,
+    sgd_stream_lds<R, false, ATOM>(sR + sub * CH, sC + sub * CH, sV + sub * CH, left < CH ? (int)left : CH, sl, W,
+                                   (unsigned)ldw, H,
                       (unsigned)ldh, lr, lam);
 }
 
-template <int R, int CH>
+template <int R, int CH, bool ATOM>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_placed_kernel(const int* __restrict__ rows,
                                                                 const int* __restrict__ cols,
                                                                 const float* __restrict__ vals,
@@ -492,7 +558,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_placed_kernel(const int* __res
     const long rd = s_round;
     __syncthreads();  // everyone read s_round before it is rewritten
     if (rd >= rounds) break;
-    xcd_round<R, CH>(rows, cols, vals, a, w0, ncell, n, rd, sR, sC, sV, W, ldw, H, ldh, lr, lam);
+    xcd_round<R, CH, ATOM>(rows, cols, vals, a, w0, ncell, n, rd, sR, sC, sV, W, ldw, H, ldh, lr, lam);
   }
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(ws + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
@@ -503,7 +569,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_placed_kernel(const int* __res
     cell_of(xx, a, w0, ncell, n);
     const long rr = (n + 16 * CH - 1) / (16 * CH);
     for (long rd = 0; rd < rr; ++rd)
-      xcd_round<R, CH>(rows, cols, vals, a, w0, ncell, n, rd, sR, sC, sV, W, ldw, H, ldh, lr, lam);
+      xcd_round<R, CH, ATOM>(rows, cols, vals, a, w0, ncell, n, rd, sR, sC, sV, W, ldw, H, ldh, lr, lam);
     if (threadIdx.x == 0 && rr > 0) __hip_atomic_fetch_add(ws + 9, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
@@ -711,19 +777,31 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
+constexpr int kAtomBit = 4;  // variant bit: ATOM write-back (sgd_stream_lds)
+
 // variant 0: blockIdx-placed sub-steps (+ placement check when chk != NULL; `gen` is the
 // first launch's generation, one per sub-step); 2: mf_sgd_xcd_placed_kernel (pws)
 template <int R, int CH>
 int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const long* off, const long* win, int steps,
                    int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, int variant,
                    unsigned long long* chk, unsigned long long gen, int* pws, hipStream_t s) {
+  const dim3 grid((unsigned)(blocks_per_xcd * XCDS));
+  const bool atom = (variant & kAtomBit) != 0;
+  const bool placed = (variant & ~kAtomBit) == 2;
   for (int step = 0; step < steps; ++step) {
-    if (variant == 2)
-      mf_sgd_xcd_placed_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam, pws);
+    const unsigned long long g = gen + (unsigned long long)step;
+    if (placed && atom)
+      mf_sgd_xcd_placed_kernel<R, CH, true><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H,
+                                                                       ldh, lr, lam, pws);
+    else if (placed)
+      mf_sgd_xcd_placed_kernel<R, CH, false><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H,
+                                                                        ldh, lr, lam, pws);
+    else if (atom)
+      mf_sgd_xcd_kernel<R, CH, true><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H, ldh, lr,
+                                                                lam, chk, g);
     else
-      mf_sgd_xcd_kernel<R, CH><<<dim3((unsigned)(blocks_per_xcd * XCDS)), dim3(256), 0, s>>>(
-          rows, cols, vals, off, win, step, W, ldw, H, ldh, lr, lam, chk, gen + (unsigned long long)step);
+      mf_sgd_xcd_kernel<R, CH, false><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H, ldh, lr,
+                                                                 lam, chk, g);
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -984,7 +1062,8 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 // `variant`: 0 = blockIdx-placed sub-steps, checked when `chk` (harp_mf_chk_words() zeroed
 // uint64 per stream) is given: launch generations gen .. gen + steps - 1 (> 0, never reused
 // on that chk); 2 = the placement-independent kernel (`pws`: harp_mf_placed_ws_ints()
-// zeroed int32, left zeroed; ranks <= 256). Non-temporal H stores (23 % slower) and forced
+// zeroed int32, left zeroed; ranks <= 256); + 4 (kAtomBit, ranks <= 256): the ATOM
+// write-back (H / W changes added with L2 atomics, no lost updates). Non-temporal H stores (23 % slower) and forced
 // 6 / 7 / 8 waves per SIMD were measured in round 1 and are no longer built.
 // `win`: optional DEVICE array [2 x 64] of per-cell window starts and lengths (NULL = all).
 HARP_EXPORT int harp_mf_chk_words() { return kChkWords; }
@@ -994,9 +1073,11 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
                                 int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
                                 float* H, int ldh, float lr, float lam, unsigned long long* chk,
                                 unsigned long long gen, int* pws, hipStream_t s) {
-  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || (variant != 0 && variant != 2))
+  const int base_variant = variant & ~kAtomBit;
+  if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || (base_variant != 0 && base_variant != 2))
     return HARP_EBADARG;
-  if ((chk && gen == 0) || (variant == 2 && (!pws || wide_ok(r)))) return HARP_EBADARG;
+  if ((chk && gen == 0) || (base_variant == 2 && (!pws || wide_ok(r))) || ((variant & kAtomBit) && wide_ok(r)))
+    return HARP_EBADARG;
   if (wide_ok(r)) {  // wide ranks: one wave per stream
     if (chunk != 32 && chunk != 64 && chunk != 128) return HARP_EBADARG;
 #define SGDXW_CALL(QQ) \

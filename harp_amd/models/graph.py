@@ -61,6 +61,38 @@ def parse_adjacency(lines: Sequence[str]) -> Tuple[torch.Tensor, torch.Tensor, t
     return torch.tensor(src, dtype=torch.long), torch.tensor(dst, dtype=torch.long), torch.tensor(nodes, dtype=torch.long)
 
 
+def load_adjacency_dir(path: str, undirected: bool = True):
+    """SAHAD / FASCIA graph files (datasets/daal_subgraph/graphs/*: ``vertex<TAB>n1,n2,...,``
+    per line, any number of files) -> (src, dst, n_vertices). ``undirected``: both
+    directions of every edge, self loops and duplicates removed (the subgraph counters
+    treat the input as a simple undirected graph)."""
+
+    import numpy as np
+
+    from ..utils.datasets import list_files
+
+    srcs, dsts = [], []
+    for fn in list_files(path):
+        with open(fn) as f:
+            for ln in f:
+                head, _, rest = ln.partition("\t")
+                if not head.strip():
+                    continue
+                nb = np.array(rest.replace(",", " ").split(), dtype=np.int64)
+                srcs.append(np.full(nb.size, int(head), dtype=np.int64))
+                dsts.append(nb)
+    s = np.concatenate(srcs) if srcs else np.zeros(0, dtype=np.int64)
+    t = np.concatenate(dsts) if dsts else np.zeros(0, dtype=np.int64)
+    n = int(max(s.max(initial=-1), t.max(initial=-1))) + 1
+    if undirected:
+        keep = s != t
+        a, b = np.minimum(s[keep], t[keep]), np.maximum(s[keep], t[keep])
+        key = np.unique(a * n + b)
+        a, b = key // n, key % n
+        s, t = np.concatenate([a, b]), np.concatenate([b, a])
+    return torch.from_numpy(s), torch.from_numpy(t), n
+
+
 # ---------------------------------------------------------------- PageRank
 def pagerank(comm: Communicator, src: torch.Tensor, dst: torch.Tensor, nodes: torch.Tensor, num_urls: int,
              iterations: int = 10, damping: float = 0.85) -> torch.Tensor:

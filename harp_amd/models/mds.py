@@ -220,6 +220,43 @@ def _max():
     return Operation.MAX
 
 
+def read_ids(path: str) -> List[Dict[str, int]]:
+    """A wdamds ids file (tutorial/mds_data/ids/*_ids): per row block ``id height width
+    id row_offset`` (tab separated; MDSDataSplit / DataFileUtil layout)."""
+    out = []
+    with open(path) as f:
+        for ln in f:
+            t = ln.split()
+            if len(t) >= 5:
+                out.append({"id": int(t[0]), "height": int(t[1]), "width": int(t[2]), "row0": int(t[4])})
+    return out
+
+
+def load_row_block(data_dir: str, kind: str, block: Dict[str, int]) -> torch.Tensor:
+    """One row block of the reference's binary matrices (DataFileUtil.java:150-200:
+    big-endian Java shorts, row-major ``height x width``): ``kind`` "distance" ->
+    delta / Short.MAX_VALUE (fp64), "weight" -> the short value as fp64."""
+    import numpy as np
+
+    path = os.path.join(data_dir, f"{kind}_{block['id']}")
+    a = np.fromfile(path, dtype=">i2")
+    if a.size != block["height"] * block["width"]:
+        raise ValueError(f"{path}: {a.size} shorts, expected {block['height']} x {block['width']}")
+    a = a.reshape(block["height"], block["width"]).astype(np.float64)
+    if kind == "distance":
+        a /= 32767.0
+    return torch.from_numpy(a)
+
+
+def load_rows(data_dir: str, ids_dir: str, blocks: List[int]):
+    """(delta rows, weight rows, first row) of the consecutive row blocks ``blocks``."""
+    dist_ids = {b["id"]: b for b in read_ids(os.path.join(ids_dir, "distance_ids"))}
+    w_ids = {b["id"]: b for b in read_ids(os.path.join(ids_dir, "weight_ids"))}
+    D = torch.cat([load_row_block(data_dir, "distance", dist_ids[b]) for b in blocks])
+    W = torch.cat([load_row_block(data_dir, "weight", w_ids[b]) for b in blocks])
+    return D, W, dist_ids[blocks[0]]["row0"]
+
+
 def quantize_distances(D: torch.Tensor) -> torch.Tensor:
     """The reference's storage format: short(delta / max * Short.MAX_VALUE), back to
     [0, 1] doubles."""

@@ -45,6 +45,7 @@ class SGDConfig:
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
     kernel_variant: int = 0    # blocked kernel: 0 = a launch per sub-step, 1 = persistent flow kernel (ops.mf)
+    atomic: bool = False       # GPU blocked kernel: add H / W changes with L2 atomics (no lost concurrent updates)
     train_fraction: float = 1.0  # per rotation step each cell trains this fraction (window advances per epoch)
     random_order: bool = False  # random rotation orders (RotationUtil) vs ring
     test_every: int = 5        # rmseIteInterval
@@ -289,7 +290,7 @@ class SGDCollectiveMapper(CollectiveMapper):
                         win = MF.cell_windows(hoff, cfg.train_fraction, epoch) if cfg.train_fraction < 1.0 else None
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
                                                    cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
-                                                   window=win)
+                                                   window=win, atomic=cfg.atomic)
                     else:
                         if cfg.train_fraction < 1.0:
                             raise ValueError("train_fraction < 1 needs the XCD-blocked layout")
@@ -327,7 +328,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             if cfg.xcd_blocks:
                 return MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
                                              cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
-                                             window=(starts, L))
+                                             window=(starts, L), atomic=cfg.atomic)
             a, m = starts[0], L[0]
             return MF.sgd_update(r_[a:a + m], c_[a:a + m], v_[a:a + m], self.W, slab, cfg.lr, cfg.lam,
                                  cfg.chunk) if m else 0

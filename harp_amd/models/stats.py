@@ -383,11 +383,25 @@ def sort_features(X: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ outlier detection
-def outliers_univariate(X: torch.Tensor, threshold: float = 3.0, comm: Optional[Communicator] = None) -> torch.Tensor:
-    """Per-feature weights (1 = inlier): |x - mean| / std <= threshold, with global moments
-    (DAAL univariate_outlier_detection default initialization)."""
-    mom = low_order_moments(X, comm)
-    z = (X.double() - mom["mean"].to(X.device)) / mom["standardDeviation"].to(X.device).clamp_min(1e-300)
+def outliers_univariate(X: torch.Tensor, threshold: float = 3.0, comm: Optional[Communicator] = None,
+                        init: str = "moments", location: Optional[torch.Tensor] = None,
+                        scatter: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-feature weights (1 = inlier): |x - location| / scatter <= threshold.
+    ``init``: "moments" (global mean / standard deviation), "default" (DAAL
+    univariate_outlier_detection's default initialisation: location 0, scatter 1 -- the
+    reference app, daal_outlier/unidensebatch, runs it), or "given" (``location`` /
+    ``scatter`` per feature)."""
+    if init == "moments":
+        mom = low_order_moments(X, comm)
+        loc, sc = mom["mean"].to(X.device), mom["standardDeviation"].to(X.device)
+    elif init == "default":
+        loc = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+        sc = torch.ones_like(loc)
+    elif init == "given":
+        loc, sc = location.double().to(X.device), scatter.double().to(X.device)
+    else:
+        raise ValueError(init)
+    z = (X.double() - loc) / sc.clamp_min(1e-300)
     return (z.abs() <= threshold).to(X.dtype)
 
 

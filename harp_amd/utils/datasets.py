@@ -123,11 +123,14 @@ def load_features_labels(path: str, n_labels: int = 1) -> Tuple[torch.Tensor, to
 
 
 def load_daal_csr(path: str, n_cols: Optional[int] = None) -> torch.Tensor:
-    """DAAL CSR text: line 1 row offsets, line 2 column indices, line 3 values (1-based)."""
+    """DAAL CSR text: line 1 row offsets, line 2 column indices, line 3 values (1-based).
+    A file whose column indices contain 0 is read as zero-based columns (the reference's
+    daal_kernelfunc/csrbatch fixture mixes 1-based offsets with 0-based columns)."""
     with open(path) as f:
         lines = [ln.strip().rstrip(",") for ln in f if ln.strip()]
     ro = np.array([int(x) for x in lines[0].split(",")], dtype=np.int64) - 1
-    ci = np.array([int(x) for x in lines[1].split(",")], dtype=np.int64) - 1
+    ci = np.array([int(x) for x in lines[1].split(",")], dtype=np.int64)
+    ci = ci - (0 if ci.size and ci.min() == 0 else 1)
     va = np.array([float(x) for x in lines[2].split(",")], dtype=np.float64)
     nc = n_cols or int(ci.max()) + 1
     return torch.sparse_csr_tensor(torch.from_numpy(ro), torch.from_numpy(ci), torch.from_numpy(va),

@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--threads", type=int, default=4, help="CPU BlockScheduler threads per worker")
     ap.add_argument("--epochs", type=int, default=200)
     ap.add_argument("--rank", type=int, default=40)
+    ap.add_argument("--atomic", type=int, default=-1, help="GPU: atomic write-back (1/0; -1 = model default)")
+    ap.add_argument("--blocks-per-xcd", type=int, default=0)
+    ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--pack", action="store_true", help=f"write {PACKED} from the reference text files and exit")
     args = ap.parse_args()
     if args.pack:
@@ -88,14 +91,19 @@ def main():
     load_s = time.perf_counter() - t0
     nu, ni = int(max(u.max(), tu.max())) + 1, int(max(i.max(), ti.max())) + 1
     cfg = SGDConfig(rank=args.rank, lam=0.05, lr=0.002, epochs=args.epochs, num_slices=2, test_every=5,
-                    init="reference", cpu_threads=args.threads if args.device == "cpu" else 1)
+                    init="reference", cpu_threads=args.threads if args.device == "cpu" else 1, chunk=args.chunk)
+    if args.atomic >= 0:
+        cfg.atomic = bool(args.atomic)
+    if args.blocks_per_xcd:
+        cfg.blocks_per_xcd = args.blocks_per_xcd
     res = launch(job, args.workers, args=(cfg, nu, ni, (u, i, v.float()), (tu, ti, tv.float()), args.device),
                  timeout=1100)
     r0 = res[0]
     test_rmse = r0["rmse"][-1][2]
     out = {
         "gate": "mfsgd.sh:64 r=40 lambda=0.05 eps=0.002 200 iters 2 workers, test RMSE in (0.80, 0.84)",
-        "data": src, "device": args.device, "workers": args.workers, "rank": args.rank, "storage_rank": r0["storage_rank"],
+        "data": src, "device": args.device, "atomic": cfg.atomic, "blocks_per_xcd": cfg.blocks_per_xcd,
+        "chunk": cfg.chunk, "workers": args.workers, "rank": args.rank, "storage_rank": r0["storage_rank"],
         "train_ratings": int(u.numel()), "test_ratings": int(tu.numel()),
         "test_rmse": test_rmse, "pass": 0.80 < test_rmse < 0.84, "reference_run": 0.8345,
         "trained": sum(r["trained"] for r in res),

@@ -2,7 +2,7 @@
 # round 5 first GPU pass: any-rank MF-SGD, placement check / placed kernel, LDA K%4 fused rows,
 # the ML-10M gate at r=40 on the GPU, and the full bench
 set -o pipefail
-O=gpurun_out/r5a
+O=gpurun_out/round5_a
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread \

@@ -154,3 +154,41 @@ def test_placement_under_cu_hog(cuda, hog_us):
         assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
     print(f"hog {hog_us} us: default check {outs[0]}, placed {outs[MF.PLACED_VARIANT]}")
     assert not outs[MF.PLACED_VARIANT]["violation"]  # the placed kernel is never checked / never wrong
+
+
+@pytest.mark.parametrize("variant", [0, MF.PLACED_VARIANT])
+@pytest.mark.parametrize("r", [16, 40, 128])
+def test_atomic_writeback_one_stream_per_cell_matches_cpu(cuda, variant, r):
+    """ATOM write-back (H / W changes added with L2 atomics): with one stream per cell there
+    is no concurrency, so the result is the CPU schedule's up to the rounding of w0 + (w - w0)."""
+    R, C, V, off, W0, H0 = _cells(64, 48, 4000, r, 13)
+    Wc, Hc = W0.clone(), H0.clone()
+    MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.01, 0.05)
+    Wg, Hg = W0.to(cuda), H0.to(cuda)
+    MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=128,
+                          blocks_per_xcd=4, variant=variant, atomic=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
+
+
+def test_atomic_writeback_keeps_concurrent_updates(cuda):
+    """Many streams on few rows (3000 users x 100 items, chunk 8): a plain store loses the
+    updates of concurrent writers, the atomic write-back keeps them -- after the same passes
+    its error is at least as low as the sequential CPU schedule's neighbourhood and clearly
+    below the lossy store's."""
+    R, C, V, off, W0, H0 = _cells(3000, 100, 200000, 32, 5)
+    Rg, Cg, Vg, og = R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda)
+    Wc, Hc = W0.clone(), H0.clone()
+    Wa, Ha = W0.to(cuda), H0.to(cuda)
+    Wb, Hb = W0.to(cuda), H0.to(cuda)
+    for _ in range(3):
+        MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.002, 0.05)
+        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wa, Ha, 0.002, 0.05, chunk=8, atomic=True)
+        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wb, Hb, 0.002, 0.05, chunk=8, atomic=False)
+    torch.cuda.synchronize()
+    e0 = MF.sse(R, C, V, W0, H0).item()
+    ec = MF.sse(R, C, V, Wc, Hc).item()
+    ea = MF.sse(Rg, Cg, Vg, Wa, Ha).item()
+    eb = MF.sse(Rg, Cg, Vg, Wb, Hb).item()
+    print(f"sse initial {e0:.5g} cpu {ec:.5g} atomic {ea:.5g} store {eb:.5g}")
+    assert ea < e0 and abs(ea - ec) < 0.05 * (e0 - ec)
