@@ -392,7 +392,7 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 
 
 // ---------------------------------------------------------------------------------------
-// Sparse-doc sampler (any K <= 16384; the only path for K > 1024 — BASELINE #5 runs
+// Sparse-doc sampler (any K <= 32768; the only path for K > 1024 — BASELINE #5 runs
 // K = 10,000). The reference's SparseLDA (LDAMPTask.java:85-330) splits
 //   p(t) ~ (n_dt + alpha) * qw_t,   qw_t = (n_wt + beta) / (n_t + V beta)
 // into a doc bucket sum_t n_dt qw_t and a smoothing bucket alpha * sum_t qw_t. Here the
@@ -400,7 +400,7 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 // other tokens j of qw[z_j], so a token reads its document's topic list (zdoc, doc
 // order, 2 B per token: a few hundred bytes, not a K-wide row) and gathers qw from LDS.
 //  * ONE workgroup per word chunk; the word's qw[Kp] row lives in LDS (4 B x Kp: 40 KB at
-//    K = 10,000, four 8-wave workgroups per CU) and the workgroup's waves sample the
+//    K = 10,000, four 8-wave workgroups per CU; 128 KB at the K = 32768 limit, one per CU) and the workgroup's waves sample the
 //    chunk's tokens round-robin. qw is linear in the count (a move changes qw_t by exactly
 //    +-1/(n_t + V beta)), so moves are LDS float atomics on qw itself and no count row is
 //    kept (an 8 B/topic {count, qw} layout fitted only two workgroups per CU: 0.85e9 vs
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
   // LDS atomics, flushed at the chunk end
   int* s_wd = wdelta == 1 ? (int*)(smem + 2 * Kp) + (long)(threadIdx.x >> 6) * Kp
                           : wdelta == 2 ? (int*)(smem + (ldelta ? 2 : 1) * Kp) : nullptr;
-  __shared__ float s_bs[256];  // per-64-topic block sums of qw (Kp <= 16384)
+  __shared__ float s_bs[512];  // per-64-topic block sums of qw (Kp <= 32768)
   __shared__ float s_q;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -803,6 +803,10 @@ namespace {
 // deltas + per-wave word rows; <= 4096: workgroup topic deltas + one workgroup word row
 // (chunk-end flush); larger: qw only (both deltas as global atomics -- a second 40 KB row
 // would halve the resident workgroups at K = 10,000).
+// K limit of the sparse sampler: the word's qw row (4 B per topic) lives in LDS, so 32768
+// topics take 128 KB of the CU's 160 KB (one workgroup per CU); larger K runs the exact
+// host sampler (ops/lda.py cgs_sample)
+constexpr int kSparseMaxK = 32768;
 int sparse_wdelta(int Kp) { return Kp <= 1024 ? 1 : Kp <= 4096 ? 2 : 0; }
 size_t sparse_lds_bytes(int Kp, int waves) {
   const int wd = sparse_wdelta(Kp);
@@ -847,7 +851,7 @@ HARP_EXPORT int harp_lda_cgs_sparse(const int* tdoc, const int* tword, int* tz, 
                                     int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K,
                                     float alpha, float beta, unsigned long long seed, int waves, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  if (K <= 0 || K > 16384 || ldw < K || (ndk && ldd < K) || !tpos || !doc_off || !zdoc || !work) return HARP_EBADARG;
+  if (K <= 0 || K > kSparseMaxK || ldw < K || (ndk && ldd < K) || !tpos || !doc_off || !zdoc || !work) return HARP_EBADARG;
   const int det = waves < 0 ? 1 : 0;  // waves < 0: one one-wave workgroup, bit-reproducible (tests)
   if (det) waves = 1;
   if (waves == 0) {  // auto: the smallest workgroup that still puts >= 24 waves on a CU
@@ -900,7 +904,7 @@ HARP_EXPORT int harp_lda_cgs_sparse_span(const long* tspan, const int* tword, in
                                          int K, float alpha, float beta, unsigned long long seed, int waves,
                                          hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  if (K <= 0 || K > 16384 || ldw < K || !tspan || !tpos || !zdoc || !work) return HARP_EBADARG;
+  if (K <= 0 || K > kSparseMaxK || ldw < K || !tspan || !tpos || !zdoc || !work) return HARP_EBADARG;
   const int det = waves < 0 ? 1 : 0;
   if (det) waves = 1;
   if (waves == 0) {

@@ -290,28 +290,31 @@ constexpr int XCDS = 8;
 // ATOM: conflict-preserving write-back. Concurrent streams of an XCD share hot H rows and
 // the rows of users whose ratings straddle two streams; a plain store keeps one writer's
 // update (measured on the reference's ML-10M gate: 0.855 test RMSE after 200 epochs on the
-// GPU vs 0.834 sequential). With ATOM the H write of a rating is an L2 atomic add of that
-// rating's change, and a W row is written back as the atomic add of the stream's total
-// change to it (w - w at load), so no update is lost -- concurrent updates are merely stale.
-template <int R, bool WL2 = false, bool ATOM = false>
+// GPU vs 0.834 sequential). Bit 0: a W row is written back as the atomic add of the
+// stream's total change to it (w - w at load; one add per factor per user run). Bit 1:
+// the H write of every rating is an L2 atomic add of that rating's change (measured 60x
+// slower on the skewed Netflix-shape bench: hot rows serialise in the L2 atomic units).
+// With both no update is lost -- concurrent updates are merely stale.
+template <int R, bool WL2 = false, int ATOM = 0>
 __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, const float* sV, int n, int sl,
                                                float* __restrict__ W, unsigned ldw, float* __restrict__ H,
                                                unsigned ldh, float lr, float lam) {
   constexpr int EPL = R / 16;
   constexpr int PAIRS = EPL / 2;
-  constexpr int W0 = ATOM ? EPL : 1;
+  constexpr bool AW = (ATOM & 1) != 0, AH = (ATOM & 2) != 0;
+  constexpr int W0 = AW ? EPL : 1;
   const float decay = 1.0f - lr * lam;
   const unsigned lo = lane_off<EPL>(sl);
   float w[EPL], h[EPL], hp[EPL], hA[EPL], hB[EPL];
   float w0[W0];  // ATOM: the W row as loaded (its write-back is w - w0)
   auto keep_w0 = [&]() {
-    if constexpr (ATOM) {
+    if constexpr (AW) {
 #pragma unroll
       for (int k = 0; k < EPL; ++k) w0[k] = w[k];
     }
   };
   auto put_w = [&](float* p) {
-    if constexpr (ATOM) {
+    if constexpr (AW) {
       float dw[EPL];
 #pragma unroll
       for (int k = 0; k < EPL; ++k) dw[k] = w[k] - w0[k];
@@ -332,7 +335,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
 #pragma unroll
   for (int k = 0; k < EPL; ++k) hp[k] = 0.f;
   int i = 0;
-  float dh[ATOM ? EPL : 1];  // ATOM: this rating's change of its H row
+  float dh[AH ? EPL : 1];  // AH: this rating's change of its H row
   const float dm1 = -lr * lam;
   auto step = [&](float(&hl)[EPL], float(&hx)[EPL]) -> bool {
     floatx2 d2 = {0.f, 0.f};
@@ -347,7 +350,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     for (int p = 0; p < PAIRS; ++p) {
       const floatx2 wk = {w[2 * p], w[2 * p + 1]}, hk = {h[2 * p], h[2 * p + 1]};
       const floatx2 wn = __builtin_elementwise_fma(g, hk, dc * wk);
-      if constexpr (ATOM) {
+      if constexpr (AH) {
         const floatx2 d = __builtin_elementwise_fma(g, wk, floatx2{dm1, dm1} * hk);
         dh[2 * p] = d[0];
         dh[2 * p + 1] = d[1];
@@ -364,7 +367,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     if constexpr (EPL % 2) {
       const float wk = w[EPL - 1], hk = h[EPL - 1];
       w[EPL - 1] = fmaf(ge, hk, decay * wk);
-      if constexpr (ATOM) {
+      if constexpr (AH) {
         dh[EPL - 1] = fmaf(ge, wk, dm1 * hk);
         h[EPL - 1] = hk + dh[EPL - 1];
       } else {
@@ -382,7 +385,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     const unsigned row2 = (unsigned)sR[i2], col2 = (unsigned)sC[i2];
     const float v2 = sV[i2];
     load_row_l2<EPL>(H + (col2 * ldh + lo), hl);
-    if constexpr (ATOM)
+    if constexpr (AH)
       add_row<EPL>(H + (col0 * ldh + lo), dh);
     else
       store_row<EPL>(H + (col0 * ldh + lo), h);
@@ -451,7 +454,7 @@ __device__ __forceinline__ void placement_check(unsigned long long* chk, unsigne
   if (bad) __hip_atomic_store(chk + kChkErr, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int R, int CH, bool ATOM>
+template <int R, int CH, int ATOM>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__ rows, const int* __restrict__ cols,
                                                          const float* __restrict__ vals, const long* __restrict__ off,
                                                          const long* __restrict__ win, int step,
@@ -503,7 +506,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
 // ws layout (int32): claim[8] | exit | drained
 constexpr int kPlacedWs = 10;
 
-template <int R, int CH, bool ATOM>
+template <int R, int CH, int ATOM>
 __device__ __forceinline__ void xcd_round(const int* __restrict__ rows, const int* __restrict__ cols,
                                           const float* __restrict__ vals, long a, long w0, long ncell, long n, long rd,
                                           int* sR, int* sC, float* sV, float* __restrict__ W, int ldw,
@@ -529,7 +532,7 @@ __device__ __forceinline__ void xcd_round(const int* __restrict__ rows, const in
                       (unsigned)ldh, lr, lam);
 }
 
-template <int R, int CH, bool ATOM>
+template <int R, int CH, int ATOM>
 __global__ __launch_bounds__(256) void mf_sgd_xcd_placed_kernel(const int* __restrict__ rows,
                                                                 const int* __restrict__ cols,
                                                                 const float* __restrict__ vals,
@@ -777,7 +780,7 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
-constexpr int kAtomBit = 4;  // variant bit: ATOM write-back (sgd_stream_lds)
+constexpr int kAtomBits = 12;  // variant bits 2..3: ATOM write-back mode (sgd_stream_lds: 4 = W, 8 = H)
 
 // variant 0: blockIdx-placed sub-steps (+ placement check when chk != NULL; `gen` is the
 // first launch's generation, one per sub-step); 2: mf_sgd_xcd_placed_kernel (pws)
@@ -786,22 +789,26 @@ int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const lo
                    int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, int variant,
                    unsigned long long* chk, unsigned long long gen, int* pws, hipStream_t s) {
   const dim3 grid((unsigned)(blocks_per_xcd * XCDS));
-  const bool atom = (variant & kAtomBit) != 0;
-  const bool placed = (variant & ~kAtomBit) == 2;
+  const int atom = (variant >> 2) & 3;
+  const bool placed = (variant & 3) == 2;
   for (int step = 0; step < steps; ++step) {
     const unsigned long long g = gen + (unsigned long long)step;
-    if (placed && atom)
-      mf_sgd_xcd_placed_kernel<R, CH, true><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H,
-                                                                       ldh, lr, lam, pws);
-    else if (placed)
-      mf_sgd_xcd_placed_kernel<R, CH, false><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H,
-                                                                        ldh, lr, lam, pws);
-    else if (atom)
-      mf_sgd_xcd_kernel<R, CH, true><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H, ldh, lr,
-                                                                lam, chk, g);
-    else
-      mf_sgd_xcd_kernel<R, CH, false><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H, ldh, lr,
-                                                                 lam, chk, g);
+#define XCD_LAUNCH(A)                                                                                        \
+  do {                                                                                                       \
+    if (placed)                                                                                              \
+      mf_sgd_xcd_placed_kernel<R, CH, A><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H, \
+                                                                    ldh, lr, lam, pws);                        \
+    else                                                                                                     \
+      mf_sgd_xcd_kernel<R, CH, A><<<grid, dim3(256), 0, s>>>(rows, cols, vals, off, win, step, W, ldw, H, ldh,   \
+                                                             lr, lam, chk, g);                                \
+  } while (0)
+    switch (atom) {
+      case 1: XCD_LAUNCH(1); break;
+      case 2: XCD_LAUNCH(2); break;
+      case 3: XCD_LAUNCH(3); break;
+      default: XCD_LAUNCH(0); break;
+    }
+#undef XCD_LAUNCH
     const int st = harp_launch_status();
     if (st != HARP_OK) return st;
   }
@@ -1062,8 +1069,8 @@ HARP_EXPORT int harp_mf_xcds() { return XCDS; }
 // `variant`: 0 = blockIdx-placed sub-steps, checked when `chk` (harp_mf_chk_words() zeroed
 // uint64 per stream) is given: launch generations gen .. gen + steps - 1 (> 0, never reused
 // on that chk); 2 = the placement-independent kernel (`pws`: harp_mf_placed_ws_ints()
-// zeroed int32, left zeroed; ranks <= 256); + 4 (kAtomBit, ranks <= 256): the ATOM
-// write-back (H / W changes added with L2 atomics, no lost updates). Non-temporal H stores (23 % slower) and forced
+// zeroed int32, left zeroed; ranks <= 256); + 4 / + 8 (kAtomBits, ranks <= 256): the ATOM
+// write-back of W / of H (changes added with L2 atomics, no lost updates). Non-temporal H stores (23 % slower) and forced
 // 6 / 7 / 8 waves per SIMD were measured in round 1 and are no longer built.
 // `win`: optional DEVICE array [2 x 64] of per-cell window starts and lengths (NULL = all).
 HARP_EXPORT int harp_mf_chk_words() { return kChkWords; }
@@ -1073,10 +1080,10 @@ HARP_EXPORT int harp_mf_sgd_xcd(const int* rows, const int* cols, const float* v
                                 int r, int steps, int chunk, int blocks_per_xcd, int variant, float* W, int ldw,
                                 float* H, int ldh, float lr, float lam, unsigned long long* chk,
                                 unsigned long long gen, int* pws, hipStream_t s) {
-  const int base_variant = variant & ~kAtomBit;
+  const int base_variant = variant & ~kAtomBits;
   if (blocks_per_xcd <= 0 || steps <= 0 || steps > XCDS || ldw < r || ldh < r || (base_variant != 0 && base_variant != 2))
     return HARP_EBADARG;
-  if ((chk && gen == 0) || (base_variant == 2 && (!pws || wide_ok(r))) || ((variant & kAtomBit) && wide_ok(r)))
+  if ((chk && gen == 0) || (base_variant == 2 && (!pws || wide_ok(r))) || ((variant & kAtomBits) && wide_ok(r)))
     return HARP_EBADARG;
   if (wide_ok(r)) {  // wide ranks: one wave per stream
     if (chunk != 32 && chunk != 64 && chunk != 128) return HARP_EBADARG;

@@ -45,7 +45,7 @@ class SGDConfig:
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
     kernel_variant: int = 0    # blocked kernel: 0 = a launch per sub-step, 1 = persistent flow kernel (ops.mf)
-    atomic: bool = False       # GPU blocked kernel: add H / W changes with L2 atomics (no lost concurrent updates)
+    atomic: int = 0            # GPU blocked kernel: add the W (1) / H (2) changes with L2 atomics (no lost updates)
     train_fraction: float = 1.0  # per rotation step each cell trains this fraction (window advances per epoch)
     random_order: bool = False  # random rotation orders (RotationUtil) vs ring
     test_every: int = 5        # rmseIteInterval

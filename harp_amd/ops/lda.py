@@ -41,7 +41,7 @@ SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "3"))
 
 
 # Sampler choice: "dense" = register-row kernel (K <= 1024), "sparse" = doc-token-list
-# kernel (any K <= 16384, see csrc/lda.hip lda_cgs_sparse_kernel), "auto" = sparse for
+# kernel (any K <= 32768, see csrc/lda.hip lda_cgs_sparse_kernel), "auto" = sparse for
 # K > 1024 or corpora of >= SPARSE_MIN_TOKENS tokens, dense otherwise. Measured at
 # 1M docs x 1M words x 1000 topics (1e8 tokens, profiles/r1_lda/sparse): sparse 1.56e9
 # tokens/s and log-likelihood -1.676e9 after 4 iterations vs dense 1.48e9 and -1.688e9;
@@ -51,7 +51,8 @@ SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "3"))
 SAMPLER = os.environ.get("HARP_LDA_SAMPLER", "auto")
 SPARSE_WAVES = int(os.environ.get("HARP_LDA_SPARSE_WAVES", "0"))  # 0: by K (csrc launcher)
 SPARSE_MIN_TOKENS = 1 << 24
-MAX_TOPICS = 16384
+MAX_TOPICS = 32768      # GPU sparse sampler: the word's qw row in LDS (csrc/lda.hip kSparseMaxK)
+MAX_TOPICS_GPU_HOST = 65535  # GPU workers above MAX_TOPICS: the exact host sampler (uint16 doc-order topics)
 
 
 def use_sparse(K: int, n_tokens: int = 0) -> bool:
@@ -69,9 +70,7 @@ def padded_topics(K: int) -> int:
         return 512
     if K <= 1024:
         return 1024
-    if K <= MAX_TOPICS:
-        return (K + 127) // 128 * 128
-    raise NotImplementedError(f"LDA sampler supports K <= {MAX_TOPICS}")
+    return (K + 127) // 128 * 128  # any K (GPU workers: see cgs_sample for K > MAX_TOPICS)
 
 
 @dataclass
@@ -219,6 +218,8 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
         raise ValueError(f"K={K} needs the sparse sampler: pass doc_index (DocIndex.build)")
     if doc_index is not None and tpos is None:
         tpos = doc_index.tpos
+    if _lib.use_native(tz) and K > MAX_TOPICS:
+        return _host_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed, doc_index, tpos)
     if _lib.use_native(tz):
         inv = torch.zeros(Kp, dtype=torch.float32, device=dev)
         inv[:K] = 1.0 / (nk[:K].float() + vbeta)
@@ -254,6 +255,15 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
                                          _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
         return delta
+    delta = _cpu_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed)
+    if doc_index is not None:
+        doc_index.sync(tz, tpos)
+    return delta
+
+
+def _cpu_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed) -> torch.Tensor:
+    """The native sequential sampler (csrc/host/lda_cpu.cpp) on host tensors: updates tz,
+    ndk, nwk in place and returns the topic-count delta."""
     rt = _lib.runtime()
     if rt is None:
         raise _lib.NativeUnavailable("libharp_runtime.so not built")
@@ -265,9 +275,46 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
     work = nk.clone()
     fn(tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), tz.numel(), ndk.data_ptr(), ndk.stride(0), nwk.data_ptr(),
        nwk.stride(0), work.data_ptr(), K, float(alpha), float(beta), float(vbeta), seed & 0xFFFFFFFFFFFFFFFF)
+    return work - nk
+
+
+def _host_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed, doc_index, tpos):
+    """GPU worker, K > :data:`MAX_TOPICS` (the sparse kernel's LDS word row does not fit):
+    the exact sequential collapsed-Gibbs sweep of the native host sampler
+    (``csrc/host``, the reference's per-token order, LDAMPTask.java:85-330) on host copies,
+    results copied back. Correct at any K, not fast -- a documented capacity path, not a
+    throughput one. The doc-topic counts are rebuilt on the host from the doc-order topic
+    lists when the worker keeps no dense table (the sparse sampler's setting)."""
+    if K > MAX_TOPICS_GPU_HOST:
+        raise ValueError(f"GPU LDA workers support K <= {MAX_TOPICS_GPU_HOST} (uint16 doc-order topic lists); "
+                         f"run K = {K} on CPU workers")
+    dev = tz.device
+    h_doc, h_word, h_tz = tdoc.cpu().int().contiguous(), tword.cpu().int().contiguous(), tz.cpu().int().contiguous()
+    Kp = nwk.shape[1]
+    h_nwk = nwk.cpu().contiguous()
+    h_nk = nk.cpu().int().contiguous()
+    if ndk is not None:
+        h_ndk = ndk.cpu().int()
+        if ndk.dtype == torch.int16:
+            h_ndk = h_ndk & 0xFFFF
+        h_ndk = h_ndk.contiguous()
+    else:
+        n_docs = int(doc_index.doc_off.numel() - 1) if doc_index is not None else int(h_doc.max()) + 1
+        # counts of EVERY token of each doc (not only this sweep's): from the doc-order lists
+        off = doc_index.doc_off.cpu()
+        lens = off[1:] - off[:-1]
+        all_doc = torch.repeat_interleave(torch.arange(n_docs), lens)
+        all_z = doc_index.zdoc.cpu().long() & 0xFFFF
+        h_ndk = torch.zeros((n_docs, Kp), dtype=torch.int32)
+        h_ndk.index_put_((all_doc, all_z), torch.ones(all_z.numel(), dtype=torch.int32), accumulate=True)
+    delta = _cpu_sweep(h_doc, h_word, h_tz, h_ndk, h_nwk, h_nk, K, alpha, beta, vbeta, seed)
+    tz.copy_(h_tz.to(dev))
+    nwk.copy_(h_nwk.to(dev))
+    if ndk is not None:
+        ndk.copy_(h_ndk.to(ndk.dtype).to(dev))
     if doc_index is not None:
         doc_index.sync(tz, tpos)
-    return work - nk
+    return delta.to(dev)
 
 
 def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: float, vbeta: float, seed: int,

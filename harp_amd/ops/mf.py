@@ -140,7 +140,8 @@ def check_flow_errors(device: torch.device) -> None:
 # (HW_REG_XCC_ID), so one XCD per cell holds whatever the dispatcher does; the fallback
 # the models switch to when the placement check of the default kernel fires
 PLACED_VARIANT = 2
-ATOMIC_BIT = 4  # harp_mf_sgd_xcd variant bit: atomic (no-lost-update) write-back
+# harp_mf_sgd_xcd variant bits 2..3: atomic (no-lost-update) write-back of W (1) / H (2)
+ATOMIC_W, ATOMIC_H = 1, 2
 CHECK_PLACEMENT = True  # default kernel: tag residue <-> XCC per launch, raise an error word on a mismatch
 _CHK: dict = {}
 
@@ -269,7 +270,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
                        W: torch.Tensor, H: torch.Tensor, lr: float, lam: float, chunk: int = 64,
                        blocks_per_xcd: int = 256, host_off: list | None = None, variant: int = 0,
                        window: Optional[Tuple[List[int], List[int]]] = None, threads: int = 1,
-                       time_budget: Optional[float] = None, atomic: bool = False) -> int:
+                       time_budget: Optional[float] = None, atomic: int = 0) -> int:
     """One SGD pass over ratings laid out in nb x nb cells (cell-major, user-sorted inside a
     cell; ``cell_off`` = nb*nb+1 int64 offsets on W's device). Sub-step s trains the nb
     row- and column-disjoint cells (x, (x+s) mod nb): on the GPU one XCD per cell
@@ -280,9 +281,9 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
     1 (:data:`FLOW_VARIANT`, ranks <= 256) = the whole pass in one persistent launch
     ordered by per-XCD completion flags; 2 (:data:`PLACED_VARIANT`, ranks <= 256) = one
     launch per sub-step whose blocks pick their cell by the XCD they run on. ``atomic``
-    (variants 0 / 2, ranks <= 256): H and W changes are ADDED with L2 atomics instead of
-    stored, so updates of concurrent streams to one row are never lost (csrc/mf_sgd.hip
-    sgd_stream_lds ATOM).
+    (variants 0 / 2, ranks <= 256; bit set of :data:`ATOMIC_W` / :data:`ATOMIC_H`): the
+    W / H changes are ADDED with L2 atomics instead of stored, so updates of concurrent
+    streams to one row are never lost (csrc/mf_sgd.hip sgd_stream_lds ATOM).
     ``window=(starts, lengths)`` (64 each): cell c trains only ``lengths[c]`` ratings from
     ``starts[c]``, wrapping around the cell (fixed-fraction mode, :func:`cell_windows`).
     CPU only: ``threads > 1`` or a ``time_budget`` (s) run the cells through the 2-D
@@ -320,7 +321,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
             ck = _chk(W.device)
             words = ck.words if (CHECK_PLACEMENT and not placed) else None
             gen = ck.next_gen(nb) if words is not None else 0
-            kv = (PLACED_VARIANT if placed else 0) | (ATOMIC_BIT if atomic and r <= 256 else 0)
+            kv = (PLACED_VARIANT if placed else 0) | ((int(atomic) & 3) << 2 if r <= 256 else 0)
             st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
                                      _lib.ptr(win), r, nb, chunk, blocks_per_xcd, kv,
                                      W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam),

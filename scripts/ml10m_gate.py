@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--threads", type=int, default=4, help="CPU BlockScheduler threads per worker")
     ap.add_argument("--epochs", type=int, default=200)
     ap.add_argument("--rank", type=int, default=40)
-    ap.add_argument("--atomic", type=int, default=-1, help="GPU: atomic write-back (1/0; -1 = model default)")
+    ap.add_argument("--atomic", type=int, default=-1, help="GPU: atomic write-back 0 none / 1 W / 2 H / 3 both (-1 = model default)")
     ap.add_argument("--blocks-per-xcd", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--pack", action="store_true", help=f"write {PACKED} from the reference text files and exit")
@@ -93,7 +93,7 @@ def main():
     cfg = SGDConfig(rank=args.rank, lam=0.05, lr=0.002, epochs=args.epochs, num_slices=2, test_every=5,
                     init="reference", cpu_threads=args.threads if args.device == "cpu" else 1, chunk=args.chunk)
     if args.atomic >= 0:
-        cfg.atomic = bool(args.atomic)
+        cfg.atomic = args.atomic
     if args.blocks_per_xcd:
         cfg.blocks_per_xcd = args.blocks_per_xcd
     res = launch(job, args.workers, args=(cfg, nu, ni, (u, i, v.float()), (tu, ti, tv.float()), args.device),

@@ -130,8 +130,31 @@ def test_padded_topics_large_k():
     assert L.padded_topics(1025) == 1152 and L.padded_topics(10000) == 10112
     if L.SAMPLER == "auto":
         assert L.use_sparse(10000) and not L.use_sparse(1000) and L.use_sparse(1000, 10 ** 8)
-    with pytest.raises(NotImplementedError):
-        L.padded_topics(20000)
+    # no K limit: past the GPU kernel's LDS row the exact host sampler runs
+    assert L.padded_topics(20000) == 20096 and L.padded_topics(40000) == 40064
+
+
+def test_cpu_sampler_k_above_gpu_limits(corpus):
+    """A CPU worker at K = 70,000 (above every GPU path): the exact sequential sampler keeps
+    the counts consistent with the assignments."""
+    import torch
+
+    n_docs, V = 50, 80
+    g = torch.Generator().manual_seed(0)
+    tdoc = torch.randint(0, n_docs, (2000,), generator=g).int()
+    tword = torch.sort(torch.randint(0, V, (2000,), generator=g).int()).values
+    K = 70000
+    tz = torch.randint(0, K, (2000,), generator=g).int()
+    Kp = L.padded_topics(K)
+    ndk = torch.zeros((n_docs, Kp), dtype=torch.int32)
+    nwk = torch.zeros((V, Kp), dtype=torch.int32)
+    nk = torch.zeros(Kp, dtype=torch.int32)
+    L.count(tdoc, tword, tz, ndk, nwk, nk)
+    d = L._cpu_sweep(tdoc, tword, tz, ndk, nwk, nk, K, 0.01, 0.01, V * 0.01, 5)
+    r_d, r_w, r_k = torch.zeros_like(ndk), torch.zeros_like(nwk), torch.zeros_like(nk)
+    L.count(tdoc, tword, tz, r_d, r_w, r_k)
+    assert torch.equal(ndk, r_d) and torch.equal(nwk, r_w) and torch.equal(nk + d, r_k)
+    assert int(tz.max()) < K
 
 
 def test_lda_large_k_cpu_rotation(corpus):

@@ -156,9 +156,10 @@ def test_placement_under_cu_hog(cuda, hog_us):
     assert not outs[MF.PLACED_VARIANT]["violation"]  # the placed kernel is never checked / never wrong
 
 
+@pytest.mark.parametrize("atomic", [MF.ATOMIC_W, MF.ATOMIC_W | MF.ATOMIC_H])
 @pytest.mark.parametrize("variant", [0, MF.PLACED_VARIANT])
 @pytest.mark.parametrize("r", [16, 40, 128])
-def test_atomic_writeback_one_stream_per_cell_matches_cpu(cuda, variant, r):
+def test_atomic_writeback_one_stream_per_cell_matches_cpu(cuda, variant, r, atomic):
     """ATOM write-back (H / W changes added with L2 atomics): with one stream per cell there
     is no concurrency, so the result is the CPU schedule's up to the rounding of w0 + (w - w0)."""
     R, C, V, off, W0, H0 = _cells(64, 48, 4000, r, 13)
@@ -166,7 +167,7 @@ def test_atomic_writeback_one_stream_per_cell_matches_cpu(cuda, variant, r):
     MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.01, 0.05)
     Wg, Hg = W0.to(cuda), H0.to(cuda)
     MF.sgd_update_blocked(R.to(cuda), C.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=128,
-                          blocks_per_xcd=4, variant=variant, atomic=True)
+                          blocks_per_xcd=4, variant=variant, atomic=atomic)
     torch.cuda.synchronize()
     assert torch.allclose(Wg.cpu(), Wc, atol=2e-5) and torch.allclose(Hg.cpu(), Hc, atol=2e-5)
 
@@ -183,8 +184,8 @@ def test_atomic_writeback_keeps_concurrent_updates(cuda):
     Wb, Hb = W0.to(cuda), H0.to(cuda)
     for _ in range(3):
         MF.sgd_update_blocked(R, C, V, off, Wc, Hc, 0.002, 0.05)
-        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wa, Ha, 0.002, 0.05, chunk=8, atomic=True)
-        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wb, Hb, 0.002, 0.05, chunk=8, atomic=False)
+        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wa, Ha, 0.002, 0.05, chunk=8, atomic=3)
+        MF.sgd_update_blocked(Rg, Cg, Vg, og, Wb, Hb, 0.002, 0.05, chunk=8, atomic=0)
     torch.cuda.synchronize()
     e0 = MF.sse(R, C, V, W0, H0).item()
     ec = MF.sse(R, C, V, Wc, Hc).item()
