@@ -409,6 +409,8 @@ def bench_sgd(args, comm, torch):
         "rotation_strides": [s.stride for s in m.schedules],
         "xcd_placement": placement,
         "atomic_writeback": cfg.atomic,
+        "blocks_per_xcd": m.bpx,
+        "cell_sum_p2": round(getattr(m, "cell_sum_p2", 0.0), 6),  # the concurrency cap's input (SGDConfig)
         "train_rmse": round(train_rmse, 6),
         "users": args.sgd_users, "items": args.sgd_items, "ratings": args.sgd_ratings, "rank": args.sgd_rank,
         "slices_per_rank": cfg.num_slices,

@@ -430,8 +430,13 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     const long* __restrict__ tpos, const long* __restrict__ doc_off, unsigned short* __restrict__ zdoc,
     DT* __restrict__ ndk, int ldd,
     int* __restrict__ nwk, int ldw, const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, int Kp,
-    float alpha, float beta, unsigned long long seed, int ldelta, int wdelta) {
+    float alpha, float beta, unsigned long long seed, int ldelta, int wdelta, PsRows ps) {
   extern __shared__ float smem[];
+  // fused parameter-server rows (ps.pbuf != null, the dense kernel's PsRows contract): a
+  // chunk's qw row is built from its word's PULL slot and the chunk's word-row moves go to
+  // the word's PUSH slot (no dense local table, no decode / delta re-encode around the sweep);
+  // chunks of one word see the sweep-start counts plus their own moves
+  const bool fused = ps.pbuf != nullptr;
   float* s_qw = smem;
   // ldelta: this workgroup's topic-sum deltas accumulate in LDS (after s_qw) and are
   // flushed once when it exits, instead of two global atomics per moved token on only K
@@ -463,20 +468,66 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     if (s_c >= nchunks) break;
     const long c = order ? order[s_c] : s_c;
     const long a = chunk_start[c], b = chunk_start[c + 1];
-    int* wrow = nwk + (long)tword[a] * ldw;
-    auto flush_wd = [&]() {  // this wave's word-row moves -> global row (all 64 lanes)
+    const int wl = tword[a];
+    int* wrow = fused ? nullptr : nwk + (long)wl * ldw;
+    unsigned char* qslot = fused ? ps.qbuf + ps.qoff[wl] : nullptr;
+    const int qcap = fused ? ps.qcap[wl] : 0;
+    // one word-row move of v (+-1 or a flushed sum) for topic t: the global row, or the
+    // push slot (dense: add at t; sparse: one reserved (count, topic) entry -- entries of
+    // several flushes may repeat a topic, the owner's decode_add sums them)
+    auto put_move = [&](int t, int v) {
+      if (!fused) {
+        atomicAdd(wrow + t, v);
+      } else if (qcap < 0) {
+        atomicAdd((int*)qslot + t, v);
+      } else {
+        const int pos = atomicAdd((int*)qslot, 1);
+        if (pos < qcap) {
+          ((int*)(qslot + 4))[pos] = v;
+          ((unsigned short*)(qslot + 4 + 4 * (long)qcap))[pos] = (unsigned short)t;
+        } else {
+          ps.overflow[0] = 1;
+        }
+      }
+    };
+    auto flush_wd = [&]() {  // this wave's word-row moves -> global row / push slot (all 64 lanes)
       for (int t = lane; t < K; t += 64) {
         const int v = s_wd[t];
         if (v) {
-          atomicAdd(wrow + t, v);
+          put_move(t, v);
           s_wd[t] = 0;
         }
       }
     };
     int ntok = 0;
-    for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
-      s_qw[t] = t < K ? ((float)__builtin_nontemporal_load(wrow + t) + beta) * inv_nk[t] : 0.f;
-      if (wdelta == 2) s_wd[t] = 0;
+    if (!fused) {
+      for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
+        s_qw[t] = t < K ? ((float)__builtin_nontemporal_load(wrow + t) + beta) * inv_nk[t] : 0.f;
+        if (wdelta == 2) s_wd[t] = 0;
+      }
+    } else {
+      const unsigned char* pslot = ps.pbuf + ps.poff[wl];
+      const int pcap = ps.pcap[wl];
+      if (pcap < 0) {  // dense slot: the whole padded row
+        for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
+          s_qw[t] = t < K ? ((float)((const int*)pslot)[t] + beta) * inv_nk[t] : 0.f;
+          if (wdelta == 2) s_wd[t] = 0;
+        }
+      } else {  // sparse slot: the smoothing value everywhere, then the row's nonzeros
+        for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
+          s_qw[t] = t < K ? beta * inv_nk[t] : 0.f;
+          if (wdelta == 2) s_wd[t] = 0;
+        }
+        __syncthreads();
+        int nnz = *(const int*)pslot;
+        nnz = nnz < 0 ? 0 : (nnz > pcap ? pcap : nnz);
+        const int* cnt = (const int*)(pslot + 4);
+        const unsigned short* top = (const unsigned short*)(pslot + 4 + 4 * (long)pcap);
+        for (int e = threadIdx.x; e < nnz; e += 64 * WAVES) {  // a row's topics are distinct
+          const int t = top[e];
+          if (t < K) s_qw[t] = ((float)cnt[e] + beta) * inv_nk[t];
+        }
+      }
     }
     __syncthreads();
     for (int k = wv; k < nb; k += WAVES) {
@@ -660,8 +711,8 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
             atomicSub(&s_wd[z], 1);
             atomicAdd(&s_wd[nz], 1);
           } else {
-            atomicSub(wrow + z, 1);
-            atomicAdd(wrow + nz, 1);
+            put_move(z, -1);
+            put_move(nz, 1);
           }
           if (ldelta) {
             atomicSub(&s_nkd[z], 1);
@@ -675,7 +726,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
       // one wave are separate threads to the compiler, so order them explicitly
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (wdelta == 1 && ++ntok % WFLUSH == 0) {
+      if (wdelta == 1 && !fused && ++ntok % WFLUSH == 0) {
         flush_wd();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
       }
@@ -699,7 +750,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     } else if (wdelta == 2) {
       __syncthreads();  // every wave's moves of this chunk are in the row
       for (int t = threadIdx.x; t < K; t += 64 * WAVES)
-        if (s_wd[t]) atomicAdd(wrow + t, s_wd[t]);
+        if (s_wd[t]) put_move(t, s_wd[t]);
     }
   }
   if (ldelta) {  // every wave left the chunk loop together (the break follows a barrier)
@@ -818,7 +869,8 @@ int launch_sparse(const int* tdoc, const long* tspan, const int* tword, int* tz,
                   const int* order,
                   int* work, const long* tpos,
                   const long* doc_off, unsigned short* zdoc, DT* ndk, int ldd, int* nwk, int ldw, const float* inv_nk,
-                  int* nk_delta, int K, float alpha, float beta, unsigned long long seed, int det, hipStream_t s) {
+                  int* nk_delta, int K, float alpha, float beta, unsigned long long seed, int det, hipStream_t s,
+                  PsRows ps = PsRows{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}) {
   const int Kp = (K + 63) / 64 * 64;
   const int ldelta = Kp <= 4096;  // LDS topic-sum deltas while they cost at most 16 KB
   const int wdelta = sparse_wdelta(Kp);
@@ -837,7 +889,7 @@ int launch_sparse(const int* tdoc, const long* tspan, const int* tword, int* tz,
   if (det) blocks = 1;
   lda_cgs_sparse_kernel<WAVES, DT, SPAN><<<dim3((unsigned)blocks), dim3(64 * WAVES), lds, s>>>(
       tdoc, tspan, tword, tz, chunk_start, nchunks, order, work, tpos, doc_off, zdoc, ndk, ldd, nwk, ldw, inv_nk, nk_delta, K, Kp, alpha,
-      beta, seed, ldelta, wdelta);
+      beta, seed, ldelta, wdelta, ps);
   return harp_launch_status();
 }
 }  // namespace
@@ -920,6 +972,45 @@ HARP_EXPORT int harp_lda_cgs_sparse_span(const long* tspan, const int* tword, in
   }
 #define SS_ARGS nullptr, tspan, tword, tz, chunk_start, nchunks, order, work, tpos, nullptr, zdoc, (int*)nullptr, 0
 #define SS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, s
+  return waves == 1    ? launch_sparse<1, int, true>(SS_ARGS, SS_TAIL)
+         : waves == 2  ? launch_sparse<2, int, true>(SS_ARGS, SS_TAIL)
+         : waves == 4  ? launch_sparse<4, int, true>(SS_ARGS, SS_TAIL)
+         : waves == 16 ? launch_sparse<16, int, true>(SS_ARGS, SS_TAIL)
+                       : launch_sparse<8, int, true>(SS_ARGS, SS_TAIL);
+#undef SS_ARGS
+#undef SS_TAIL
+}
+
+// harp_lda_cgs_sparse_span with fused parameter-server rows: word rows come from the pull
+// payload slots (pbuf / poff / pcap, one per local row) and the sweep's word-row moves are
+// written into the zeroed push payload (qbuf / qoff / qcap); no dense word table. Slot
+// formats: parallel/sparse_ps.py, csrc/rowcodec.hip (K_pad ints per dense slot).
+HARP_EXPORT int harp_lda_cgs_sparse_span_ps(const long* tspan, const int* tword, int* tz, const long* chunk_start,
+                                            long nchunks, const int* order, int* work, const long* tpos,
+                                            unsigned short* zdoc, const float* inv_nk, int* nk_delta, int K,
+                                            float alpha, float beta, unsigned long long seed, int waves,
+                                            const unsigned char* pbuf, const long* poff, const int* pcap,
+                                            unsigned char* qbuf, const long* qoff, const int* qcap, int* overflow,
+                                            hipStream_t s) {
+  if (nchunks <= 0) return HARP_OK;
+  if (K <= 0 || K > kSparseMaxK || !tspan || !tpos || !zdoc || !work) return HARP_EBADARG;
+  if (!pbuf || !poff || !pcap || !qbuf || !qoff || !qcap || !overflow) return HARP_EBADARG;
+  const PsRows ps{pbuf, poff, pcap, qbuf, qoff, qcap, overflow};
+  const int det = waves < 0 ? 1 : 0;
+  if (det) waves = 1;
+  if (waves == 0) {
+    const int Kp = (K + 63) / 64 * 64;
+    waves = 16;
+    for (int w = 4; w <= 8; w *= 2) {
+      const long per_cu = 163840 / ((long)sparse_lds_bytes(Kp, w) + 1100);
+      if (per_cu * w >= 24) {
+        waves = w;
+        break;
+      }
+    }
+  }
+#define SS_ARGS nullptr, tspan, tword, tz, chunk_start, nchunks, order, work, tpos, nullptr, zdoc, (int*)nullptr, 0
+#define SS_TAIL nullptr, 0, inv_nk, nk_delta, K, alpha, beta, seed, det, s, ps
   return waves == 1    ? launch_sparse<1, int, true>(SS_ARGS, SS_TAIL)
          : waves == 2  ? launch_sparse<2, int, true>(SS_ARGS, SS_TAIL)
          : waves == 4  ? launch_sparse<4, int, true>(SS_ARGS, SS_TAIL)

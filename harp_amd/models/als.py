@@ -186,7 +186,13 @@ def train_als(comm: Communicator, u: torch.Tensor, i: torch.Tensor, v: torch.Ten
             tu, ti, tv = test
             mine = (tu % P) == me
             pred = (Xf[tu[mine].to(dev)] * Yf[ti[mine].to(dev)]).sum(1)
-            rec["test_rmse"] = rmse(comm, ((pred - tv[mine].to(dev, dt)) ** 2).sum(), int(mine.sum()))
+            tvm = tv[mine].to(dev, dt)
+            rec["test_rmse"] = rmse(comm, ((pred - tvm) ** 2).sum(), int(mine.sum()))
+            if cfg.implicit:
+                # the reference's implicit-ALS test error (daal_als/ComputeRMSE.java:97-104):
+                # preference 1 for every test pair, weighted by the confidence 1 + alpha r
+                rec["test_conf_rmse"] = rmse(comm, (((1.0 - pred) ** 2) * (1.0 + cfg.alpha * tvm)).sum(),
+                                             int(mine.sum()))
         hist.append(rec)
         inject_fault(me, it)
         ck.maybe_save(it, {"X": (X, my_users), "Y": (Y, my_items)}, hist)

@@ -501,8 +501,10 @@ class LDAPushPullMapper(LDACollectiveMapper):
             self.ps.push(self.pull_buf, self._glob_rows(), delta=False)  # initial counts into an empty model
             # fused rows: the dense sampler reads the pull payload and writes the push payload
             # itself, so the dense local table is only the initial-count source
-            self.fused = (cfg.fused_rows and not self.sparse and K <= 1024 and dev.type == "cuda"
-                          and L._lib.use_native(self.tz))
+            # (the sparse doc-span sampler too: the doc-order lists replace the doc table)
+            self.fused = (cfg.fused_rows and dev.type == "cuda" and L._lib.use_native(self.tz)
+                          and ((not self.sparse and K <= 1024)
+                               or (self.sparse and self.ndk is None and L.SPAN and K <= L.MAX_TOPICS)))
             if self.fused:
                 self.slots = self.ps.row_slots()
                 self.pull_buf = None
@@ -600,7 +602,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
             n = self.tz.numel()
             d = (L.cgs_sample_ps(self.tdoc, self.tword, self.tz, self.chunk_idx, self.ndk, self.nk, cfg.num_topics,
                                  cfg.alpha, cfg.beta, self.vbeta, seed, pbuf, qbuf, self.slots, self.ps.overflow,
-                                 deterministic=cfg.deterministic)
+                                 deterministic=cfg.deterministic, doc_index=self.doc_index)
                  if n else torch.zeros(self.Kp, dtype=torch.int32, device=self.device))
             self._timed_ps("push", lambda: self.ps.push_payload(self._glob_rows()), push_b)
             if self.get_num_workers() > 1:

@@ -43,7 +43,13 @@ class SGDConfig:
                                # contend for their L2 lines (ops.mf.balanced_blocks; 6.35 -> 6.02 ms per
                                # 100M-rating epoch at skew 2, profiles/r3_sgd_hot_balance); 0 = equal counts
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
-    blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel
+    blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel (upper bound, see conflicts_per_rating)
+    conflicts_per_rating: float = 5.0  # GPU: cap the XCD's concurrent streams S (16 x blocks_per_xcd) at
+                               # this / sum_i p_i^2 of a cell (expected same-item concurrent updates per rating;
+                               # two streams updating one H row at once lose one update). The reference's ML-10M
+                               # gate (sum p^2 = 0.021 per cell): test RMSE 0.8369 / 0.8388 / 0.8408 / 0.8450 /
+                               # 0.8552 at S = 128 / 256 / 512 / 1024 / 2048 (profiles/r5_mf_gate); Netflix-shape
+                               # synthetic at P = 1 (0.0015): no cap below 128 blocks; 0 = no cap
     kernel_variant: int = 0    # blocked kernel: 0 = a launch per sub-step, 1 = persistent flow kernel (ops.mf)
     atomic: int = 0            # GPU blocked kernel: add the W (1) / H (2) changes with L2 atomics (no lost updates)
     train_fraction: float = 1.0  # per rotation step each cell trains this fraction (window advances per epoch)
@@ -201,6 +207,25 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.local_of_item = (pos % self.ips).to(u.device)
         self.item_perm = perm  # slice s holds items perm[s*ips:(s+1)*ips]
         cells = (self.users.numel(), self.ips) if cfg.xcd_blocks else None
+        # concurrency cap: an XCD's 16 x blocks streams share one cell's items; a stream meets
+        # another on its item with probability ~ sum_i p_i^2 (p_i: item i's share of the cell's
+        # ratings), so the expected concurrent same-item updates per rating are ~ S sum p^2
+        self.bpx = cfg.blocks_per_xcd
+        if cfg.conflicts_per_rating > 0 and dev.type == "cuda":
+            key = self.slice_of_item[i] * self.ips + self.local_of_item[i]
+            cnt = torch.bincount(key, minlength=n_slices * self.ips).view(n_slices, self.ips).double()
+            tot = cnt.sum(1).clamp_min(1.0)
+            # a cell holds 1/8 of a slice's items with ~1/8 of its ratings (equal-work item
+            # blocks): its sum of squared shares is ~8 x the slice's
+            sp2 = float((MF.XCDS * ((cnt / tot[:, None]) ** 2).sum(1)).mean())
+            if P > 1:
+                import torch.distributed as dist
+
+                t = torch.tensor([sp2], dtype=torch.float64, device=dev)
+                self.comm.all_reduce(t, op=dist.ReduceOp.MAX)
+                sp2 = float(t.item())
+            self.cell_sum_p2 = sp2
+            self.bpx = max(2, min(cfg.blocks_per_xcd, int(cfg.conflicts_per_rating / max(sp2, 1e-12) / 16)))
         trace("user / item maps")
         self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells,
                               hot=cfg.hot_balance)
@@ -289,7 +314,7 @@ class SGDCollectiveMapper(CollectiveMapper):
                         r_, c_, v_, off, hoff = self.train.get_cells(gs)
                         win = MF.cell_windows(hoff, cfg.train_fraction, epoch) if cfg.train_fraction < 1.0 else None
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
-                                                   cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
+                                                   self.bpx, host_off=hoff, variant=cfg.kernel_variant,
                                                    window=win, atomic=cfg.atomic)
                     else:
                         if cfg.train_fraction < 1.0:
@@ -327,7 +352,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             L = [((q + 1) * m) // P - (q * m) // P for m in sizes]
             if cfg.xcd_blocks:
                 return MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
-                                             cfg.blocks_per_xcd, host_off=hoff, variant=cfg.kernel_variant,
+                                             self.bpx, host_off=hoff, variant=cfg.kernel_variant,
                                              window=(starts, L), atomic=cfg.atomic)
             a, m = starts[0], L[0]
             return MF.sgd_update(r_[a:a + m], c_[a:a + m], v_[a:a + m], self.W, slab, cfg.lr, cfg.lam,
@@ -360,7 +385,7 @@ class SGDCollectiveMapper(CollectiveMapper):
         if self.cfg.model_dir:
             self.save_models(self.cfg.model_dir)
         self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained,
-                       "start_epoch": start, "placement": self.placement_events}
+                       "start_epoch": start, "placement": self.placement_events, "blocks_per_xcd": self.bpx}
 
     def _check_placement(self, ep: int) -> None:
         """Once per epoch (the epoch is already synchronised): did a default XCD-blocked

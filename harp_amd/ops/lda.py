@@ -19,6 +19,10 @@ _lib.register({
     "harp_lda_cgs_sparse_span": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 5 + [
         _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_ulonglong,
         _lib.c_int, _lib.c_void_p],
+    # tspan, tword, tz, chunks, nchunks, order, work, tpos, zdoc, inv, delta, K, alpha, beta, seed, waves,
+    # pbuf, poff, pcap, qbuf, qoff, qcap, overflow, stream
+    "harp_lda_cgs_sparse_span_ps": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 6 + [
+        _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_ulonglong, _lib.c_int] + [_lib.c_void_p] * 8,
     "harp_lda_cgs_sparse": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 6 + [
         _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
         _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
@@ -318,16 +322,39 @@ def _host_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed, doc_
 
 
 def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: float, vbeta: float, seed: int,
-                  pull_buf, push_buf, slots, overflow, deterministic: bool = False) -> torch.Tensor:
-    """:func:`cgs_sample` (dense sampler, GPU) with the word rows read from the pull
-    payload and the word-row deltas written into the (zeroed) push payload -- no dense
-    local table (``parallel.sparse_ps.SparseRowPS.row_slots`` gives ``slots``). Returns
-    the topic-count delta."""
+                  pull_buf, push_buf, slots, overflow, deterministic: bool = False,
+                  doc_index: Optional[DocIndex] = None, order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """:func:`cgs_sample` on the GPU with the word rows read from the pull payload and the
+    word-row deltas written into the (zeroed) push payload -- no dense local table
+    (``parallel.sparse_ps.SparseRowPS.row_slots`` gives ``slots``). Dense sampler (``ndk``,
+    K <= 1024), or with ``doc_index`` (and no ``ndk``) the sparse doc-span sampler
+    (K <= :data:`MAX_TOPICS`). Returns the topic-count delta."""
     dev = tz.device
+    poff, pcap, qoff, qcap = slots
+    if doc_index is not None:
+        if not _lib.use_native(tz) or K > MAX_TOPICS or ndk is not None:
+            raise ValueError("fused push-pull rows with the sparse sampler need the GPU doc-span kernel")
+        Kp = nk.shape[0]
+        inv = torch.zeros(Kp, dtype=torch.float32, device=dev)
+        inv[:K] = 1.0 / (nk[:K].float() + vbeta)
+        delta = torch.zeros(Kp, dtype=torch.int32, device=dev)
+        tpos = doc_index.tpos
+        assert tpos.numel() == tz.numel()
+        if order is None:
+            order = chunk_order(chunks)
+        work = torch.zeros(1, dtype=torch.int32, device=dev)
+        span = _span_slice(doc_index, tdoc, tpos)
+        st = _lib.kernels().harp_lda_cgs_sparse_span_ps(
+            span.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(), chunks.numel() - 1, order.data_ptr(),
+            work.data_ptr(), tpos.data_ptr(), doc_index.zdoc.data_ptr(), inv.data_ptr(), delta.data_ptr(), K,
+            float(alpha), float(beta), seed & 0xFFFFFFFFFFFFFFFF, -1 if deterministic else SPARSE_WAVES,
+            pull_buf.data_ptr(), poff.data_ptr(), pcap.data_ptr(), push_buf.data_ptr(), qoff.data_ptr(),
+            qcap.data_ptr(), overflow.data_ptr(), _lib.stream_ptr(dev))
+        _lib.check(st, "lda_cgs_sparse_span_ps")
+        return delta
     Kp = ndk.shape[1]
     if not _lib.use_native(tz) or K > 1024:
         raise ValueError("fused push-pull rows need the GPU dense sampler (K <= 1024)")
-    poff, pcap, qoff, qcap = slots
     inv = torch.zeros(Kp, dtype=torch.float32, device=dev)
     inv[:K] = 1.0 / (nk[:K].float() + vbeta)
     delta = torch.zeros(Kp, dtype=torch.int32, device=dev)

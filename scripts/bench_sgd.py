@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--layout", choices=("xcd", "flat"), default="xcd")
     ap.add_argument("--skew", type=float, default=2.0, help="item popularity skew (1 = uniform)")
     ap.add_argument("--blocks-per-xcd", type=int, default=128)
+    ap.add_argument("--conflicts-per-rating", type=float, default=0.0,
+                    help="SGDConfig concurrency cap (0 = use --blocks-per-xcd as is)")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant: 0 (per-sub-step launches), 1 (flow)")
     ap.add_argument("--slices", type=int, default=1,
                     help="H slices per rank (rotation slice steps per epoch; 1 as in bench.py, profiles/r3_sgd_slices)")
@@ -44,7 +46,7 @@ def main():
     u, i, v = synthetic_ratings(a.users, a.items, a.ratings, seed=7, device=dev, skew=a.skew)
     gen_s = time.perf_counter() - t0
     cfg = SGDConfig(rank=a.rank, lam=a.lam, lr=a.lr, epochs=a.warmup + a.epochs, chunk=a.chunk, test_every=0,
-                    xcd_blocks=a.layout == "xcd", blocks_per_xcd=a.blocks_per_xcd,
+                    xcd_blocks=a.layout == "xcd", blocks_per_xcd=a.blocks_per_xcd, conflicts_per_rating=a.conflicts_per_rating,
                     kernel_variant=a.variant, num_slices=a.slices)
     m = SGDCollectiveMapper(comm, cfg, a.users, a.items, (u, i, v), None)
     m.init_model(KeyValReader([]))

@@ -39,7 +39,23 @@ def job(comm, cfg, nu, ni, train, test, device):
     wall = time.perf_counter() - t0
     res = m.result
     return {"rmse": res["rmse"], "trained": res["trained"], "epoch_s": res["epoch_s"], "wall_s": wall,
-            "placement": res["placement"], "storage_rank": int(m.W.shape[1])}
+            "placement": res["placement"], "storage_rank": int(m.W.shape[1]), "blocks_per_xcd": m.bpx}
+
+
+def als_job(comm, cfg, nu, ni, train, test, device):
+    import torch
+
+    from harp_amd.models.als import train_als
+    from harp_amd.parallel.comm import Communicator
+
+    if device == "cuda":
+        comm = Communicator(None, torch.device("cuda", 0))
+    P, me = comm.world_size, comm.rank
+    u, i, v = train
+    mine = torch.arange(u.numel()) % P == me  # any split of the training triples (train_als shuffles)
+    t0 = time.perf_counter()
+    r = train_als(comm, u[mine], i[mine], v[mine], nu, ni, cfg, test=test)
+    return {"history": r["history"], "wall_s": time.perf_counter() - t0}
 
 
 def main():
@@ -52,6 +68,8 @@ def main():
     ap.add_argument("--atomic", type=int, default=-1, help="GPU: atomic write-back 0 none / 1 W / 2 H / 3 both (-1 = model default)")
     ap.add_argument("--blocks-per-xcd", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--als", action="store_true",
+                    help="DAAL implicit ALS instead (harp-daal-als.sh:51-63: Dim 100, lambda 0.05, 5 iterations)")
     ap.add_argument("--pack", action="store_true", help=f"write {PACKED} from the reference text files and exit")
     args = ap.parse_args()
     if args.pack:
@@ -90,6 +108,18 @@ def main():
         src = PACKED
     load_s = time.perf_counter() - t0
     nu, ni = int(max(u.max(), tu.max())) + 1, int(max(i.max(), ti.max())) + 1
+    if args.als:
+        from harp_amd.models.als import ALSConfig
+
+        acfg = ALSConfig(factors=100, lam=0.05, alpha=40.0, iterations=5, implicit=True)
+        res = launch(als_job, args.workers, args=(acfg, nu, ni, (u, i, v.double()), (tu, ti, tv.double()), args.device),
+                     timeout=1100)
+        h = res[0]["history"]
+        print(json.dumps({"app": "daal_als (harp-daal-als.sh:51-63)", "data": src, "device": args.device,
+                          "workers": args.workers, "factors": 100, "lambda": 0.05, "alpha": 40.0, "iterations": 5,
+                          "test_conf_rmse": h[-1].get("test_conf_rmse"), "test_rmse_vs_ratings": h[-1]["test_rmse"],
+                          "history": h, "wall_s": max(r["wall_s"] for r in res)}))
+        return
     cfg = SGDConfig(rank=args.rank, lam=0.05, lr=0.002, epochs=args.epochs, num_slices=2, test_every=5,
                     init="reference", cpu_threads=args.threads if args.device == "cpu" else 1, chunk=args.chunk)
     if args.atomic >= 0:
@@ -102,7 +132,7 @@ def main():
     test_rmse = r0["rmse"][-1][2]
     out = {
         "gate": "mfsgd.sh:64 r=40 lambda=0.05 eps=0.002 200 iters 2 workers, test RMSE in (0.80, 0.84)",
-        "data": src, "device": args.device, "atomic": cfg.atomic, "blocks_per_xcd": cfg.blocks_per_xcd,
+        "data": src, "device": args.device, "atomic": cfg.atomic, "blocks_per_xcd": r0["blocks_per_xcd"],
         "chunk": cfg.chunk, "workers": args.workers, "rank": args.rank, "storage_rank": r0["storage_rank"],
         "train_ratings": int(u.numel()), "test_ratings": int(tu.numel()),
         "test_rmse": test_rmse, "pass": 0.80 < test_rmse < 0.84, "reference_run": 0.8345,

@@ -29,12 +29,13 @@ def _worker(comm, fused, K=64):
             "dense_slots": dense}
 
 
-# K = 50: K % 4 != 0, the padded row's tail topics must come from the dense pull slots too
-@pytest.mark.parametrize("K", [64, 50])
+# K = 50: K % 4 != 0, the padded row's tail topics must come from the dense pull slots too;
+# K = 2000: the sparse doc-span sampler (K > 1024) with fused rows (sparse and dense slots)
+@pytest.mark.parametrize("K", [64, 50, 2000])
 def test_fused_rows_two_ranks_match_unfused(cuda, K):
     a = launch(_worker, 2, args=(True, K), timeout=300)
     b = launch(_worker, 2, args=(False, K), timeout=300)
-    assert any(r["dense_slots"] > 0 for r in a), "no dense pull slot exercised"
+    assert K > 1024 or any(r["dense_slots"] > 0 for r in a), "no dense pull slot exercised"
     for ra, rb in zip(a, b):
         assert ra["fused"] and not rb["fused"]
         assert ra["ok"] and rb["ok"]

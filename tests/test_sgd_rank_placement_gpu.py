@@ -193,3 +193,23 @@ def test_atomic_writeback_keeps_concurrent_updates(cuda):
     eb = MF.sse(Rg, Cg, Vg, Wb, Hb).item()
     print(f"sse initial {e0:.5g} cpu {ec:.5g} atomic {ea:.5g} store {eb:.5g}")
     assert ea < e0 and abs(ea - ec) < 0.05 * (e0 - ec)
+
+
+def test_concurrency_cap_from_item_concentration(cuda):
+    """SGDConfig.conflicts_per_rating caps the XCD's concurrent streams at C / sum p^2 of a
+    cell: few, skewed items (a small dense problem like the reference's ML-10M gate) get
+    few workgroups; a problem with many items keeps the full grid."""
+    from harp_amd.models.sgd_mf import SGDCollectiveMapper
+    from harp_amd.runtime.mapper import KeyValReader
+
+    small = synthetic_ratings(20000, 300, 400000, seed=1)
+    big = synthetic_ratings(20000, 60000, 400000, seed=1, skew=1.0)
+    got = {}
+    for name, (u, i, v), ni in (("small", small, 300), ("big", big, 60000)):
+        m = SGDCollectiveMapper(Communicator(None, cuda), SGDConfig(rank=16, epochs=1, test_every=0), 20000, ni,
+                                (u, i, v), None)
+        m.run(KeyValReader([]))
+        got[name] = (m.bpx, m.cell_sum_p2)
+    print("cap", got)
+    assert got["small"][0] < 32 <= got["big"][0]
+    assert got["small"][1] > got["big"][1]
