@@ -78,8 +78,24 @@ def solve_rows(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_row
         crow = crow.to(torch.int64).contiguous()
         blk = max(blk, 1 << 17)  # no per-rating intermediates: big blocks, fewer solver launches
         blk = min(blk, (2**32 - 1) // OA.THREADS)  # one workgroup per row: grid x threads < 2^32
-    for a in range(0, n_rows, blk):
-        b = min(n_rows, a + blk)
+    # torch path: the per-rating f x f outer products of a block live in memory at once, so
+    # blocks are bounded by RATINGS (a row block of popular items holds millions of them);
+    # at least one row per block
+    per_rating = f * f * dt.itemsize
+    max_ratings = max(1, int(cfg.block_bytes // per_rating))
+    crow_h = crow.cpu() if not native else None
+    bounds = []
+    a = 0
+    while a < n_rows:
+        if native:
+            b = min(n_rows, a + blk)
+        else:
+            lim = int(crow_h[a]) + max_ratings
+            b = int(torch.searchsorted(crow_h, torch.tensor([lim], dtype=crow_h.dtype), right=True)[0]) - 1
+            b = min(n_rows, max(b, a + 1), a + blk)
+        bounds.append((a, b))
+        a = b
+    for a, b in bounds:
         if native:
             # build + Cholesky-solve every row's system in one kernel; rows whose system is
             # not SPD (info) send the block through rocSOLVER with the lstsq fallback

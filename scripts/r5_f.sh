@@ -11,3 +11,8 @@ timeout -k 10 300 python -u scripts/bench_lda.py --docs 1e6 --strategy push_pull
 tail -1 $O/full.log | cut -c 1-600
 timeout -k 10 300 python -u scripts/bench_lda.py --docs 125000 --strategy push_pull --local-server off --iters 5 > $O/share8.log 2>&1 || { echo share failed; tail $O/share8.log; exit 1; }
 tail -1 $O/share8.log | cut -c 1-600
+timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_sgd_rank_placement_gpu.py -k "cap or model_any" -s \
+  > $O/pytest_cap.log 2>&1 || { echo "cap pytest failed"; tail -30 $O/pytest_cap.log; exit 1; }
+grep -E "^cap|passed|failed" $O/pytest_cap.log | tail -3
+timeout -k 10 600 python -u scripts/ml10m_gate.py --device cuda --workers 2 --als > $O/als.json 2> $O/als.err || { echo "als failed"; tail -5 $O/als.err; exit 1; }
+tail -1 $O/als.json | cut -c 1-500

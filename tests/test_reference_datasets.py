@@ -1,9 +1,9 @@
 """Algorithms on the reference's own fixture files (datasets/daal_*; read as text only).
 
-Where the reference ships expected outputs (daal_reg groundTruth, daal_nn groundTruth,
-daal_naive testTruth) we compare to them; elsewhere we compare to sklearn on the same
-file ("parity unpinned" for DAAL's exact numbers: the DAAL native library is not
-available). Skipped when the reference tree is absent (e.g. on the GPU box)."""
+Where the reference ships expected outputs (daal_reg groundTruth, daal_naive testTruth) we
+compare to them (daal_nn's groundTruth: tests/test_reference_fixtures.py); elsewhere we
+compare to sklearn on the same file ("parity unpinned" for DAAL's exact numbers: the DAAL
+native library is not available). Skipped when the reference tree is absent (e.g. on the GPU box)."""
 import os
 
 import pytest
