@@ -490,15 +490,48 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         }
       }
     };
-    auto flush_wd = [&]() {  // this wave's word-row moves -> global row / push slot (all 64 lanes)
-      for (int t = lane; t < K; t += 64) {
-        const int v = s_wd[t];
+    // a delta row (this wave's topics t0, t0 + stride, ...) -> global row / push slot, all 64
+    // lanes; into a sparse push slot with ONE reservation per wave (a scan of the lanes'
+    // nonzero counts), not one atomic on the slot's nnz word per entry
+    auto flush_row = [&](int* row, int t0, int stride) {
+      if (!fused || qcap < 0) {
+        for (int t = t0; t < K; t += stride) {
+          const int v = row[t];
+          if (v) {
+            put_move(t, v);
+            row[t] = 0;
+          }
+        }
+        return;
+      }
+      int mine = 0;
+      for (int t = t0; t < K; t += stride) mine += row[t] != 0 ? 1 : 0;
+      const float incl = wave_incl_scan((float)mine, lane);
+      const int tot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+      if (tot == 0) return;
+      int base = 0;
+      if (lane == 0) base = atomicAdd((int*)qslot, tot);
+      base = __builtin_amdgcn_readfirstlane(base);
+      int pos = base + (int)incl - mine;
+      int* cnt = (int*)(qslot + 4);
+      unsigned short* top = (unsigned short*)(qslot + 4 + 4 * (long)qcap);
+      bool over = false;
+      for (int t = t0; t < K; t += stride) {
+        const int v = row[t];
         if (v) {
-          put_move(t, v);
-          s_wd[t] = 0;
+          if (pos < qcap) {
+            cnt[pos] = v;
+            top[pos] = (unsigned short)t;
+          } else {
+            over = true;
+          }
+          ++pos;
+          row[t] = 0;
         }
       }
+      if (__ballot(over) && lane == 0) ps.overflow[0] = 1;
     };
+    auto flush_wd = [&]() { flush_row(s_wd, lane, 64); };  // this wave's word-row moves
     int ntok = 0;
     if (!fused) {
       for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
@@ -749,8 +782,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     } else if (wdelta == 2) {
       __syncthreads();  // every wave's moves of this chunk are in the row
-      for (int t = threadIdx.x; t < K; t += 64 * WAVES)
-        if (s_wd[t]) put_move(t, s_wd[t]);
+      flush_row(s_wd, threadIdx.x, 64 * WAVES);  // zeroes it too (re-zeroed per chunk anyway)
     }
   }
   if (ldelta) {  // every wave left the chunk loop together (the break follows a barrier)

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--max-chunk", type=int, default=0, help="tokens per word chunk (0: LDAConfig default)")
     ap.add_argument("--strategy", default="rotation", choices=["rotation", "push_pull"])
     ap.add_argument("--sparse-comm", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--fused-rows", default="on", choices=["on", "off"],
+                    help="push_pull with sparse rows: the sampler reads pull slots / writes push slots")
     ap.add_argument("--local-server", default="on", choices=["on", "off"],
                     help="push_pull at P=1: off runs the pull / push collectives even on one rank")
     a = ap.parse_args()
@@ -40,7 +42,7 @@ def main():
     toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
     gen = time.perf_counter() - t0
     cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters,
-                    sparse_comm=a.sparse_comm, local_server=a.local_server == "on")
+                    sparse_comm=a.sparse_comm, local_server=a.local_server == "on", fused_rows=a.fused_rows == "on")
     if a.max_chunk:
         cfg.max_chunk = a.max_chunk
     cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper

@@ -18,4 +18,7 @@ for C in "share:$SHARE" "full:$FULL"; do
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM_RD --kernel-include-regex "lda_cgs" -d $O/pmcA_$N -o run -- python3 scripts/bench_lda.py $A > $O/pmcA_$N.log 2>&1 || { echo "pmcA $N failed"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAIT_ANY SQ_INSTS_VMEM_WR --kernel-include-regex "lda_cgs" -d $O/pmcB_$N -o run -- python3 scripts/bench_lda.py $A > $O/pmcB_$N.log 2>&1 || { echo "pmcB $N failed"; exit 1; }
 done
+for D in $O/kt_* $O/pmcA_* $O/pmcB_*; do
+  [ -d "$D" ] && python3 scripts/pmc_summary.py "$D" --match lda_cgs > /dev/null 2>&1
+done
 echo done
