@@ -21,6 +21,15 @@
 
 namespace {
 
+// wave-uniform copies (SGPRs) of values every lane of the wave holds equally
+__device__ __forceinline__ long uni64(long v) {
+  return ((long)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+         (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ float uni_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -252,7 +261,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
                                            // waits on ONE memory round trip, not two
     for (long i = a; i < b; ++i) {
       const int d = d_next;
-      const int z = z_next;
+      // wave-uniform (every lane loaded the same id): the topic slot index below is then a
+      // scalar, and the one-lane row updates are dynamic register indexing (s_set_gpr_idx),
+      // not a select over all TPL registers
+      const int z = __builtin_amdgcn_readfirstlane(z_next);
       DT* drow = ndk + (long)d * ldd;
       float nd[TPL];
       if (i + 1 < b) {
@@ -265,19 +277,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
 #pragma unroll
         for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
       }
-      // remove the token: only lane z / TPL changes, at the uniform slot z % TPL (a
-      // scalar branch picks the slot; one lane updates three registers)
+      // remove the token: only lane z / TPL changes, at the uniform slot z % TPL. The slot is
+      // read and written by dynamic register indexing with the scalar index (a loop of
+      // "if (t == zt)" was if-converted into selects over all TPL registers: ~5 VALU per
+      // topic per update, most of the token's VALU work)
       const int zl = z / TPL, zt = z % TPL;
       const float inv_z = s_inv[z];
-#pragma unroll
-      for (int t = 0; t < TPL; ++t) {
-        if (t == zt) {
-          if (lane == zl) {
-            nd[t] -= 1.f;
-            nwf[t] -= 1.f;
-            qw[t] = (nwf[t] + beta) * inv_z;
-          }
-        }
+      {
+        const bool me = lane == zl;
+        const float dv = nd[zt], wv = nwf[zt], qv = qw[zt];
+        const float nw = me ? wv - 1.f : wv;
+        nd[zt] = me ? dv - 1.f : dv;
+        nwf[zt] = nw;
+        qw[zt] = me ? (nw + beta) * inv_z : qv;
       }
       float s = 0.f;
 #pragma unroll
@@ -302,17 +314,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
       }
       int nz = __builtin_amdgcn_readlane(k0 + found, src);
       if (nz >= K) nz = K - 1;
-      // add the token back with its new topic
+      // add the token back with its new topic (uniform slot: dynamic register indexing)
       const int nzl = nz / TPL, nzt = nz % TPL;
       const float inv_nz = s_inv[nz];
-#pragma unroll
-      for (int t = 0; t < TPL; ++t) {
-        if (t == nzt) {
-          if (lane == nzl) {
-            nwf[t] += 1.f;
-            qw[t] = (nwf[t] + beta) * inv_nz;
-          }
-        }
+      {
+        const bool me = lane == nzl;
+        const float wv = nwf[nzt], qv = qw[nzt];
+        const float nw = me ? wv + 1.f : wv;
+        nwf[nzt] = nw;
+        qw[nzt] = me ? (nw + beta) * inv_nz : qv;
       }
       if (lane == 0) {
         tz[i] = nz;
@@ -455,6 +465,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
   __shared__ float s_q;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
   const int nb = Kp >> 6;
   __shared__ int s_c;
   if (ldelta)
@@ -575,82 +586,98 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       if (lane == 63) s_q = v;
     }
     __syncthreads();
-    long i = a + wv;
+    // every per-token value below is wave-uniform (the wave samples ONE token at a time):
+    // they are read into SGPRs (readfirstlane), so the doc-list bounds, positions and the
+    // RNG are scalar work and each lane's list entry is a 32-bit offset from a scalar base
+    // (the 64-bit per-lane index arithmetic of the first form was a third of the loop's VALU
+    // instructions; PMC of the round-5 kernel: 190 VALU per token, VALU-bound at 81 %)
+    const long a_u = uni64(a), b_u = uni64(b);
+    long i = a_u + wvu;
     int d = 0, z = 0;
-    long p = 0, lo = 0, hi = 0;
+    long p = 0, lo = 0;
+    int len = 0;
     float inv_z = 0.f;
     // the first 128 entries of the token's doc list sit in registers (zv0: lo + lane, zv1:
     // lo + 64 + lane), loaded one token ahead; the (rare) rest is read in the loop
     int zv0 = 0, zv1 = 0;
-    if (i < b) {
-      z = tz[i];
-      p = tpos[i];
+    if (i < b_u) {
+      z = __builtin_amdgcn_readfirstlane(tz[i]);
+      p = uni64(tpos[i]);
       if constexpr (SPAN) {
-        const long sp = tspan[i];
+        const long sp = uni64(tspan[i]);
         lo = sp & ((1L << 40) - 1);
-        hi = lo + (sp >> 40);
+        len = (int)(sp >> 40);
       } else {
-        d = tdoc[i];
-        lo = doc_off[d];
-        hi = doc_off[d + 1];
+        d = __builtin_amdgcn_readfirstlane(tdoc[i]);
+        lo = uni64(doc_off[d]);
+        len = (int)(uni64(doc_off[d + 1]) - lo);
       }
-      inv_z = inv_nk[z];
-      if (lo + lane < hi) zv0 = __builtin_nontemporal_load(zdoc + lo + lane);
-      if (lo + 64 + lane < hi) zv1 = __builtin_nontemporal_load(zdoc + lo + 64 + lane);
+      inv_z = uni_f(inv_nk[z]);
+      const unsigned short* zb = zdoc + lo;
+      if (lane < len) zv0 = __builtin_nontemporal_load(zb + lane);
+      if (64 + lane < len) zv1 = __builtin_nontemporal_load(zb + 64 + lane);
     }
-    for (; i < b; i += WAVES) {
+    for (; i < b_u; i += WAVES) {
       const long inx = i + WAVES;
       int dn = 0, zn = 0;
       long pn = 0, spn = 0;
-      if (inx < b) {
+      if (inx < b_u) {
         if constexpr (SPAN) spn = tspan[inx];
         else dn = tdoc[inx];
         zn = tz[inx];
         pn = tpos[inx];
       }
+      const unsigned short* zb = zdoc + lo;
+      const int pl = (int)(p - lo);  // this token's own entry in its doc list
       const float qz = s_qw[z] - inv_z;  // z's factor without this token
       float sb = 0.f;
-      if (lo + lane < hi && lo + lane != p) sb += zv0 == z ? qz : s_qw[zv0];
-      if (lo + 64 + lane < hi && lo + 64 + lane != p) sb += zv1 == z ? qz : s_qw[zv1];
+      if (lane < len && lane != pl) sb += zv0 == z ? qz : s_qw[zv0];
+      if (64 + lane < len && 64 + lane != pl) sb += zv1 == z ? qz : s_qw[zv1];
       // the rest of a long document's list (clueweb1 averages 392 tokens per doc): four
       // entries per lane per round with their loads issued together (one memory round trip
       // per 256 entries, not per 64), added in list order as before
       // (a predicated form that also batches the last < 256 entries took 81 VGPRs and ran
       // 1.99 vs 1.54 s per clueweb1 half-share sweep)
-      long j = lo + 128 + lane;
-      for (; j + 192 < hi; j += 256) {
+      int j = 128 + lane;
+      for (; j + 192 < len; j += 256) {
         int zq[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) zq[q] = __builtin_nontemporal_load(zdoc + j + 64 * q);
+        for (int q = 0; q < 4; ++q) zq[q] = __builtin_nontemporal_load(zb + j + 64 * q);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sb += j + 64 * q == p ? 0.f : (zq[q] == z ? qz : s_qw[zq[q]]);
+        for (int q = 0; q < 4; ++q) sb += j + 64 * q == pl ? 0.f : (zq[q] == z ? qz : s_qw[zq[q]]);
       }
-      for (; j < hi; j += 64) {
-        const int zj = __builtin_nontemporal_load(zdoc + j);
-        sb += j == p ? 0.f : (zj == z ? qz : s_qw[zj]);
+      for (; j < len; j += 64) {
+        const int zj = __builtin_nontemporal_load(zb + j);
+        sb += j == pl ? 0.f : (zj == z ? qz : s_qw[zj]);
       }
       const float inclb = wave_incl_scan(sb, lane);
       const float B = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inclb), 63));
       const float corr = inv_z;
-      const float A = alpha * fmaxf(s_q - corr, 0.f);
+      const float A = alpha * fmaxf(uni_f(s_q) - corr, 0.f);
       const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
       const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * (A + B);
       // next token's doc range and topic factor: its ids have arrived by now
-      long lon = 0, hin = 0;
+      long lon = 0;
+      int lenn = 0;
       float invn = 0.f;
       int zn0 = 0, zn1 = 0;
-      if (inx < b) {
+      if (inx < b_u) {
+        zn = __builtin_amdgcn_readfirstlane(zn);
+        pn = uni64(pn);
         if constexpr (SPAN) {
+          spn = uni64(spn);
           lon = spn & ((1L << 40) - 1);
-          hin = lon + (spn >> 40);
+          lenn = (int)(spn >> 40);
         } else {
-          lon = doc_off[dn];
-          hin = doc_off[dn + 1];
+          dn = __builtin_amdgcn_readfirstlane(dn);
+          lon = uni64(doc_off[dn]);
+          lenn = (int)(uni64(doc_off[dn + 1]) - lon);
         }
-        invn = inv_nk[zn];
+        invn = uni_f(inv_nk[zn]);
         // the next token's doc list, in flight while this token samples
-        if (lon + lane < hin) zn0 = __builtin_nontemporal_load(zdoc + lon + lane);
-        if (lon + 64 + lane < hin) zn1 = __builtin_nontemporal_load(zdoc + lon + 64 + lane);
+        const unsigned short* zbn = zdoc + lon;
+        if (lane < lenn) zn0 = __builtin_nontemporal_load(zbn + lane);
+        if (64 + lane < lenn) zn1 = __builtin_nontemporal_load(zbn + 64 + lane);
       }
       int nz;
       if (u < B) {  // doc bucket: the topic of one of the doc's other tokens
@@ -661,31 +688,31 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           float pre = inclb - sb;
           bool done = false;
           for (int q = 0; q < 2 && !done; ++q) {  // the two entries held in registers
-            const long j = lo + lane + 64 * q;
-            if (j >= hi) break;
-            if (j == p) continue;
+            const int jq = lane + 64 * q;
+            if (jq >= len) break;
+            if (jq == pl) continue;
             const int zj = q == 0 ? zv0 : zv1;
             f = zj;
             pre += zj == z ? qz : s_qw[zj];
             done = pre > u;
           }
-          long j = lo + lane + 128;
-          for (; !done && j + 192 < hi; j += 256) {  // then four loads per round trip
+          int jw = lane + 128;
+          for (; !done && jw + 192 < len; jw += 256) {  // then four loads per round trip
             int zq[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) zq[q] = __builtin_nontemporal_load(zdoc + j + 64 * q);
+            for (int q = 0; q < 4; ++q) zq[q] = __builtin_nontemporal_load(zb + jw + 64 * q);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              if (!done && j + 64 * q != p) {
+              if (!done && jw + 64 * q != pl) {
                 f = zq[q];
                 pre += zq[q] == z ? qz : s_qw[zq[q]];
                 done = pre > u;
               }
             }
           }
-          for (; !done && j < hi; j += 64) {
-            if (j == p) continue;
-            const int zj = __builtin_nontemporal_load(zdoc + j);
+          for (; !done && jw < len; jw += 64) {
+            if (jw == pl) continue;
+            const int zj = __builtin_nontemporal_load(zb + jw);
             f = zj;
             pre += zj == z ? qz : s_qw[zj];
             done = pre > u;
@@ -694,9 +721,9 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         nz = __builtin_amdgcn_readlane(f, src);
       } else {  // smoothing bucket: block by block sums, then topic within the block
         const float u2 = (u - B) / alpha;
-        const int zb = z >> 6;
+        const int zb6 = z >> 6;
         float sd = 0.f;
-        for (int k = lane; k < nb; k += 64) sd += s_bs[k] - (k == zb ? corr : 0.f);
+        for (int k = lane; k < nb; k += 64) sd += s_bs[k] - (k == zb6 ? corr : 0.f);
         const float incld = wave_incl_scan(sd, lane);
         const unsigned long long hit = __ballot(incld > u2);
         const int src = hit ? (int)__builtin_ctzll(hit) : 63;
@@ -705,7 +732,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         if (lane == src) {
           float pre = incld - sd;
           for (int k = lane; k < nb; k += 64) {
-            const float v = s_bs[k] - (k == zb ? corr : 0.f);
+            const float v = s_bs[k] - (k == zb6 ? corr : 0.f);
             fb = k;
             base = pre;
             if (pre + v > u2) break;
@@ -764,15 +791,15 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
       }
       // the next token of the same document: its prefetched list missed this token's move
-      if ((SPAN ? lon == lo : dn == d) && nz != z && inx < b) {
-        if (lon + lane == p) zn0 = nz;
-        if (lon + 64 + lane == p) zn1 = nz;
+      if ((SPAN ? lon == lo : dn == d) && nz != z && inx < b_u) {
+        if (lane == pl) zn0 = nz;
+        if (64 + lane == pl) zn1 = nz;
       }
       d = dn;
       z = zn;
       p = pn;
       lo = lon;
-      hi = hin;
+      len = lenn;
       inv_z = invn;
       zv0 = zn0;
       zv1 = zn1;

@@ -41,7 +41,7 @@ _lib.register({
 # tokens/s at 1M x 1M x 1000 (profiles/r1_lda/occupancy) — more resident waves hide the
 # random doc-row fetch best. (The doc-row prefetch and the other occupancies measured
 # there were slower and are no longer built.)
-SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "3"))
+SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "0"))  # 3 (+2 waves per SIMD) spills the dynamically indexed topic rows to scratch since round 5
 
 
 # Sampler choice: "dense" = register-row kernel (K <= 1024), "sparse" = doc-token-list
