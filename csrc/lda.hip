@@ -182,7 +182,7 @@ struct PsRows {
 // (0.90e9 vs 1.17e9 tokens/s at K = 1000, profiles/r1_lda/ldapf: its extra VGPRs cost a
 // wave per SIMD) and was removed.
 template <int TPL, class DT, int XW = 0>  // topics per lane; K_pad = 64 * TPL
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 ? 4 + XW : 5 + XW) < 8 ? (TPL == 16 ? 4 + XW : 5 + XW) : 8, 8))) void lda_cgs_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 ? 5 + XW : 8, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
   constexpr int WAVES = 4;
   __shared__ float s_inv[KP];
   __shared__ int s_delta[KP];
-  __shared__ int s_nw0[WAVES][KP];  // chunk-start word row (flush delta), kept out of VGPRs
+  __shared__ int s_nw0[WAVES][KP];  // per wave: the pulled word row, then the chunk's moves
+  __shared__ float4 s_x[WAVES][TPL / 2];  // the drawn lane's doc counts + qw (topic walk)
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
     s_inv[k] = k < K ? inv_nk[k] : 0.f;
     s_delta[k] = 0;
@@ -209,11 +210,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     const long a = chunk_start[c], b = chunk_start[c + 1];
     const int w = tword[a];
     int* wrow = nwk + (long)w * ldw + k0;
-    // word row held as floats (exact for counts < 2^24) plus the per-word factor
-    // qw_t = (n_wt + beta) / (n_t + V beta); a token then costs ONE multiply-add per
-    // topic, p_t = (n_dt + alpha) * qw_t, and only the two topics a token moves have
-    // their qw refreshed
-    float nwf[TPL], qw[TPL];
+    // the per-word factor qw_t = (n_wt + beta) / (n_t + V beta) in registers; a token then
+    // costs ONE multiply-add per topic, p_t = (n_dt + alpha) * qw_t, and only the two topics
+    // a token moves have their qw changed
+    float qw[TPL];
     if (ps.pbuf) {
       // the word row from its pull slot into this wave's LDS row (zero, then scatter)
       int* lrow = &s_nw0[wv][0];
@@ -245,18 +245,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
 #pragma unroll
       for (int t = 0; t < TPL; t += 4) {
         const int4 v = *(const int4*)(nw0s + t);
-        nwf[t] = (float)v.x; nwf[t + 1] = (float)v.y; nwf[t + 2] = (float)v.z; nwf[t + 3] = (float)v.w;
+        qw[t] = (float)v.x; qw[t + 1] = (float)v.y; qw[t + 2] = (float)v.z; qw[t + 3] = (float)v.w;
       }
     } else {
 #pragma unroll
       for (int t = 0; t < TPL; t += 4) {
         const int4 v = *(const int4*)(wrow + t);
-        *(int4*)(nw0s + t) = v;
-        nwf[t] = (float)v.x; nwf[t + 1] = (float)v.y; nwf[t + 2] = (float)v.z; nwf[t + 3] = (float)v.w;
+        qw[t] = (float)v.x; qw[t + 1] = (float)v.y; qw[t + 2] = (float)v.z; qw[t + 3] = (float)v.w;
       }
     }
+    // qw is linear in the word count (a move changes qw_t by exactly +-1/(n_t + V beta)),
+    // so no count row is kept in registers: the chunk's word-row moves are counted in this
+    // wave's LDS row (zeroed here, flushed at the chunk end)
+    float qs = 0.f;  // sum of this lane's qw: the token's mass is alpha * qs + sum n_dt qw_t
 #pragma unroll
-    for (int t = 0; t < TPL; ++t) qw[t] = (nwf[t] + beta) * s_inv[k0 + t];
+    for (int t = 0; t < TPL; ++t) {
+      qw[t] = (qw[t] + beta) * s_inv[k0 + t];
+      qs += qw[t];
+    }
+#pragma unroll
+    for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
+    int* wdel = &s_nw0[wv][0];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
                                            // waits on ONE memory round trip, not two
     for (long i = a; i < b; ++i) {
@@ -285,44 +297,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
       const float inv_z = s_inv[z];
       {
         const bool me = lane == zl;
-        const float dv = nd[zt], wv = nwf[zt], qv = qw[zt];
-        const float nw = me ? wv - 1.f : wv;
+        const float dv = nd[zt], qv = qw[zt];
         nd[zt] = me ? dv - 1.f : dv;
-        nwf[zt] = nw;
-        qw[zt] = me ? (nw + beta) * inv_z : qv;
+        qw[zt] = me ? qv - inv_z : qv;
+        qs -= me ? inv_z : 0.f;
       }
-      float s = 0.f;
+      float s = alpha * qs;
 #pragma unroll
-      for (int t = 0; t < TPL; ++t) s = fmaf(nd[t] + alpha, qw[t], s);
+      for (int t = 0; t < TPL; ++t) s = fmaf(nd[t], qw[t], s);
       const float incl = wave_incl_scan(s, lane);
       const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
       const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
       const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * total;
       const unsigned long long hit = __ballot(incl > u);
       const int src = hit ? (int)__builtin_ctzll(hit) : 63;
-      // walk the chosen lane's topics: first t with excl + prefix(t) > u
+      // walk the chosen lane's topics: the lane hands its TPL counts and factors to lanes
+      // 0 .. TPL-1 through LDS (one topic per lane, a 16-lane DPP row scan, one ballot)
+      // instead of every lane walking its own TPL topics (~3 VALU per topic, a third of the
+      // token's VALU work)
       int found;
       {
-        float pre = incl - s;
-        int f = -1;
+        const float ex = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl - s), src));
+        if (lane == src) {
 #pragma unroll
-        for (int t = 0; t < TPL; ++t) {
-          pre = fmaf(nd[t] + alpha, qw[t], pre);
-          f = (f < 0 && pre > u) ? t : f;
+          for (int t = 0; t < TPL; t += 4) {
+            s_x[wv][t / 4] = float4{nd[t], nd[t + 1], nd[t + 2], nd[t + 3]};
+            s_x[wv][TPL / 4 + t / 4] = float4{qw[t], qw[t + 1], qw[t + 2], qw[t + 3]};
+          }
         }
-        found = f < 0 ? TPL - 1 : f;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float* xr = (const float*)s_x[wv];
+        const float pv = lane < TPL ? (xr[lane] + alpha) * xr[TPL + lane] : 0.f;
+        float c = dpp_add(pv, 0);
+        c = dpp_add(c, 1);
+        c = dpp_add(c, 2);
+        c = dpp_add(c, 3);  // inclusive prefix over lanes 0..15 (one DPP row)
+        const unsigned long long h = __ballot(lane < TPL && c + ex > u) & ((1ull << TPL) - 1);
+        const unsigned long long nzp = __ballot(pv > 0.f) & ((1ull << TPL) - 1);
+        found = h ? (int)__builtin_ctzll(h) : (nzp ? 63 - (int)__builtin_clzll(nzp) : TPL - 1);
       }
-      int nz = __builtin_amdgcn_readlane(k0 + found, src);
+      int nz = src * TPL + found;
       if (nz >= K) nz = K - 1;
       // add the token back with its new topic (uniform slot: dynamic register indexing)
       const int nzl = nz / TPL, nzt = nz % TPL;
       const float inv_nz = s_inv[nz];
       {
         const bool me = lane == nzl;
-        const float wv = nwf[nzt], qv = qw[nzt];
-        const float nw = me ? wv + 1.f : wv;
-        nwf[nzt] = nw;
-        qw[nzt] = me ? (nw + beta) * inv_nz : qv;
+        const float qv = qw[nzt];
+        qw[nzt] = me ? qv + inv_nz : qv;
+        qs += me ? inv_nz : 0.f;
       }
       if (lane == 0) {
         tz[i] = nz;
@@ -331,9 +356,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
           DocRow<DT>::add(drow, nz, 1);
           atomicSub(&s_delta[z], 1);
           atomicAdd(&s_delta[nz], 1);
+          wdel[z] -= 1;
+          wdel[nz] += 1;
         }
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's row moves -> every lane
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // flush this chunk's word-row delta
     if (ps.qbuf) {
       unsigned char* slot = ps.qbuf + ps.qoff[w];
@@ -341,13 +371,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
       if (cap < 0) {
 #pragma unroll
         for (int t = 0; t < TPL; ++t) {
-          const int dlt = (int)nwf[t] - nw0s[t];
+          const int dlt = nw0s[t];
           if (dlt) atomicAdd((int*)slot + k0 + t, dlt);
         }
       } else {
         int mine = 0;
 #pragma unroll
-        for (int t = 0; t < TPL; ++t) mine += ((int)nwf[t] != nw0s[t]) ? 1 : 0;
+        for (int t = 0; t < TPL; ++t) mine += nw0s[t] != 0 ? 1 : 0;
         const float incl = wave_incl_scan((float)mine, lane);
         const int tot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
         int base = 0;
@@ -361,7 +391,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
         bool over = false;
 #pragma unroll
         for (int t = 0; t < TPL; ++t) {
-          const int dlt = (int)nwf[t] - nw0s[t];
+          const int dlt = nw0s[t];
           if (dlt) {
             if (pos < cap) {
               cnt[pos] = dlt;
@@ -377,7 +407,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((TPL == 16 
     } else {
 #pragma unroll
       for (int t = 0; t < TPL; ++t) {
-        const int dlt = (int)nwf[t] - nw0s[t];
+        const int dlt = nw0s[t];
         if (dlt) atomicAdd(wrow + t, dlt);
       }
     }
@@ -617,16 +647,23 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       if (lane < len) zv0 = __builtin_nontemporal_load(zb + lane);
       if (64 + lane < len) zv1 = __builtin_nontemporal_load(zb + 64 + lane);
     }
+    // the ids (span or doc, topic, list position) are loaded TWO tokens ahead into VGPRs
+    // through a VGPR index (vector loads, after the doc-list sum, so that sum waits only on
+    // its own list): a scalar load of them, or a readfirstlane next to the load, put a full
+    // memory round trip in every token (s_waitcnt lgkmcnt also covers the LDS reads)
+    auto load_ids = [&](long t, long& sp, int& dd, int& zz, long& pp) {
+      long ix = t < b_u ? t : b_u - 1;  // clamped: no branch around the loads
+      asm volatile("" : "+v"(ix));
+      if constexpr (SPAN) sp = tspan[ix];
+      else dd = tdoc[ix];
+      zz = tz[ix];
+      pp = tpos[ix];
+    };
+    long sp1 = 0, pp1 = 0;
+    int dd1 = 0, zz1 = 0;
+    load_ids(i + WAVES, sp1, dd1, zz1, pp1);
     for (; i < b_u; i += WAVES) {
       const long inx = i + WAVES;
-      int dn = 0, zn = 0;
-      long pn = 0, spn = 0;
-      if (inx < b_u) {
-        if constexpr (SPAN) spn = tspan[inx];
-        else dn = tdoc[inx];
-        zn = tz[inx];
-        pn = tpos[inx];
-      }
       const unsigned short* zb = zdoc + lo;
       const int pl = (int)(p - lo);  // this token's own entry in its doc list
       const float qz = s_qw[z] - inv_z;  // z's factor without this token
@@ -650,6 +687,9 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
         const int zj = __builtin_nontemporal_load(zb + j);
         sb += j == pl ? 0.f : (zj == z ? qz : s_qw[zj]);
       }
+      long sp2 = 0, pp2 = 0;
+      int dd2 = 0, zz2 = 0;
+      load_ids(i + 2 * WAVES, sp2, dd2, zz2, pp2);
       const float inclb = wave_incl_scan(sb, lane);
       const float B = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inclb), 63));
       const float corr = inv_z;
@@ -661,15 +701,15 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       int lenn = 0;
       float invn = 0.f;
       int zn0 = 0, zn1 = 0;
+      const int zn = __builtin_amdgcn_readfirstlane(zz1);
+      const long pn = uni64(pp1);
+      const int dn = SPAN ? 0 : __builtin_amdgcn_readfirstlane(dd1);
       if (inx < b_u) {
-        zn = __builtin_amdgcn_readfirstlane(zn);
-        pn = uni64(pn);
         if constexpr (SPAN) {
-          spn = uni64(spn);
+          const long spn = uni64(sp1);
           lon = spn & ((1L << 40) - 1);
           lenn = (int)(spn >> 40);
         } else {
-          dn = __builtin_amdgcn_readfirstlane(dn);
           lon = uni64(doc_off[dn]);
           lenn = (int)(uni64(doc_off[dn + 1]) - lon);
         }
@@ -803,6 +843,10 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       inv_z = invn;
       zv0 = zn0;
       zv1 = zn1;
+      sp1 = sp2;
+      dd1 = dd2;
+      zz1 = zz2;
+      pp1 = pp2;
     }
     if (wdelta == 1) {
       flush_wd();
