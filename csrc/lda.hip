@@ -923,7 +923,7 @@ static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* 
                         int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
                         float beta, unsigned long long seed, int variant, PsRows ps, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  // variant 0: compiler occupancy; 3: two more waves per SIMD (the default). The doc-row
+  // variant 0: five waves per SIMD (the default); 3: six (80 VGPRs). The doc-row
   // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
   // (profiles/r1_lda/occupancy) and are no longer built.
   // variant | 0x100: deterministic one-wave sampling (tests)
@@ -934,17 +934,17 @@ static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* 
 #define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, ps, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
-    return variant == 3 ? launch_cgs<int, 2>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
+    return variant == 3 ? launch_cgs<int, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
                         : launch_cgs<int, 0>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL);
   }
   if (ndk_bits == 16) {
     if (ldd % 8) return HARP_EBADARG;
-    return variant == 3 ? launch_cgs<unsigned short, 2>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
+    return variant == 3 ? launch_cgs<unsigned short, 1>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL)
                         : launch_cgs<unsigned short, 0>(CGS_ARGS, (unsigned short*)ndk, ldd, CGS_TAIL);
   }
   if (ndk_bits == 8) {
     if (ldd % 16) return HARP_EBADARG;
-    return variant == 3 ? launch_cgs<unsigned char, 2>(CGS_ARGS, (unsigned char*)ndk, ldd, CGS_TAIL)
+    return variant == 3 ? launch_cgs<unsigned char, 1>(CGS_ARGS, (unsigned char*)ndk, ldd, CGS_TAIL)
                         : launch_cgs<unsigned char, 0>(CGS_ARGS, (unsigned char*)ndk, ldd, CGS_TAIL);
   }
 #undef CGS_ARGS

@@ -36,12 +36,11 @@ _lib.register({
 })
 
 
-# csrc/lda.hip harp_lda_cgs variants: 0 = compiler occupancy (4 waves/SIMD at K=1000),
-# 3 = two more waves per SIMD. Default 3 (6 waves, a few VGPRs spilled): 1.47e9 vs 1.17e9
-# tokens/s at 1M x 1M x 1000 (profiles/r1_lda/occupancy) — more resident waves hide the
-# random doc-row fetch best. (The doc-row prefetch and the other occupancies measured
-# there were slower and are no longer built.)
-SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "0"))  # 3 (+2 waves per SIMD) spills the dynamically indexed topic rows to scratch since round 5
+# csrc/lda.hip harp_lda_cgs variants: 0 = five waves per SIMD, 3 = six (the default). Since
+# the round-5 LDS topic walk and linear qw updates the six-wave build fits 80 VGPRs with two
+# spilled in the chunk prologue only: 8-share sweep 8.72 -> 8.06 ms, full size dense 48.2 ->
+# 43.2 ms (profiles/r5_lda_waves). More resident waves hide the per-token doc-row fetch.
+SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "3"))
 
 
 # Sampler choice: "dense" = register-row kernel (K <= 1024), "sparse" = doc-token-list
