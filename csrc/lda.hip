@@ -67,6 +67,16 @@ __device__ __forceinline__ float wave_incl_scan(float v, int) {
 // bytes of the per-token row read that bounds this kernel; updated with 32-bit atomics
 // on the containing dword: counts stay in [0, 65535], so a +-1 on one half never
 // carries or borrows into the other)
+// a relaxed device-scope atomic add by ONE lane through a global-address-space pointer
+// laundered into VGPRs: a uniform address would be rewritten into a wave reduction (mbcnt,
+// popcount and two branches around the atomic) although only one lane is active
+__device__ __forceinline__ void lane_atomic_add(const void* p, unsigned v) {
+  typedef __attribute__((address_space(1))) unsigned gu32;
+  unsigned long a = (unsigned long)p;
+  asm volatile("" : "+v"(a));
+  __hip_atomic_fetch_add((gu32*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <class DT>
 struct DocRow;
 template <>
@@ -80,6 +90,7 @@ struct DocRow<int> {
     }
   }
   __device__ static __forceinline__ void add(int* drow, int k, int v) { atomicAdd(drow + k, v); }
+  __device__ static __forceinline__ void add1(int* drow, int k, int v) { lane_atomic_add(drow + k, (unsigned)v); }
 };
 template <>
 struct DocRow<unsigned short> {
@@ -113,6 +124,11 @@ struct DocRow<unsigned short> {
     const unsigned sh = (k & 1) ? 16u : 0u;
     if (v > 0) atomicAdd(word, (unsigned)v << sh);
     else atomicSub(word, (unsigned)(-v) << sh);
+  }
+  // v = +-1 from one lane (two's complement: a -1 on a nonzero count borrows only inside
+  // its own field)
+  __device__ static __forceinline__ void add1(unsigned short* drow, int k, int v) {
+    lane_atomic_add(drow + (k & ~1), (unsigned)v << ((k & 1) ? 16u : 0u));
   }
 };
 
@@ -158,6 +174,9 @@ struct DocRow<unsigned char> {
     if (v > 0) atomicAdd(word, (unsigned)v << sh);
     else atomicSub(word, (unsigned)(-v) << sh);
   }
+  __device__ static __forceinline__ void add1(unsigned char* drow, int k, int v) {
+    lane_atomic_add(drow + (k & ~3), (unsigned)v << ((unsigned)(k & 3) * 8u));
+  }
 };
 
 // Fused parameter-server rows (push-pull with sparse rows, models/lda.py): the word rows
@@ -189,6 +208,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     unsigned long long seed, int det, PsRows ps) {
   constexpr int KP = 64 * TPL;
   constexpr int WAVES = 4;
+  constexpr bool PK = sizeof(DT) == 1 && TPL == 16;  // packed-row token loop (below)
   __shared__ float s_inv[KP];
   __shared__ int s_delta[KP];
   __shared__ int s_nw0[WAVES][KP];  // per wave: the pulled word row, then the chunk's moves
@@ -202,7 +222,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
   const int wv = threadIdx.x >> 6;
   // det: ONE wave samples every chunk in order (no races on doc rows: bit-reproducible,
   // independent of the word-row numbering; a test mode, launched as one workgroup)
-  const long wave_g = det ? (wv == 0 ? 0 : nchunks) : ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // wave-uniform (SGPR): the chunk bounds, the token index and its RNG are scalar work
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const long wave_g = det ? (wvu == 0 ? 0 : nchunks) : (long)blockIdx.x * (blockDim.x >> 6) + wvu;
   const long nwaves = det ? 1 : ((long)gridDim.x * blockDim.x) >> 6;
   const int k0 = lane * TPL;
   int* nw0s = &s_nw0[wv][k0];
@@ -269,95 +291,225 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
-                                           // waits on ONE memory round trip, not two
-    for (long i = a; i < b; ++i) {
-      const int d = d_next;
-      // wave-uniform (every lane loaded the same id): the topic slot index below is then a
-      // scalar, and the one-lane row updates are dynamic register indexing (s_set_gpr_idx),
-      // not a select over all TPL registers
-      const int z = __builtin_amdgcn_readfirstlane(z_next);
-      DT* drow = ndk + (long)d * ldd;
-      float nd[TPL];
-      if (i + 1 < b) {
-        d_next = tdoc[i + 1];
-        z_next = tz[i + 1];
-      }
+    if constexpr (PK) {
+      // packed uint8 rows, 16 topics per lane: the lane's counts stay the 4 loaded dwords
+      // (unpacked by one v_cvt_f32_ubyteN per use: 4 VGPRs, not 16 floats), and the NEXT
+      // token's row is loaded while this token samples. The previous token's writes are
+      // issued at the start of this token, before that row load: every wait then falls on
+      // memory operations issued a whole token earlier (vmcnt counts stores and atomics
+      // too, and the compiler's count is conservative over lane 0's branches). The row
+      // loaded for this token missed only the previous token's move: applied in registers
+      // when it is of the same document.
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const int d0 = __builtin_amdgcn_readfirstlane(tdoc[a]);
+      int zcur = __builtin_amdgcn_readfirstlane(tz[a]), dcur = d0;
+      v4u rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)d0 * ldd + k0));
+      int d_nx, z_nx;  // ids of the token after the current one (vector loads, one token ahead)
       {
-        int ndi[TPL];
-        DocRow<DT>::template load<TPL>(drow, k0, ndi);
-#pragma unroll
-        for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
+        long ix = a + 1 < b ? a + 1 : a;
+        asm volatile("" : "+v"(ix));
+        d_nx = tdoc[ix];
+        z_nx = tz[ix];
       }
-      // remove the token: only lane z / TPL changes, at the uniform slot z % TPL. The slot is
-      // read and written by dynamic register indexing with the scalar index (a loop of
-      // "if (t == zt)" was if-converted into selects over all TPL registers: ~5 VALU per
-      // topic per update, most of the token's VALU work)
-      const int zl = z / TPL, zt = z % TPL;
-      const float inv_z = s_inv[z];
-      {
-        const bool me = lane == zl;
-        const float dv = nd[zt], qv = qw[zt];
-        nd[zt] = me ? dv - 1.f : dv;
-        qw[zt] = me ? qv - inv_z : qv;
-        qs -= me ? inv_z : 0.f;
-      }
-      float s = alpha * qs;
-#pragma unroll
-      for (int t = 0; t < TPL; ++t) s = fmaf(nd[t], qw[t], s);
-      const float incl = wave_incl_scan(s, lane);
-      const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
-      const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
-      const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * total;
-      const unsigned long long hit = __ballot(incl > u);
-      const int src = hit ? (int)__builtin_ctzll(hit) : 63;
-      // walk the chosen lane's topics: the lane hands its TPL counts and factors to lanes
-      // 0 .. TPL-1 through LDS (one topic per lane, a 16-lane DPP row scan, one ballot)
-      // instead of every lane walking its own TPL topics (~3 VALU per topic, a third of the
-      // token's VALU work)
-      int found;
-      {
-        const float ex = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl - s), src));
-        if (lane == src) {
-#pragma unroll
-          for (int t = 0; t < TPL; t += 4) {
-            s_x[wv][t / 4] = float4{nd[t], nd[t + 1], nd[t + 2], nd[t + 3]};
-            s_x[wv][TPL / 4 + t / 4] = float4{qw[t], qw[t + 1], qw[t + 2], qw[t + 3]};
+      long pi = -1;
+      int pd = -1, pz = 0, pnz = 0;
+      DT* prow = ndk;
+      for (long i = a; i < b; ++i) {
+        const int d = dcur, z = zcur;
+        DT* drow = ndk + (long)d * ldd;
+        unsigned r[4] = {rw_nx.x, rw_nx.y, rw_nx.z, rw_nx.w};
+        const int dn = __builtin_amdgcn_readfirstlane(d_nx), zn = __builtin_amdgcn_readfirstlane(z_nx);
+        if (pi >= 0 && lane == 0) {
+          tz[pi] = pnz;
+          if (pnz != pz) {
+            DocRow<DT>::add1(prow, pz, -1);
+            DocRow<DT>::add1(prow, pnz, 1);
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const float* xr = (const float*)s_x[wv];
-        const float pv = lane < TPL ? (xr[lane] + alpha) * xr[TPL + lane] : 0.f;
-        float c = dpp_add(pv, 0);
-        c = dpp_add(c, 1);
-        c = dpp_add(c, 2);
-        c = dpp_add(c, 3);  // inclusive prefix over lanes 0..15 (one DPP row)
-        const unsigned long long h = __ballot(lane < TPL && c + ex > u) & ((1ull << TPL) - 1);
-        const unsigned long long nzp = __ballot(pv > 0.f) & ((1ull << TPL) - 1);
-        found = h ? (int)__builtin_ctzll(h) : (nzp ? 63 - (int)__builtin_clzll(nzp) : TPL - 1);
+        if (i + 1 < b) rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)dn * ldd + k0));
+        {
+          long ix = i + 2 < b ? i + 2 : i;
+          asm volatile("" : "+v"(ix));
+          d_nx = tdoc[ix];
+          z_nx = tz[ix];
+        }
+        if (d == pd && pnz != pz) {  // this row was loaded before the previous token's move
+          const unsigned m1 = lane == pz / TPL ? 1u << (8 * (pz & 3)) : 0u;
+          r[(pz % TPL) >> 2] -= m1;
+          const unsigned m2 = lane == pnz / TPL ? 1u << (8 * (pnz & 3)) : 0u;
+          r[(pnz % TPL) >> 2] += m2;
+        }
+        // the token's own count is left in the packed row: its removal is the product
+        // correction -qw_z (after qw_z's own update) on lane z / TPL, and the walk below
+        // takes 1 off topic z when it reads that lane's row
+        const int zl = z / TPL, zt = z % TPL;
+        const float inv_z = s_inv[z];
+        const bool mez = lane == zl;
+        float s;
+        {
+          const float qv = qw[zt];
+          const float qn = qv - inv_z;
+          qw[zt] = mez ? qn : qv;
+          qs -= mez ? inv_z : 0.f;
+          s = alpha * qs - (mez ? qn : 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) s = fmaf((float)((r[t >> 2] >> (8 * (t & 3))) & 0xFFu), qw[t], s);
+        const float incl = wave_incl_scan(s, lane);
+        const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+        const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
+        const float u = ((float)(unsigned)(rbits >> 40) * (1.f / 16777216.f)) * total;
+        const unsigned long long hit = __ballot(incl > u);
+        const int src = hit ? (int)__builtin_ctzll(hit) : 63;
+        int found;
+        {  // the drawn lane's topics walked by lanes 0..15 (as below, packed counts)
+          const float ex = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl - s), src));
+          if (lane == src) {
+#pragma unroll
+            for (int t = 0; t < TPL; t += 4) s_x[wv][t / 4] = float4{qw[t], qw[t + 1], qw[t + 2], qw[t + 3]};
+            ((uint4*)s_x[wv])[TPL / 4] = uint4{r[0], r[1], r[2], r[3]};
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const float* xr = (const float*)s_x[wv];
+          const unsigned char* xb = (const unsigned char*)(xr + TPL);
+          const float own = src == zl && lane == zt ? 1.f : 0.f;
+          const float pv = lane < TPL ? ((float)xb[lane] - own + alpha) * xr[lane] : 0.f;
+          float c = dpp_add(pv, 0);
+          c = dpp_add(c, 1);
+          c = dpp_add(c, 2);
+          c = dpp_add(c, 3);
+          const unsigned long long h = __ballot(lane < TPL && c + ex > u) & ((1ull << TPL) - 1);
+          const unsigned long long nzp = __ballot(pv > 0.f) & ((1ull << TPL) - 1);
+          found = h ? (int)__builtin_ctzll(h) : (nzp ? 63 - (int)__builtin_clzll(nzp) : TPL - 1);
+        }
+        int nz = src * TPL + found;
+        if (nz >= K) nz = K - 1;
+        const int nzl = nz / TPL, nzt = nz % TPL;
+        const float inv_nz = s_inv[nz];
+        {
+          const bool me = lane == nzl;
+          const float qv = qw[nzt];
+          qw[nzt] = me ? qv + inv_nz : qv;
+          qs += me ? inv_nz : 0.f;
+        }
+        if (lane == 0 && nz != z) {
+          int zi = z, ni = nz;
+          asm volatile("" : "+v"(zi), "+v"(ni));  // per-lane LDS addresses: no wave-reduction rewrite
+          atomicSub(&s_delta[zi], 1);
+          atomicAdd(&s_delta[ni], 1);
+          wdel[zi] -= 1;
+          wdel[ni] += 1;
+        }
+        pi = i;
+        pz = z;
+        pnz = nz;
+        pd = d;
+        prow = drow;
+        dcur = dn;
+        zcur = zn;
       }
-      int nz = src * TPL + found;
-      if (nz >= K) nz = K - 1;
-      // add the token back with its new topic (uniform slot: dynamic register indexing)
-      const int nzl = nz / TPL, nzt = nz % TPL;
-      const float inv_nz = s_inv[nz];
-      {
-        const bool me = lane == nzl;
-        const float qv = qw[nzt];
-        qw[nzt] = me ? qv + inv_nz : qv;
-        qs += me ? inv_nz : 0.f;
+      if (lane == 0) {  // the chunk's last token
+        tz[pi] = pnz;
+        if (pnz != pz) {
+          DocRow<DT>::add1(prow, pz, -1);
+          DocRow<DT>::add1(prow, pnz, 1);
+        }
       }
-      if (lane == 0) {
-        tz[i] = nz;
-        if (nz != z) {
-          DocRow<DT>::add(drow, z, -1);
-          DocRow<DT>::add(drow, nz, 1);
-          atomicSub(&s_delta[z], 1);
-          atomicAdd(&s_delta[nz], 1);
-          wdel[z] -= 1;
-          wdel[nz] += 1;
+    } else {
+      int d_next = tdoc[a], z_next = tz[a];  // token ids one ahead: the doc-row fetch then
+                                             // waits on ONE memory round trip, not two
+      for (long i = a; i < b; ++i) {
+        const int d = d_next;
+        // wave-uniform (every lane loaded the same id): the topic slot index below is then a
+        // scalar, and the one-lane row updates are dynamic register indexing (s_set_gpr_idx),
+        // not a select over all TPL registers
+        const int z = __builtin_amdgcn_readfirstlane(z_next);
+        DT* drow = ndk + (long)d * ldd;
+        float nd[TPL];
+        if (i + 1 < b) {
+          long ix = i + 1;
+          asm volatile("" : "+v"(ix));  // vector loads (a scalar load's lgkmcnt wait also covers LDS)
+          d_next = tdoc[ix];
+          z_next = tz[ix];
+        }
+        {
+          int ndi[TPL];
+          DocRow<DT>::template load<TPL>(drow, k0, ndi);
+  #pragma unroll
+          for (int t = 0; t < TPL; ++t) nd[t] = (float)ndi[t];
+        }
+        // remove the token: only lane z / TPL changes, at the uniform slot z % TPL. The slot is
+        // read and written by dynamic register indexing with the scalar index (a loop of
+        // "if (t == zt)" was if-converted into selects over all TPL registers: ~5 VALU per
+        // topic per update, most of the token's VALU work)
+        const int zl = z / TPL, zt = z % TPL;
+        const float inv_z = s_inv[z];
+        {
+          const bool me = lane == zl;
+          const float dv = nd[zt], qv = qw[zt];
+          nd[zt] = me ? dv - 1.f : dv;
+          qw[zt] = me ? qv - inv_z : qv;
+          qs -= me ? inv_z : 0.f;
+        }
+        float s = alpha * qs;
+  #pragma unroll
+        for (int t = 0; t < TPL; ++t) s = fmaf(nd[t], qw[t], s);
+        const float incl = wave_incl_scan(s, lane);
+        const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+        const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
+        const float u = ((float)(unsigned)(rbits >> 40) * (1.f / 16777216.f)) * total;
+        const unsigned long long hit = __ballot(incl > u);
+        const int src = hit ? (int)__builtin_ctzll(hit) : 63;
+        // walk the chosen lane's topics: the lane hands its TPL counts and factors to lanes
+        // 0 .. TPL-1 through LDS (one topic per lane, a 16-lane DPP row scan, one ballot)
+        // instead of every lane walking its own TPL topics (~3 VALU per topic, a third of the
+        // token's VALU work)
+        int found;
+        {
+          const float ex = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl - s), src));
+          if (lane == src) {
+  #pragma unroll
+            for (int t = 0; t < TPL; t += 4) {
+              s_x[wv][t / 4] = float4{nd[t], nd[t + 1], nd[t + 2], nd[t + 3]};
+              s_x[wv][TPL / 4 + t / 4] = float4{qw[t], qw[t + 1], qw[t + 2], qw[t + 3]};
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const float* xr = (const float*)s_x[wv];
+          const float pv = lane < TPL ? (xr[lane] + alpha) * xr[TPL + lane] : 0.f;
+          float c = dpp_add(pv, 0);
+          c = dpp_add(c, 1);
+          c = dpp_add(c, 2);
+          c = dpp_add(c, 3);  // inclusive prefix over lanes 0..15 (one DPP row)
+          const unsigned long long h = __ballot(lane < TPL && c + ex > u) & ((1ull << TPL) - 1);
+          const unsigned long long nzp = __ballot(pv > 0.f) & ((1ull << TPL) - 1);
+          found = h ? (int)__builtin_ctzll(h) : (nzp ? 63 - (int)__builtin_clzll(nzp) : TPL - 1);
+        }
+        int nz = src * TPL + found;
+        if (nz >= K) nz = K - 1;
+        // add the token back with its new topic (uniform slot: dynamic register indexing)
+        const int nzl = nz / TPL, nzt = nz % TPL;
+        const float inv_nz = s_inv[nz];
+        {
+          const bool me = lane == nzl;
+          const float qv = qw[nzt];
+          qw[nzt] = me ? qv + inv_nz : qv;
+          qs += me ? inv_nz : 0.f;
+        }
+        if (lane == 0) {
+          tz[i] = nz;
+          if (nz != z) {
+            DocRow<DT>::add1(drow, z, -1);
+            DocRow<DT>::add1(drow, nz, 1);
+            atomicSub(&s_delta[z], 1);
+            atomicAdd(&s_delta[nz], 1);
+            wdel[z] -= 1;
+            wdel[nz] += 1;
+          }
         }
       }
     }
@@ -695,7 +847,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       const float corr = inv_z;
       const float A = alpha * fmaxf(uni_f(s_q) - corr, 0.f);
       const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
-      const float u = (float)((rbits >> 40) * (1.0 / 16777216.0)) * (A + B);
+      const float u = ((float)(unsigned)(rbits >> 40) * (1.f / 16777216.f)) * (A + B);
       // next token's doc range and topic factor: its ids have arrived by now
       long lon = 0;
       int lenn = 0;
