@@ -19,6 +19,13 @@
 //  * counter-based RNG (splitmix64 of seed, token index): reproducible, no state.
 #include "common.h"
 
+#ifdef HARP_LDA_STAMPS
+// diagnostic build only (scripts/lda_stamps.py): per-phase shader-clock totals of the dense
+// sampler's chunk loop: [0] prologue, [1] token loop, [2] flush, [3] chunks, [4] tokens,
+// [5] whole wave
+__device__ unsigned long long g_lda_stamps[8];
+#endif
+
 namespace {
 
 // wave-uniform copies (SGPRs) of values every lane of the wave holds equally
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
-    unsigned long long seed, int det, PsRows ps) {
+    unsigned long long seed, int det, PsRows ps, const long* __restrict__ lpt) {
   constexpr int KP = 64 * TPL;
   constexpr int WAVES = 4;
   constexpr bool PK = sizeof(DT) == 1 && TPL == 16;  // packed-row token loop (below)
@@ -228,8 +235,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
   const long nwaves = det ? 1 : ((long)gridDim.x * blockDim.x) >> 6;
   const int k0 = lane * TPL;
   int* nw0s = &s_nw0[wv][k0];
-  for (long c = wave_g; c < nchunks; c += nwaves) {
-    const long a = chunk_start[c], b = chunk_start[c + 1];
+#ifdef HARP_LDA_STAMPS
+  unsigned long long st_pro = 0, st_tok = 0, st_fl = 0, st_n = 0, st_t = 0, st_t1 = 0, st_t2 = 0;
+  const unsigned long long st_w0 = clock64();
+#endif
+  // lpt (not in det mode): the chunks' (start, end) pairs longest first, dealt to the
+  // resident waves in snake order (round r: wave w takes rank r W + w, or r W + W-1-w on odd
+  // rounds), so every wave gets about the same number of tokens. The static stride over
+  // word order left the waves that drew the longest word chunks running long after the rest.
+  const bool lptm = lpt != nullptr && !det;
+  for (long r = 0;; ++r) {
+#ifdef HARP_LDA_STAMPS
+    const unsigned long long st_t0 = clock64();
+#endif
+    long a, b;
+    if (lptm) {
+      const long k = r * nwaves + ((r & 1) ? nwaves - 1 - wave_g : wave_g);
+      if (k >= nchunks) break;
+      a = lpt[2 * k];
+      b = lpt[2 * k + 1];
+    } else {
+      const long c = wave_g + r * nwaves;
+      if (c >= nchunks) break;
+      a = chunk_start[c];
+      b = chunk_start[c + 1];
+    }
     const int w = tword[a];
     int* wrow = nwk + (long)w * ldw + k0;
     // the per-word factor qw_t = (n_wt + beta) / (n_t + V beta) in registers; a token then
@@ -291,6 +321,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef HARP_LDA_STAMPS
+    st_t1 = clock64();
+    st_pro += st_t1 - st_t0;
+    st_n += 1;
+    st_t += b - a;
+#endif
     if constexpr (PK) {
       // packed uint8 rows, 16 topics per lane: the lane's counts stay the 4 loaded dwords
       // (unpacked by one v_cvt_f32_ubyteN per use: 4 VGPRs, not 16 floats), and the NEXT
@@ -516,6 +552,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's row moves -> every lane
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef HARP_LDA_STAMPS
+    st_t2 = clock64();
+    st_tok += st_t2 - st_t1;
+#endif
     // flush this chunk's word-row delta
     if (ps.qbuf) {
       unsigned char* slot = ps.qbuf + ps.qoff[w];
@@ -563,7 +603,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
         if (dlt) atomicAdd(wrow + t, dlt);
       }
     }
+#ifdef HARP_LDA_STAMPS
+    st_fl += clock64() - st_t2;
+#endif
   }
+#ifdef HARP_LDA_STAMPS
+  if (lane == 0) {
+    atomicAdd(&g_lda_stamps[0], st_pro);
+    atomicAdd(&g_lda_stamps[1], st_tok);
+    atomicAdd(&g_lda_stamps[2], st_fl);
+    atomicAdd(&g_lda_stamps[3], st_n);
+    atomicAdd(&g_lda_stamps[4], st_t);
+    atomicAdd(&g_lda_stamps[5], clock64() - st_w0);
+  }
+#endif
   __syncthreads();
   for (int k = threadIdx.x; k < K; k += blockDim.x)
     if (s_delta[k]) atomicAdd(nk_delta + k, s_delta[k]);
@@ -1017,26 +1070,47 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
 }  // namespace
 
 namespace {
+// workgroups of the dense sampler resident at once on this device (occupancy x CUs)
+template <class DT, int XW>
+long resident_blocks(int K) {
+  static long cached[3] = {0, 0, 0};
+  const int slot = K <= 256 ? 0 : K <= 512 ? 1 : 2;
+  if (cached[slot]) return cached[slot];
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  hipError_t e = slot == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lda_cgs_kernel<4, DT, XW>, 256, 0)
+                 : slot == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lda_cgs_kernel<8, DT, XW>, 256, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lda_cgs_kernel<16, DT, XW>, 256, 0);
+  if (e != hipSuccess || per <= 0) return 0;
+  cached[slot] = (long)per * cus;
+  return cached[slot];
+}
+
 template <class DT, int XW = 0>
 int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, DT* ndk, int ldd,
                int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha, float beta,
-               unsigned long long seed, int det, PsRows ps, hipStream_t s) {
+               unsigned long long seed, int det, PsRows ps, const long* lpt, hipStream_t s) {
   long blocks = (nchunks + 3) / 4;  // 4 waves per block
   if (blocks > 8192) blocks = 8192;
+  if (lpt && !det) {  // the snake deal assumes every wave is resident: one wave per slot
+    const long res = resident_blocks<DT, XW>(K);
+    if (res > 0 && blocks > res) blocks = res;
+  }
   if (det) blocks = 1;
   const dim3 g((unsigned)blocks), bl(256);
   if (K <= 256) {
     if (ldd < 256 || ldw < 256) return HARP_EBADARG;
     lda_cgs_kernel<4, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                           nk_delta, K, alpha, beta, seed, det, ps);
+                                           nk_delta, K, alpha, beta, seed, det, ps, lpt);
   } else if (K <= 512) {
     if (ldd < 512 || ldw < 512) return HARP_EBADARG;
     lda_cgs_kernel<8, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                           nk_delta, K, alpha, beta, seed, det, ps);
+                                           nk_delta, K, alpha, beta, seed, det, ps, lpt);
   } else {
     if (ldd < 1024 || ldw < 1024) return HARP_EBADARG;
     lda_cgs_kernel<16, DT, XW><<<g, bl, 0, s>>>(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, nwk, ldw, inv_nk,
-                                            nk_delta, K, alpha, beta, seed, det, ps);
+                                            nk_delta, K, alpha, beta, seed, det, ps, lpt);
   }
   return harp_launch_status();
 }
@@ -1047,14 +1121,15 @@ int launch_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_sta
 // variant: 0 = compiler occupancy, 3 = two more waves per SIMD (fewer VGPRs, some spilled)
 static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, void* ndk,
                         int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
-                        float beta, unsigned long long seed, int variant, PsRows ps, hipStream_t s);
+                        float beta, unsigned long long seed, int variant, PsRows ps, const long* lpt, hipStream_t s);
 
 HARP_EXPORT int harp_lda_cgs(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks,
                              void* ndk, int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta,
-                             int K, float alpha, float beta, unsigned long long seed, int variant, hipStream_t s) {
+                             int K, float alpha, float beta, unsigned long long seed, int variant, const long* lpt,
+                             hipStream_t s) {
   const PsRows none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   return lda_cgs_impl(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, ndk_bits, nwk, ldw, inv_nk, nk_delta, K, alpha,
-                      beta, seed, variant, none, s);
+                      beta, seed, variant, none, lpt, s);
 }
 
 // The dense sampler on fused parameter-server rows (PsRows above): pull payload slots in,
@@ -1063,17 +1138,17 @@ HARP_EXPORT int harp_lda_cgs_ps(const int* tdoc, const int* tword, int* tz, cons
                                 void* ndk, int ldd, int ndk_bits, const float* inv_nk, int* nk_delta, int K,
                                 float alpha, float beta, unsigned long long seed, int variant,
                                 const unsigned char* pbuf, const long* poff, const int* pcap, unsigned char* qbuf,
-                                const long* qoff, const int* qcap, int* overflow, hipStream_t s) {
+                                const long* qoff, const int* qcap, int* overflow, const long* lpt, hipStream_t s) {
   if (!pbuf || !poff || !pcap || !qbuf || !qoff || !qcap || !overflow) return HARP_EBADARG;
   const PsRows ps{pbuf, poff, pcap, qbuf, qoff, qcap, overflow};
   int kp = K <= 256 ? 256 : K <= 512 ? 512 : 1024;
   return lda_cgs_impl(tdoc, tword, tz, chunk_start, nchunks, ndk, ldd, ndk_bits, nullptr, kp, inv_nk, nk_delta, K,
-                      alpha, beta, seed, variant, ps, s);
+                      alpha, beta, seed, variant, ps, lpt, s);
 }
 
 static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* chunk_start, long nchunks, void* ndk,
                         int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
-                        float beta, unsigned long long seed, int variant, PsRows ps, hipStream_t s) {
+                        float beta, unsigned long long seed, int variant, PsRows ps, const long* lpt, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
   // variant 0: five waves per SIMD (the default); 3: six (80 VGPRs). The doc-row
   // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
@@ -1083,7 +1158,7 @@ static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* 
   variant &= 0xff;
   if (K <= 0 || K > 1024 || ldw % 4 || (variant != 0 && variant != 3)) return HARP_EBADARG;
 #define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks
-#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, ps, s
+#define CGS_TAIL nwk, ldw, inv_nk, nk_delta, K, alpha, beta, seed, det, ps, lpt, s
   if (ndk_bits == 32) {
     if (ldd % 4) return HARP_EBADARG;
     return variant == 3 ? launch_cgs<int, 1>(CGS_ARGS, (int*)ndk, ldd, CGS_TAIL)
@@ -1295,3 +1370,14 @@ HARP_EXPORT int harp_lda_count(const int* tdoc, const int* tword, const int* tz,
   }
   return harp_launch_status();
 }
+
+#ifdef HARP_LDA_STAMPS
+HARP_EXPORT int harp_lda_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lda_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return HARP_EBADARG;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lda_stamps), z, sizeof(z)) != hipSuccess) return HARP_EBADARG;
+  }
+  return HARP_OK;
+}
+#endif

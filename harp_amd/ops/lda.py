@@ -11,9 +11,10 @@ import torch
 from . import _lib
 
 _lib.register({
+    # ..., seed, variant, lpt (longest-first chunk bounds or null), stream
     "harp_lda_cgs": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int,
                      _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
-                     _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
+                     _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
     # tspan, tword, tz, chunks, nchunks, order, work, tpos, zdoc, nwk, ldw, inv_nk, nk_delta, K, alpha, beta,
     # seed, waves, stream
     "harp_lda_cgs_sparse_span": [_lib.c_void_p] * 4 + [_lib.c_long] + [_lib.c_void_p] * 5 + [
@@ -27,10 +28,10 @@ _lib.register({
         _lib.c_int, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_float,
         _lib.c_float, _lib.c_ulonglong, _lib.c_int, _lib.c_void_p],
     # tdoc, tword, tz, chunks, nchunks, ndk, ldd, ndk_bits, inv_nk, nk_delta, K, alpha, beta, seed, variant,
-    # pull buf / off / cap, push buf / off / cap, overflow, stream
+    # pull buf / off / cap, push buf / off / cap, overflow, lpt, stream
     "harp_lda_cgs_ps": [_lib.c_void_p] * 4 + [_lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p,
                                               _lib.c_void_p, _lib.c_int, _lib.c_float, _lib.c_float, _lib.c_ulonglong,
-                                              _lib.c_int] + [_lib.c_void_p] * 8,
+                                              _lib.c_int] + [_lib.c_void_p] * 9,
     "harp_lda_count": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_long, _lib.c_void_p, _lib.c_int, _lib.c_int,
                        _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
 })
@@ -163,6 +164,28 @@ def chunk_order(chunks: torch.Tensor) -> torch.Tensor:
     return torch.argsort(chunks[1:] - chunks[:-1], descending=True).to(torch.int32)
 
 
+_LPT: dict = {}
+
+
+def lpt_bounds(chunks: torch.Tensor) -> Optional[torch.Tensor]:
+    """The dense sampler's chunk schedule: the (start, end) pairs of ``chunks`` longest first
+    (int64 [2 n]), dealt to the resident waves in snake order by the kernel. Cached per
+    chunk tensor (chunk layouts are static across sweeps). None with HARP_LDA_ORDER=identity
+    (the static word-order stride)."""
+    if os.environ.get("HARP_LDA_ORDER", "lpt") == "identity" or chunks.numel() < 2:
+        return None
+    key = (id(chunks), chunks.data_ptr(), chunks.numel())
+    hit = _LPT.get(key)
+    if hit is not None and hit[0] is chunks:
+        return hit[1]
+    order = torch.argsort(chunks[1:] - chunks[:-1], descending=True)
+    b = torch.stack([chunks[:-1][order], chunks[1:][order]], 1).reshape(-1).contiguous()
+    if len(_LPT) >= 16:
+        _LPT.pop(next(iter(_LPT)))
+    _LPT[key] = (chunks, b)
+    return b
+
+
 DOC_TOPIC_8BIT = os.environ.get("HARP_LDA_NDK8", "1") != "0"
 # sparse sampler without a doc-topic table: per-token doc spans instead of doc ids (one
 # independent load for the next token's doc range instead of ids -> doc_off)
@@ -255,7 +278,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
                                          chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
                                          seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0),
-                                         _lib.stream_ptr(dev))
+                                         _lib.ptr(None if deterministic else lpt_bounds(chunks)), _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
         return delta
     delta = _cpu_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed)
@@ -362,7 +385,7 @@ def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: 
         ndk.stride(0), _bits(ndk), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
         seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0), pull_buf.data_ptr(),
         poff.data_ptr(), pcap.data_ptr(), push_buf.data_ptr(), qoff.data_ptr(), qcap.data_ptr(), overflow.data_ptr(),
-        _lib.stream_ptr(dev))
+        _lib.ptr(None if deterministic else lpt_bounds(chunks)), _lib.stream_ptr(dev))
     _lib.check(st, "lda_cgs_ps")
     return delta
 
