@@ -80,6 +80,14 @@ def synthetic_corpus(n_docs: int, vocab: int, true_topics: int, mean_len: int, s
     return doc, word
 
 
+def _max_doc_len(doc: torch.Tensor, K: int, n_tokens: int) -> Optional[int]:
+    """The corpus's longest document (global doc ids: the same on every worker), when it
+    decides the sampler (ops.lda.use_sparse: K <= 1024 on a big corpus); else None."""
+    if K > 1024 or n_tokens < L.SPARSE_MIN_TOKENS or doc.numel() == 0:
+        return None
+    return int(torch.bincount(doc).max())
+
+
 class LDACollectiveMapper(CollectiveMapper):
     budget = None  # StepBudget when cfg.time_budget_ms > 0
     tuner = None   # BudgetTuner when a [min_bound, max_bound] band is set
@@ -104,7 +112,7 @@ class LDACollectiveMapper(CollectiveMapper):
         # same choice on every worker, by the tokens ONE worker samples (the sparse sampler's
         # per-word setup does not pay at a few tokens per word: 8-GPU share, 12.5M tokens over
         # 1M words, dense 10.0 vs sparse 14.0 ms per sweep, profiles/r4_lda_share)
-        self.sparse = L.use_sparse(K, doc.numel() // P)
+        self.sparse = L.use_sparse(K, doc.numel() // P, _max_doc_len(doc, K, doc.numel() // P))
         self._tokens = None  # the mapper keeps only its own token arrays (int32, word-sorted)
         if P > 1:
             mine = (doc % P) == me
@@ -136,7 +144,7 @@ class LDACollectiveMapper(CollectiveMapper):
         self.chunks = []
         for s in range(ns):
             a, b = self.offsets[s], self.offsets[s + 1]
-            self.chunks.append(L.build_chunks(self.tword[a:b], L.max_chunk(cfg.max_chunk, self.sparse)))
+            self.chunks.append(L.build_chunks(self.tword[a:b], L.max_chunk(cfg.max_chunk, self.sparse, b - a)))
         gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
         self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local) if self.sparse else None
@@ -450,7 +458,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         # same choice on every worker, by the tokens ONE worker samples (the sparse sampler's
         # per-word setup does not pay at a few tokens per word: 8-GPU share, 12.5M tokens over
         # 1M words, dense 10.0 vs sparse 14.0 ms per sweep, profiles/r4_lda_share)
-        self.sparse = L.use_sparse(K, doc.numel() // P)
+        self.sparse = L.use_sparse(K, doc.numel() // P, _max_doc_len(doc, K, doc.numel() // P))
         mine = (doc % P) == me
         doc, word = doc[mine].to(dev), word[mine].to(dev)
         del mine
@@ -478,7 +486,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         order = torch.argsort(lrow, stable=True)  # token order by word id in either layout
         self.tdoc = ldoc[order].contiguous()
         self.tword = lrow[order].to(torch.int32).contiguous()
-        self.chunk_idx = L.build_chunks(self.tword, L.max_chunk(cfg.max_chunk, self.sparse))
+        self.chunk_idx = L.build_chunks(self.tword, L.max_chunk(cfg.max_chunk, self.sparse, self.tword.numel()))
         gz = torch.Generator(device=dev if dev.type == "cuda" else "cpu").manual_seed(cfg.seed * 7 + me)
         self.tz = torch.randint(0, K, (self.tdoc.numel(),), generator=gz, device=dev, dtype=torch.int32)
         self.doc_index = L.DocIndex.build(self.tdoc, self.tz, self.ndoc_local) if self.sparse else None

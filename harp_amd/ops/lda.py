@@ -59,12 +59,21 @@ MAX_TOPICS = 32768      # GPU sparse sampler: the word's qw row in LDS (csrc/lda
 MAX_TOPICS_GPU_HOST = 65535  # GPU workers above MAX_TOPICS: the exact host sampler (uint16 doc-order topics)
 
 
-def use_sparse(K: int, n_tokens: int = 0) -> bool:
+def use_sparse(K: int, n_tokens: int = 0, max_doc_len: Optional[int] = None) -> bool:
+    """Sampler choice (identical on every worker: by the tokens ONE worker samples and the
+    corpus's longest document). auto: the dense sampler for K <= 1024 -- since round 5 (packed
+    uint8 doc rows with the next row prefetched, longest-first chunk schedule, chunks of up to
+    32768 tokens) it is faster AND mixes better per sweep at the full BASELINE #5 size (3.11e9
+    vs 2.63e9 tokens/s, log-likelihood -1.443e9 vs -1.466e9 after 6 sweeps,
+    profiles/r5_lda_chunks) -- except on corpora of >= SPARSE_MIN_TOKENS tokens whose
+    documents reach 256 tokens (no packed uint8 rows: 2-4 KB doc-row reads per token)."""
     if SAMPLER not in ("auto", "dense", "sparse"):
         raise ValueError(f"HARP_LDA_SAMPLER={SAMPLER!r}: expected auto, dense or sparse")
     if K > 1024 or SAMPLER == "sparse":
         return True
-    return SAMPLER == "auto" and n_tokens >= SPARSE_MIN_TOKENS
+    if SAMPLER == "dense" or n_tokens < SPARSE_MIN_TOKENS:
+        return False
+    return max_doc_len is None or max_doc_len >= 256
 
 
 def padded_topics(K: int) -> int:
@@ -145,15 +154,21 @@ def build_chunks(words: torch.Tensor, max_chunk: int = 2048) -> torch.Tensor:
     return torch.cat([b, torch.tensor([n], device=words.device)]).to(torch.int64)
 
 
-def max_chunk(requested: int, sparse: bool) -> int:
-    """Tokens per word chunk: ``requested`` if set, else 2048 for the dense sampler (a
-    wave per chunk: splitting long words balances the waves) and 65536 for the sparse
-    sampler (a workgroup per chunk, longest first: a word split over several workgroups
-    is sampled against several stale copies of its row — measured 1.83e9 vs 1.86e9
-    log-likelihood after 4 iterations at K = 10,000, profiles/r1_lda/sparse)."""
+def max_chunk(requested: int, sparse: bool, n_tokens: int = 0) -> int:
+    """Tokens per word chunk: ``requested`` if set; the sparse sampler 65536 (a workgroup
+    per chunk, longest first: a word split over several workgroups is sampled against
+    several stale copies of its row -- 1.83e9 vs 1.86e9 log-likelihood after 4 iterations
+    at K = 10,000, profiles/r1_lda/sparse); the dense sampler (a wave per chunk, chunks
+    dealt longest first to the resident waves) n_tokens / 3072 within [2048, 32768]: long
+    enough that a frequent word is not sampled against many stale copies of its row (full
+    BASELINE #5 size: 2048 -> 32768 tokens moves the log-likelihood after 6 sweeps from
+    -1.554e9 to -1.443e9 and the sweep from 33.6 to 32.2 ms), short enough that the longest
+    chunk stays within about twice a wave's share of the sweep."""
     if requested:
         return requested
-    return 65536 if sparse else 2048
+    if sparse:
+        return 65536
+    return int(min(32768, max(2048, n_tokens // 3072)))
 
 
 def chunk_order(chunks: torch.Tensor) -> torch.Tensor:

@@ -130,6 +130,12 @@ def test_padded_topics_large_k():
     assert L.padded_topics(1025) == 1152 and L.padded_topics(10000) == 10112
     if L.SAMPLER == "auto":
         assert L.use_sparse(10000) and not L.use_sparse(1000) and L.use_sparse(1000, 10 ** 8)
+        # big corpora: dense while every document fits packed uint8 doc rows
+        assert not L.use_sparse(1000, 10 ** 8, 255) and L.use_sparse(1000, 10 ** 8, 256)
+    # dense chunks: n_tokens / 3072 within [2048, 32768]; sparse 65536; an explicit request wins
+    assert L.max_chunk(0, False, 10 ** 5) == 2048 and L.max_chunk(0, False, 10 ** 8) == 32552
+    assert L.max_chunk(0, False, 10 ** 9) == 32768 and L.max_chunk(0, True, 10 ** 8) == 65536
+    assert L.max_chunk(4096, False, 10 ** 8) == 4096
     # no K limit: past the GPU kernel's LDS row the exact host sampler runs
     assert L.padded_topics(20000) == 20096 and L.padded_topics(40000) == 40064
 
