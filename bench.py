@@ -746,12 +746,17 @@ def run(args) -> int:
         comm = Communicator(None, torch.device("cuda", torch.cuda.current_device()))
     if comm.world_size != args.gpus and backend != "gloo":
         raise RuntimeError(f"world size {comm.world_size} != --gpus {args.gpus}")
-    if world > 1:
-        comm.barrier()  # rank 0's (rare) build finishes before any rank loads the library
     # self-diagnosis before any timed record; bounded like the nested records (a guard that
-    # fires prints what exists and exits 124 instead of hanging the node)
+    # fires prints what exists and exits 124 instead of hanging the node). The first barrier
+    # (rank 0's rare build finishes before any rank loads the library) is inside the bound:
+    # it is the first collective of the run.
+    def barrier_and_preflight(a, c, t):
+        if world > 1:
+            c.barrier()
+        return rccl_preflight(a, c, t)
+
     pre = {}
-    _nested(pre, "rccl", rccl_preflight, args.preflight_timeout, args, comm, torch)
+    _nested(pre, "rccl", barrier_and_preflight, args.preflight_timeout, args, comm, torch)
     rec = bench_kmeans(args, comm, torch)
     rec["rccl"] = pre["rccl"]
     if comm.device.type == "cuda":
