@@ -226,3 +226,16 @@ def test_lda_init_past_the_sort_limit(corpus, monkeypatch):
     di = m.doc_index
     assert torch.equal(di.doc_off, ref.doc_index.doc_off)
     assert torch.equal(di.zdoc[di.tpos].int(), m.tz)
+
+
+def test_lpt_bounds_longest_first_and_cached():
+    """The dense sampler's chunk schedule: every chunk's (start, end) once, longest first,
+    cached per chunk tensor; identity order turns it off."""
+    words = torch.tensor([0] * 5 + [1] * 2 + [2] * 9 + [3] * 1 + [4] * 3, dtype=torch.int32)
+    chunks = L.build_chunks(words, 4)
+    b = L.lpt_bounds(chunks)
+    pairs = b.view(-1, 2).tolist()
+    lens = [e - s for s, e in pairs]
+    assert lens == sorted(lens, reverse=True)
+    assert sorted(pairs) == [[int(chunks[i]), int(chunks[i + 1])] for i in range(chunks.numel() - 1)]
+    assert L.lpt_bounds(chunks) is b
