@@ -239,28 +239,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
   unsigned long long st_pro = 0, st_tok = 0, st_fl = 0, st_n = 0, st_t = 0, st_t1 = 0, st_t2 = 0;
   const unsigned long long st_w0 = clock64();
 #endif
-  // lpt (not in det mode): the chunks' (start, end) pairs longest first, dealt to the
-  // resident waves in snake order (round r: wave w takes rank r W + w, or r W + W-1-w on odd
-  // rounds), so every wave gets about the same number of tokens. The static stride over
-  // word order left the waves that drew the longest word chunks running long after the rest.
+  // lpt (not in det mode): chunk descriptors longest first, dealt to the resident waves in
+  // snake order (round r: wave w takes rank r W + w, or r W + W-1-w on odd rounds), so every
+  // wave gets about the same number of tokens (the static stride over word order left the
+  // waves that drew the longest word chunks running long after the rest). A descriptor is 4
+  // int64: start, length | word << 32, the word's pull-slot and push-slot offsets (fused
+  // rows; else 0) -- one scalar load instead of the chain bounds -> word -> slot offsets.
   const bool lptm = lpt != nullptr && !det;
   for (long r = 0;; ++r) {
 #ifdef HARP_LDA_STAMPS
     const unsigned long long st_t0 = clock64();
 #endif
-    long a, b;
+    long a, b, poff_c = 0, qoff_c = 0;
+    int w;
     if (lptm) {
       const long k = r * nwaves + ((r & 1) ? nwaves - 1 - wave_g : wave_g);
       if (k >= nchunks) break;
-      a = lpt[2 * k];
-      b = lpt[2 * k + 1];
+      const long* dk = lpt + 4 * k;
+      a = dk[0];
+      const long lw = dk[1];
+      b = a + (lw & 0xFFFFFFFFL);
+      w = (int)(lw >> 32);
+      poff_c = dk[2];
+      qoff_c = dk[3];
     } else {
       const long c = wave_g + r * nwaves;
       if (c >= nchunks) break;
       a = chunk_start[c];
       b = chunk_start[c + 1];
+      w = tword[a];
+      if (ps.pbuf) {
+        poff_c = ps.poff[w];
+        qoff_c = ps.qoff[w];
+      }
     }
-    const int w = tword[a];
     int* wrow = nwk + (long)w * ldw + k0;
     // the per-word factor qw_t = (n_wt + beta) / (n_t + V beta) in registers; a token then
     // costs ONE multiply-add per topic, p_t = (n_dt + alpha) * qw_t, and only the two topics
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     if (ps.pbuf) {
       // the word row from its pull slot into this wave's LDS row (zero, then scatter)
       int* lrow = &s_nw0[wv][0];
-      const unsigned char* slot = ps.pbuf + ps.poff[w];
+      const unsigned char* slot = ps.pbuf + poff_c;
       const int cap = ps.pcap[w];
 #pragma unroll
       for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
@@ -558,7 +570,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
 #endif
     // flush this chunk's word-row delta
     if (ps.qbuf) {
-      unsigned char* slot = ps.qbuf + ps.qoff[w];
+      unsigned char* slot = ps.qbuf + qoff_c;
       const int cap = ps.qcap[w];
       if (cap < 0) {
 #pragma unroll

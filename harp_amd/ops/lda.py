@@ -182,23 +182,35 @@ def chunk_order(chunks: torch.Tensor) -> torch.Tensor:
 _LPT: dict = {}
 
 
-def lpt_bounds(chunks: torch.Tensor) -> Optional[torch.Tensor]:
-    """The dense sampler's chunk schedule: the (start, end) pairs of ``chunks`` longest first
-    (int64 [2 n]), dealt to the resident waves in snake order by the kernel. Cached per
-    chunk tensor (chunk layouts are static across sweeps). None with HARP_LDA_ORDER=identity
-    (the static word-order stride)."""
+def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[torch.Tensor]:
+    """The dense sampler's chunk schedule: one descriptor per chunk, longest first (int64
+    [n, 4]: start, length | word << 32, the word's pull-slot and push-slot offsets when
+    ``slots`` (fused rows) are given, else 0), dealt to the resident waves in snake order by
+    the kernel. Cached per (chunks, tword, slots) (the layouts are static across sweeps).
+    None with HARP_LDA_ORDER=identity (the static word-order stride)."""
     if os.environ.get("HARP_LDA_ORDER", "lpt") == "identity" or chunks.numel() < 2:
         return None
-    key = (id(chunks), chunks.data_ptr(), chunks.numel())
+    # (a rotation slice passes a new view of the same token array every call: keyed by its
+    # address; the entry keeps the view, so the address cannot be reused while cached)
+    key = (id(chunks), chunks.data_ptr(), chunks.numel(), tword.data_ptr(), tword.numel(),
+           None if slots is None else tuple(x.data_ptr() for x in slots))
     hit = _LPT.get(key)
     if hit is not None and hit[0] is chunks:
         return hit[1]
     order = torch.argsort(chunks[1:] - chunks[:-1], descending=True)
-    b = torch.stack([chunks[:-1][order], chunks[1:][order]], 1).reshape(-1).contiguous()
+    a = chunks[:-1][order]
+    n = chunks[1:][order] - a
+    w = tword[a].long()
+    d = torch.zeros((order.numel(), 4), dtype=torch.int64, device=chunks.device)
+    d[:, 0] = a
+    d[:, 1] = n | (w << 32)
+    if slots is not None:
+        d[:, 2] = slots[0][w]
+        d[:, 3] = slots[2][w]
     if len(_LPT) >= 16:
         _LPT.pop(next(iter(_LPT)))
-    _LPT[key] = (chunks, b)
-    return b
+    _LPT[key] = (chunks, d.contiguous(), tword, slots)
+    return _LPT[key][1]
 
 
 DOC_TOPIC_8BIT = os.environ.get("HARP_LDA_NDK8", "1") != "0"
@@ -293,7 +305,7 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
                                          chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
                                          seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0),
-                                         _lib.ptr(None if deterministic else lpt_bounds(chunks)), _lib.stream_ptr(dev))
+                                         _lib.ptr(None if deterministic else lpt_desc(chunks, tword)), _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
         return delta
     delta = _cpu_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed)
@@ -400,7 +412,7 @@ def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: 
         ndk.stride(0), _bits(ndk), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
         seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0), pull_buf.data_ptr(),
         poff.data_ptr(), pcap.data_ptr(), push_buf.data_ptr(), qoff.data_ptr(), qcap.data_ptr(), overflow.data_ptr(),
-        _lib.ptr(None if deterministic else lpt_bounds(chunks)), _lib.stream_ptr(dev))
+        _lib.ptr(None if deterministic else lpt_desc(chunks, tword, slots)), _lib.stream_ptr(dev))
     _lib.check(st, "lda_cgs_ps")
     return delta
 

@@ -228,14 +228,19 @@ def test_lda_init_past_the_sort_limit(corpus, monkeypatch):
     assert torch.equal(di.zdoc[di.tpos].int(), m.tz)
 
 
-def test_lpt_bounds_longest_first_and_cached():
-    """The dense sampler's chunk schedule: every chunk's (start, end) once, longest first,
-    cached per chunk tensor; identity order turns it off."""
+def test_lpt_desc_longest_first_and_cached():
+    """The dense sampler's chunk schedule: every chunk once, longest first, as (start,
+    length | word << 32, pull-slot offset, push-slot offset); cached per layout."""
     words = torch.tensor([0] * 5 + [1] * 2 + [2] * 9 + [3] * 1 + [4] * 3, dtype=torch.int32)
     chunks = L.build_chunks(words, 4)
-    b = L.lpt_bounds(chunks)
-    pairs = b.view(-1, 2).tolist()
-    lens = [e - s for s, e in pairs]
-    assert lens == sorted(lens, reverse=True)
-    assert sorted(pairs) == [[int(chunks[i]), int(chunks[i + 1])] for i in range(chunks.numel() - 1)]
-    assert L.lpt_bounds(chunks) is b
+    poff = torch.arange(5, dtype=torch.int64) * 100
+    qoff = torch.arange(5, dtype=torch.int64) * 1000
+    cap = torch.zeros(5, dtype=torch.int32)
+    d = L.lpt_desc(chunks, words, (poff, cap, qoff, cap))
+    a, ln, w = d[:, 0], d[:, 1] & 0xFFFFFFFF, d[:, 1] >> 32
+    assert ln.tolist() == sorted(ln.tolist(), reverse=True)
+    assert sorted(zip(a.tolist(), (a + ln).tolist())) == [(int(chunks[i]), int(chunks[i + 1]))
+                                                          for i in range(chunks.numel() - 1)]
+    assert torch.equal(w, words[a].long()) and torch.equal(d[:, 2], w * 100) and torch.equal(d[:, 3], w * 1000)
+    assert L.lpt_desc(chunks, words, (poff, cap, qoff, cap)) is d
+    assert L.lpt_desc(chunks, words)[:, 2:].abs().sum() == 0
