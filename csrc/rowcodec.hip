@@ -42,6 +42,18 @@ __device__ __forceinline__ void load_row(int* lrow, const int* __restrict__ g, i
   for (int c = lane; c < K / 4; c += 64) l4[c] = g4[c];
 }
 
+// narrow global tables (uint16 counts, parameter-server owners whose words all have fewer
+// than 65536 tokens): half the bytes of the pull encode's row reads (K % 8 == 0)
+__device__ __forceinline__ void load_row(int* lrow, const unsigned short* __restrict__ g, int K, int lane) {
+  const uint4* g8 = (const uint4*)g;
+  int4* l4 = (int4*)lrow;
+  for (int c = lane; c < K / 8; c += 64) {
+    const uint4 v = g8[c];
+    l4[2 * c] = make_int4((int)(v.x & 0xFFFFu), (int)(v.x >> 16), (int)(v.y & 0xFFFFu), (int)(v.y >> 16));
+    l4[2 * c + 1] = make_int4((int)(v.z & 0xFFFFu), (int)(v.z >> 16), (int)(v.w & 0xFFFFu), (int)(v.w >> 16));
+  }
+}
+
 // subtract a slot (dense or sparse) from the LDS row
 __device__ __forceinline__ void sub_slot(int* lrow, const unsigned char* slot, int cap, int K, int lane) {
   if (cap < 0) {
@@ -98,9 +110,9 @@ __device__ __forceinline__ void store_slot(const int* lrow, unsigned char* slot,
   if (__ballot(over) && lane == 0) overflow[0] = 1;
 }
 
-template <bool kDelta>
+template <bool kDelta, class ST = int>
 __global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_encode_kernel(
-    const int* __restrict__ src, long ld, int K, const int* __restrict__ rows, int n,
+    const ST* __restrict__ src, long ld, int K, const int* __restrict__ rows, int n,
     const long* __restrict__ slot_off, const int* __restrict__ cap, unsigned char* __restrict__ out,
     const unsigned char* __restrict__ before, const long* __restrict__ b_off, const int* __restrict__ b_cap,
     int* __restrict__ overflow) {
@@ -177,6 +189,44 @@ __global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_decode_add_kernel(
   }
 }
 
+// add a slot into a narrow (uint16) row: one 32-bit atomic on the dword holding the count,
+// +v or -(-v) in its half. Counts stay in [0, 65535] (every count is at most its word's
+// token total, < 65536 for a narrow table, and a requester's decrements never exceed its
+// own tokens counted in the row), so neither half ever carries or borrows into the other.
+__device__ __forceinline__ void add16(unsigned short* row, int t, int v) {
+  unsigned* word = (unsigned*)(row + (t & ~1));
+  const unsigned sh = (t & 1) ? 16u : 0u;
+  if (v > 0) atomicAdd(word, (unsigned)v << sh);
+  else atomicSub(word, (unsigned)(-v) << sh);
+}
+
+__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_decode_add16_kernel(
+    unsigned short* __restrict__ dst, long ld, int K, const int* __restrict__ rows, int n,
+    const long* __restrict__ slot_off, const int* __restrict__ cap, const unsigned char* __restrict__ in) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = blockIdx.x * (blockDim.x >> 6) + w;
+  if (j >= n) return;
+  unsigned short* d = dst + (long)rows[j] * ld;
+  const int c = cap[j];
+  const unsigned char* slot = in + slot_off[j];
+  if (c < 0) {
+    const int* s = (const int*)slot;
+    for (int t = lane; t < K; t += 64) {
+      const int v = s[t];
+      if (v) add16(d, t, v);
+    }
+    return;
+  }
+  int nnz = *(const int*)slot;
+  nnz = nnz < 0 ? 0 : (nnz > c ? c : nnz);
+  const int* cnt = slot_counts(slot);
+  const unsigned short* top = slot_topics(slot, c);
+  for (int e = lane; e < nnz; e += 64) {
+    const int t = top[e], v = cnt[e];
+    if (v && t < K) add16(d, t, v);
+  }
+}
+
 inline bool bad_shape(long ld, int K) { return K <= 0 || (K & 3) || ld < K || (ld & 3) || 4L * K > kLdsBudget; }
 // waves (rows) per workgroup so that the LDS rows fit the default dynamic-LDS limit
 inline int waves_for(int K) {
@@ -223,5 +273,30 @@ HARP_EXPORT int harp_rowcodec_decode(int* dst, long ld, int K, const int* rows, 
   } else {
     rowcodec_decode_add_kernel<<<grid, block, 0, s>>>(dst, ld, K, rows, n, slot_off, cap, (const unsigned char*)in);
   }
+  return harp_launch_status();
+}
+
+// narrow (uint16) global tables: encode from, and add slots into, rows of K uint16 counts
+// at stride ld (K % 8 == 0, ld % 8 == 0)
+HARP_EXPORT int harp_rowcodec_encode16(const unsigned short* src, long ld, int K, const int* rows, int n,
+                                       const long* slot_off, const int* cap, void* out, int* overflow, hipStream_t s) {
+  if (n < 0 || bad_shape(ld, K) || (K & 7) || (ld & 7) || misaligned(src) || misaligned(out) || !overflow)
+    return HARP_EBADARG;
+  if (n == 0) return HARP_OK;
+  const int wv = waves_for(K);
+  const size_t lds = sizeof(int) * (size_t)K * wv;
+  const dim3 grid((n + wv - 1) / wv), block(wv * 64);
+  rowcodec_encode_kernel<false, unsigned short><<<grid, block, lds, s>>>(
+      src, ld, K, rows, n, slot_off, cap, (unsigned char*)out, nullptr, nullptr, nullptr, overflow);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_rowcodec_decode_add16(unsigned short* dst, long ld, int K, const int* rows, int n,
+                                           const long* slot_off, const int* cap, const void* in, hipStream_t s) {
+  if (n < 0 || bad_shape(ld, K) || (K & 7) || (ld & 7) || misaligned(dst) || misaligned(in)) return HARP_EBADARG;
+  if (n == 0) return HARP_OK;
+  const int wv = waves_for(K);
+  const dim3 grid((n + wv - 1) / wv), block(wv * 64);
+  rowcodec_decode_add16_kernel<<<grid, block, 0, s>>>(dst, ld, K, rows, n, slot_off, cap, (const unsigned char*)in);
   return harp_launch_status();
 }

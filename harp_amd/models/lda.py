@@ -16,6 +16,7 @@ the next slice's sampling; topic-sum deltas are allreduced once per iteration.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
@@ -23,6 +24,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from ..ops import lda as L
+from ..ops import rowcodec as RC
 from ..runtime.dymoro import BudgetTuner, DeviceRotator, RotationSchedule, StepBudget, ring_strides
 from ..runtime.mapper import CollectiveMapper, Context, KeyValReader
 from ..ops.sorting import SORT_CHUNK, argsort_small_keys
@@ -459,6 +461,10 @@ class LDAPushPullMapper(LDACollectiveMapper):
         # per-word setup does not pay at a few tokens per word: 8-GPU share, 12.5M tokens over
         # 1M words, dense 10.0 vs sparse 14.0 ms per sweep, profiles/r4_lda_share)
         self.sparse = L.use_sparse(K, doc.numel() // P, _max_doc_len(doc, K, doc.numel() // P))
+        # narrow (uint16) owner table when no word has 65536 tokens (global counts: the same
+        # decision on every worker): half the bytes of every pull encode
+        self.narrow = (dev.type == "cuda" and cfg.sparse_comm != "off" and os.environ.get("HARP_LDA_NARROW", "1") != "0"
+                       and word.numel() > 0 and RC.narrow_ok(int(torch.bincount(word).max())))
         mine = (doc % P) == me
         doc, word = doc[mine].to(dev), word[mine].to(dev)
         del mine
@@ -502,7 +508,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
         nneed = len(self.need)
         if self.ps is not None:
             self.pull_buf = slab
-            gbuf = torch.zeros((len(owned), B, self.Kp), dtype=torch.int32, device=dev)
+            gdt = torch.int16 if self.narrow and self.Kp % 8 == 0 else torch.int32
+            gbuf = torch.zeros((len(owned), B, self.Kp), dtype=gdt, device=dev)
             self.glob = PackedTable(owned, gbuf, table_id=1, combiner=self.sum)
             self.glob.static_layout = True
             self.before = self.want_pt = None
@@ -665,7 +672,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
             self.comm.all_reduce(rebuilt)
         ok = bool(torch.equal(rebuilt.sum((0, 1)).round().to(torch.int32), self.nk))
         for b in self.glob.sorted_ids():
-            ok = ok and bool(torch.equal(rebuilt[b].round().to(torch.int32), self.glob[b]))
+            ok = ok and bool(torch.equal(rebuilt[b].round().to(torch.int32), RC.widen(self.glob[b])))
         flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=self.device)
         if P > 1:
             self.comm.all_reduce(flag)
@@ -676,7 +683,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         K = cfg.num_topics
         wp = torch.zeros(2, dtype=torch.float64, device=self.device)
         for p in self.glob.get_partitions():  # each block counted once, at its owner
-            wp += L.loglik_terms(p.get(), cfg.beta, K)
+            wp += L.loglik_terms(RC.widen(p.get()), cfg.beta, K)
         dp = self._doc_loglik()
         tot = reduce_partials(self.comm, {"w": wp[:1], "d": dp})
         nk = self.nk[:K].double()
@@ -709,7 +716,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
             tabs["ndk"] = blob_table(self.ndk)
         ids = self.glob.sorted_ids()
         if ids:
-            tabs["glob"] = tensor_table(torch.stack([self.glob[b] for b in ids]), ids)
+            tabs["glob"] = tensor_table(torch.stack([RC.widen(self.glob[b]) for b in ids]), ids)
         return tabs
 
     def resume(self) -> int:
@@ -721,7 +728,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         if "glob" in tabs:
             g = tabs["glob"]
             for j, b in enumerate(g.ids):
-                self.glob[b].copy_(g.buffer[j].to(self.device))
+                self.glob[b].copy_(g.buffer[j].to(self.device))  # (into a narrow table: uint16 bit patterns)
         return it
 
     def print_word_model(self, folder: str, next_it: int = 0) -> str:
@@ -733,7 +740,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
             lo = b * self.B
             n = max(0, min(self.B, self.vocab - lo))
             ids.append(torch.arange(lo, lo + n))
-            rows.append(self.glob[b][:n])
+            rows.append(RC.widen(self.glob[b][:n]))
         if not ids:
             ids, rows = [torch.zeros(0, dtype=torch.long)], [torch.zeros((0, self.Kp), dtype=torch.int32)]
         return write_topic_counts(f"{folder}/{self.get_self_id()}", torch.cat(ids), torch.cat(rows).cpu(),

@@ -26,6 +26,11 @@ _lib.register({
                              _lib.c_void_p],
     "harp_rowcodec_decode": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
                              _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p],
+    # narrow (uint16 counts held in int16) global tables: encode from / add slots into
+    "harp_rowcodec_encode16": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                               _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    "harp_rowcodec_decode_add16": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                                   _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
 })
 
 ALIGN = 16
@@ -52,11 +57,25 @@ def layout(caps: torch.Tensor, K: int, base: int = 0) -> Tuple[torch.Tensor, int
     return off, int(sz.sum().item())
 
 
-def _check_args(t: torch.Tensor, K: int) -> None:
-    if t.dtype != torch.int32 or t.dim() != 2 or t.shape[1] < K or t.stride(1) != 1:
+def _check_args(t: torch.Tensor, K: int, narrow_ok: bool = False) -> None:
+    ok = t.dtype == torch.int32 or (narrow_ok and t.dtype == torch.int16)
+    if not ok or t.dim() != 2 or t.shape[1] < K or t.stride(1) != 1:
         raise ValueError(f"rowcodec needs an int32 [rows, >=K] table, got {tuple(t.shape)} {t.dtype}")
-    if K <= 0 or K % 4 or K > MAX_K:
-        raise ValueError(f"rowcodec needs 0 < K <= {MAX_K}, K % 4 == 0 (got {K})")
+    if K <= 0 or K % 4 or K > MAX_K or (t.dtype == torch.int16 and (K % 8 or t.stride(0) % 8)):
+        raise ValueError(f"rowcodec needs 0 < K <= {MAX_K}, K % 4 == 0 (K % 8 and a row stride % 8 for a "
+                         f"narrow table; got K={K})")
+
+
+def narrow_ok(max_count: int) -> bool:
+    """A global count table may be narrow (uint16 counts stored in int16: half the bytes of
+    every pull encode) when no count can reach 65536 -- every count of a word row is at
+    most the word's token total."""
+    return max_count < 65536
+
+
+def widen(t: torch.Tensor) -> torch.Tensor:
+    """int32 counts of a table (narrow int16 tables hold uint16 counts)."""
+    return t.to(torch.int32) & 0xFFFF if t.dtype == torch.int16 else t
 
 
 def _dense_rows(buf: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, K: int) -> torch.Tensor:
@@ -94,11 +113,23 @@ def encode(src: torch.Tensor, K: int, rows: torch.Tensor, off: torch.Tensor, cap
     """Slot j of ``out`` := row ``src[rows[j], :K]`` (minus the row decoded from slot j of
     ``before`` when given: a count delta against the pulled snapshot). Entries past a
     slot's capacity are dropped and flag ``overflow``. ``rows`` int32, ``off`` int64
-    byte offsets, ``cap`` int32 (-1 = dense slot)."""
-    _check_args(src, K)
+    byte offsets, ``cap`` int32 (-1 = dense slot). ``src`` may be a narrow table (int16
+    holding uint16 counts; no ``before``)."""
+    _check_args(src, K, narrow_ok=before is None)
     n = rows.numel()
     if n == 0:
         return out
+    if src.dtype == torch.int16 and _lib.use_native(src):
+        for t in (rows, off, cap, out, overflow):
+            assert t.device == src.device and t.is_contiguous()
+        assert rows.dtype == torch.int32 and off.dtype == torch.int64 and cap.dtype == torch.int32
+        st = _lib.kernels().harp_rowcodec_encode16(
+            src.data_ptr(), src.stride(0), K, rows.data_ptr(), n, off.data_ptr(), cap.data_ptr(), out.data_ptr(),
+            overflow.data_ptr(), _lib.stream_ptr(src.device))
+        _lib.check(st, "rowcodec_encode16")
+        return out
+    if src.dtype == torch.int16:  # CPU oracle of the narrow table
+        src = widen(src)
     if _lib.use_native(src):
         for t in (rows, off, cap, out, overflow) + ((before, b_off, b_cap) if before is not None else ()):
             assert t.device == src.device and t.is_contiguous()
@@ -140,10 +171,25 @@ def encode(src: torch.Tensor, K: int, rows: torch.Tensor, off: torch.Tensor, cap
 def decode(dst: torch.Tensor, K: int, rows: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, inp: torch.Tensor,
            add: bool = False) -> torch.Tensor:
     """Row ``dst[rows[j], :K]`` := slot j of ``inp`` (``add``: += instead; rows may repeat
-    and then all add)."""
-    _check_args(dst, K)
+    and then all add). ``dst`` may be a narrow table (int16 holding uint16 counts) when
+    ``add``."""
+    _check_args(dst, K, narrow_ok=add)
     n = rows.numel()
     if n == 0:
+        return dst
+    if dst.dtype == torch.int16:
+        if _lib.use_native(dst):
+            for t in (rows, off, cap, inp):
+                assert t.device == dst.device and t.is_contiguous()
+            assert rows.dtype == torch.int32 and off.dtype == torch.int64 and cap.dtype == torch.int32
+            st = _lib.kernels().harp_rowcodec_decode_add16(dst.data_ptr(), dst.stride(0), K, rows.data_ptr(), n,
+                                                           off.data_ptr(), cap.data_ptr(), inp.data_ptr(),
+                                                           _lib.stream_ptr(dst.device))
+            _lib.check(st, "rowcodec_decode_add16")
+            return dst
+        vals = _dense_rows(inp, off.long(), cap.long(), K)
+        wide = widen(dst[:, :K]).index_add_(0, rows.long(), vals)
+        dst[:, :K] = wide.to(torch.int16)  # two's complement: uint16 counts round-trip
         return dst
     if _lib.use_native(dst):
         for t in (rows, off, cap, inp):

@@ -49,6 +49,48 @@ def test_rowcodec_matches_oracle(cuda, K):
     assert torch.equal(RC._dense_rows(gb, off, c.long(), K), RC._dense_rows(cb, off, c.long(), K))
 
 
+@pytest.mark.parametrize("K", [256, 1024])
+def test_rowcodec_narrow_table_gpu(cuda, K):
+    """Narrow (uint16 counts in int16) owner tables: the encode of a narrow table writes the
+    same payload bytes as the encode of its int32 copy, and adding slots into it (counts up
+    to 65535, decrements included) leaves the int32 result (the LDA push-pull owner table
+    with every word under 65536 tokens)."""
+    g = torch.Generator().manual_seed(7 + K)
+    n = 2000
+    src = torch.zeros((n, K), dtype=torch.int32)
+    for r in range(n):
+        k = int(torch.randint(0, K // 3, (1,), generator=g))
+        if k:
+            src[r, torch.randperm(K, generator=g)[:k]] = torch.randint(1, 65535, (k,), generator=g, dtype=torch.int32)
+    caps = RC.slot_caps(torch.full((n,), K // 3), K).to(torch.int32)
+    rows = torch.randperm(n, generator=g).to(torch.int32)
+    c = caps[rows.long()].contiguous()
+    off, nb = RC.layout(c.long(), K)
+    bufs = []
+    for t in (src, src.to(torch.int16)):
+        buf = torch.zeros(nb, dtype=torch.uint8, device=cuda)
+        ov = torch.zeros(1, dtype=torch.int32, device=cuda)
+        RC.encode(t.to(cuda), K, rows.to(cuda), off.to(cuda), c.to(cuda), buf, ov)
+        assert int(ov) == 0
+        bufs.append(buf)
+    assert torch.equal(bufs[0], bufs[1])
+    # add a delta payload: -min(count, 3) on present topics, +k on absent ones (stays < 65536)
+    delta = torch.where(src > 0, -torch.clamp(src, max=3), torch.zeros_like(src))
+    delta[::5, 1] += 17
+    delta = torch.where(src + delta > 65535, torch.zeros_like(delta), delta)
+    dcaps = RC.slot_caps((delta != 0).sum(1) + 2, K).to(torch.int32)[rows.long()].contiguous()  # sparse + dense
+    doff, dnb = RC.layout(dcaps.long(), K)
+    dbuf = torch.zeros(dnb, dtype=torch.uint8, device=cuda)
+    ov = torch.zeros(1, dtype=torch.int32, device=cuda)
+    RC.encode(delta.to(cuda), K, rows.to(cuda), doff.to(cuda), dcaps.to(cuda), dbuf, ov)
+    wide, narrow = src.to(cuda), src.to(torch.int16).to(cuda)
+    RC.decode(wide, K, rows.to(cuda), doff.to(cuda), dcaps.to(cuda), dbuf, add=True)
+    RC.decode(narrow, K, rows.to(cuda), doff.to(cuda), dcaps.to(cuda), dbuf, add=True)
+    torch.cuda.synchronize()
+    assert torch.equal(RC.widen(narrow), wide)
+    assert torch.equal(wide.cpu(), src + delta)
+
+
 def test_rowcodec_overflow_flag_gpu(cuda):
     K = 256
     src = torch.ones((10, K), dtype=torch.int32, device=cuda)
