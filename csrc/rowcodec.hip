@@ -16,7 +16,8 @@
 //
 // One wave per row (up to 4 per workgroup, fewer for K > 4096 so the LDS rows stay
 // within 64 KB; K <= 16384), the row staged once in LDS (4 KB at K = 1024):
-//   encode        : global row -> LDS -> ballot compaction into the slot          (1 read)
+//   encode        : global row -> lanes (16 consecutive topics each) -> one wave scan
+//                   places the nonzeros into the slot in column order              (1 read)
 //   encode_delta  : LDS = row - "before" (the row's slot of the PULL payload it was
 //                   decoded from: the pull payload doubles as the snapshot)         (1 read)
 //   decode_replace: LDS = 0, scatter slot entries, LDS -> row                      (1 write)
@@ -40,18 +41,6 @@ __device__ __forceinline__ void load_row(int* lrow, const int* __restrict__ g, i
   const int4* g4 = (const int4*)g;
   int4* l4 = (int4*)lrow;
   for (int c = lane; c < K / 4; c += 64) l4[c] = g4[c];
-}
-
-// narrow global tables (uint16 counts, parameter-server owners whose words all have fewer
-// than 65536 tokens): half the bytes of the pull encode's row reads (K % 8 == 0)
-__device__ __forceinline__ void load_row(int* lrow, const unsigned short* __restrict__ g, int K, int lane) {
-  const uint4* g8 = (const uint4*)g;
-  int4* l4 = (int4*)lrow;
-  for (int c = lane; c < K / 8; c += 64) {
-    const uint4 v = g8[c];
-    l4[2 * c] = make_int4((int)(v.x & 0xFFFFu), (int)(v.x >> 16), (int)(v.y & 0xFFFFu), (int)(v.y >> 16));
-    l4[2 * c + 1] = make_int4((int)(v.z & 0xFFFFu), (int)(v.z >> 16), (int)(v.w & 0xFFFFu), (int)(v.w >> 16));
-  }
 }
 
 // subtract a slot (dense or sparse) from the LDS row
@@ -110,9 +99,89 @@ __device__ __forceinline__ void store_slot(const int* lrow, unsigned char* slot,
   if (__ballot(over) && lane == 0) overflow[0] = 1;
 }
 
-template <bool kDelta, class ST = int>
-__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_encode_kernel(
+// 16 consecutive counts of a row (t0 % 16 == 0; zero past K, K % 4 == 0)
+__device__ __forceinline__ void load16(const int* __restrict__ g, int t0, int K, int (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = t0 + 4 * q;
+    const int4 x = t < K ? *(const int4*)(g + t) : make_int4(0, 0, 0, 0);
+    v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+  }
+}
+__device__ __forceinline__ void load16(const unsigned short* __restrict__ g, int t0, int K, int (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // K % 8 == 0 for narrow rows
+    const int t = t0 + 8 * q;
+    const uint4 x = t < K ? *(const uint4*)(g + t) : make_uint4(0u, 0u, 0u, 0u);
+    const unsigned w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[8 * q + 2 * k] = (int)(w4[k] & 0xFFFFu);
+      v[8 * q + 2 * k + 1] = (int)(w4[k] >> 16);
+    }
+  }
+}
+
+// Plain encode (no delta) without LDS staging: lane L takes topics [16 L, 16 L + 16) of each
+// 1024-topic stretch straight from the row, one wave scan of the lanes' nonzero counts
+// places them, so the slot is written in column order as before (the staged form made 16
+// ballot passes over an LDS copy of the row: the pull encode of the LDA push-pull).
+template <class ST>
+__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_encode_direct_kernel(
     const ST* __restrict__ src, long ld, int K, const int* __restrict__ rows, int n,
+    const long* __restrict__ slot_off, const int* __restrict__ cap, unsigned char* __restrict__ out,
+    int* __restrict__ overflow) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = blockIdx.x * (blockDim.x >> 6) + w;
+  if (j >= n) return;  // the whole wave
+  const ST* g = src + (long)rows[j] * ld;
+  unsigned char* slot = out + slot_off[j];
+  const int c = cap[j];
+  if (c < 0) {  // dense slot: the row as int32
+    int4* s4 = (int4*)slot;
+    for (int t0 = 16 * lane; t0 < K; t0 += 1024) {
+      int v[16];
+      load16(g, t0, K, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (t0 + 4 * q < K) s4[(t0 >> 2) + q] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+    return;
+  }
+  int* cnt = (int*)(slot + 4);
+  unsigned short* top = (unsigned short*)(slot + 4 + 4 * (long)c);
+  int base = 0;
+  bool over = false;
+  for (int s0 = 0; s0 < K; s0 += 1024) {
+    const int t0 = s0 + 16 * lane;
+    int v[16];
+    load16(g, t0, K, v);
+    int mine = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) mine += v[e] != 0 ? 1 : 0;
+    const float incl = wave_scan_incl((float)mine);  // <= 1024: exact
+    int pos = base + (int)incl - mine;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if (v[e] != 0) {
+        if (pos < c) {
+          cnt[pos] = v[e];
+          top[pos] = (unsigned short)(t0 + e);
+        } else {
+          over = true;
+        }
+        ++pos;
+      }
+    }
+    base += (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+  }
+  if (lane == 0) *(int*)slot = base < c ? base : c;
+  if (__ballot(over) && lane == 0) overflow[0] = 1;
+}
+
+template <bool kDelta>
+__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_encode_kernel(
+    const int* __restrict__ src, long ld, int K, const int* __restrict__ rows, int n,
     const long* __restrict__ slot_off, const int* __restrict__ cap, unsigned char* __restrict__ out,
     const unsigned char* __restrict__ before, const long* __restrict__ b_off, const int* __restrict__ b_cap,
     int* __restrict__ overflow) {
@@ -253,9 +322,8 @@ HARP_EXPORT int harp_rowcodec_encode(const int* src, long ld, int K, const int* 
                                                                   (unsigned char*)out, (const unsigned char*)before,
                                                                   b_off, b_cap, overflow);
   } else {
-    rowcodec_encode_kernel<false><<<grid, block, lds, s>>>(src, ld, K, rows, n, slot_off, cap,
-                                                                   (unsigned char*)out, nullptr, nullptr, nullptr,
-                                                                   overflow);
+    rowcodec_encode_direct_kernel<int><<<dim3((n + kMaxWaves - 1) / kMaxWaves), dim3(kMaxWaves * 64), 0, s>>>(
+        src, ld, K, rows, n, slot_off, cap, (unsigned char*)out, overflow);
   }
   return harp_launch_status();
 }
@@ -283,11 +351,8 @@ HARP_EXPORT int harp_rowcodec_encode16(const unsigned short* src, long ld, int K
   if (n < 0 || bad_shape(ld, K) || (K & 7) || (ld & 7) || misaligned(src) || misaligned(out) || !overflow)
     return HARP_EBADARG;
   if (n == 0) return HARP_OK;
-  const int wv = waves_for(K);
-  const size_t lds = sizeof(int) * (size_t)K * wv;
-  const dim3 grid((n + wv - 1) / wv), block(wv * 64);
-  rowcodec_encode_kernel<false, unsigned short><<<grid, block, lds, s>>>(
-      src, ld, K, rows, n, slot_off, cap, (unsigned char*)out, nullptr, nullptr, nullptr, overflow);
+  rowcodec_encode_direct_kernel<unsigned short><<<dim3((n + kMaxWaves - 1) / kMaxWaves), dim3(kMaxWaves * 64), 0, s>>>(
+      src, ld, K, rows, n, slot_off, cap, (unsigned char*)out, overflow);
   return harp_launch_status();
 }
 
