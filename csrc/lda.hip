@@ -208,7 +208,7 @@ struct PsRows {
 // (0.90e9 vs 1.17e9 tokens/s at K = 1000, profiles/r1_lda/ldapf: its extra VGPRs cost a
 // wave per SIMD) and was removed.
 template <int TPL, class DT, int XW = 0>  // topics per lane; K_pad = 64 * TPL
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 ? 5 + XW : 8, 8))) void lda_cgs_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 ? 6 + XW : 8, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, DT* __restrict__ ndk, int ldd, int* __restrict__ nwk, int ldw,
     const float* __restrict__ inv_nk, int* __restrict__ nk_delta, int K, float alpha, float beta,
@@ -216,12 +216,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
   constexpr int KP = 64 * TPL;
   constexpr int WAVES = 4;
   constexpr bool PK = sizeof(DT) == 1 && TPL == 16;  // packed-row token loop (below)
-  __shared__ float s_inv[KP];
   __shared__ int s_delta[KP];
   __shared__ int s_nw0[WAVES][KP];  // per wave: the pulled word row, then the chunk's moves
   __shared__ float4 s_x[WAVES][TPL / 2];  // the drawn lane's doc counts + qw (topic walk)
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
-    s_inv[k] = k < K ? inv_nk[k] : 0.f;
     s_delta[k] = 0;
   }
   __syncthreads();
@@ -324,7 +322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
     float qs = 0.f;  // sum of this lane's qw: the token's mass is alpha * qs + sum n_dt qw_t
 #pragma unroll
     for (int t = 0; t < TPL; ++t) {
-      qw[t] = (qw[t] + beta) * s_inv[k0 + t];
+      qw[t] = (qw[t] + beta) * inv_nk[k0 + t];  // (inv_nk holds K_pad entries, 0 past K)
       qs += qw[t];
     }
 #pragma unroll
@@ -391,7 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
         // correction -qw_z (after qw_z's own update) on lane z / TPL, and the walk below
         // takes 1 off topic z when it reads that lane's row
         const int zl = z / TPL, zt = z % TPL;
-        const float inv_z = s_inv[z];
+        const float inv_z = inv_nk[z];
         const bool mez = lane == zl;
         float s;
         {
@@ -435,7 +433,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
         int nz = src * TPL + found;
         if (nz >= K) nz = K - 1;
         const int nzl = nz / TPL, nzt = nz % TPL;
-        const float inv_nz = s_inv[nz];
+        const float inv_nz = inv_nk[nz];
         {
           const bool me = lane == nzl;
           const float qv = qw[nzt];
@@ -493,7 +491,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
         // "if (t == zt)" was if-converted into selects over all TPL registers: ~5 VALU per
         // topic per update, most of the token's VALU work)
         const int zl = z / TPL, zt = z % TPL;
-        const float inv_z = s_inv[z];
+        const float inv_z = inv_nk[z];
         {
           const bool me = lane == zl;
           const float dv = nd[zt], qv = qw[zt];
@@ -541,7 +539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5 + XW < 8 
         if (nz >= K) nz = K - 1;
         // add the token back with its new topic (uniform slot: dynamic register indexing)
         const int nzl = nz / TPL, nzt = nz % TPL;
-        const float inv_nz = s_inv[nz];
+        const float inv_nz = inv_nk[nz];
         {
           const bool me = lane == nzl;
           const float qv = qw[nzt];
@@ -1162,7 +1160,7 @@ static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* 
                         int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
                         float beta, unsigned long long seed, int variant, PsRows ps, const long* lpt, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  // variant 0: five waves per SIMD (the default); 3: six (80 VGPRs). The doc-row
+  // variant 0: six waves per SIMD; 3: seven (the default). The doc-row
   // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
   // (profiles/r1_lda/occupancy) and are no longer built.
   // variant | 0x100: deterministic one-wave sampling (tests)

@@ -37,10 +37,10 @@ _lib.register({
 })
 
 
-# csrc/lda.hip harp_lda_cgs variants: 0 = five waves per SIMD, 3 = six (the default). Since
-# the round-5 LDS topic walk and linear qw updates the six-wave build fits 80 VGPRs with two
-# spilled in the chunk prologue only: 8-share sweep 8.72 -> 8.06 ms, full size dense 48.2 ->
-# 43.2 ms (profiles/r5_lda_waves). More resident waves hide the per-token doc-row fetch.
+# csrc/lda.hip harp_lda_cgs variants: 0 = six waves per SIMD, 3 = seven (the default: 67
+# VGPRs and 20.5 KB of LDS per workgroup since the inverse topic sums are read from global
+# memory; 8-share 5.44 -> 5.33 ms, profiles/r5_lda_waves7). More resident waves hide the
+# per-token doc-row fetch (round 5 before: five -> six waves, 8.72 -> 8.06 ms).
 SAMPLER_VARIANT = int(os.environ.get("HARP_LDA_VARIANT", "3"))
 
 
