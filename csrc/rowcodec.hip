@@ -296,6 +296,37 @@ __global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_decode_add16_kernel(
   }
 }
 
+// slot j of `out` := slot src_off[j] of `in` (same capacity): the owner's pull sends every
+// requester of a row the same slot, so the row is encoded once and its slot copied -- only
+// the header and the used entries of a sparse slot
+__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_copy_slots_kernel(
+    const unsigned char* __restrict__ in, const long* __restrict__ src_off, unsigned char* __restrict__ out,
+    const long* __restrict__ dst_off, const int* __restrict__ cap, int n, int K) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = blockIdx.x * (blockDim.x >> 6) + w;
+  if (j >= n) return;
+  const unsigned char* a = in + src_off[j];
+  unsigned char* d = out + dst_off[j];
+  const int c = cap[j];
+  if (c < 0) {
+    const int4* a4 = (const int4*)a;
+    int4* d4 = (int4*)d;
+    for (int q = lane; q < K / 4; q += 64) d4[q] = a4[q];
+    return;
+  }
+  int nnz = *(const int*)a;
+  nnz = nnz < 0 ? 0 : (nnz > c ? c : nnz);
+  if (lane == 0) *(int*)d = nnz;
+  const int* ac = slot_counts(a);
+  int* dc = (int*)(d + 4);
+  const unsigned short* at = slot_topics(a, c);
+  unsigned short* dt = (unsigned short*)(d + 4 + 4 * (long)c);
+  for (int e = lane; e < nnz; e += 64) {
+    dc[e] = ac[e];
+    dt[e] = at[e];
+  }
+}
+
 inline bool bad_shape(long ld, int K) { return K <= 0 || (K & 3) || ld < K || (ld & 3) || 4L * K > kLdsBudget; }
 // waves (rows) per workgroup so that the LDS rows fit the default dynamic-LDS limit
 inline int waves_for(int K) {
@@ -363,5 +394,14 @@ HARP_EXPORT int harp_rowcodec_decode_add16(unsigned short* dst, long ld, int K, 
   const int wv = waves_for(K);
   const dim3 grid((n + wv - 1) / wv), block(wv * 64);
   rowcodec_decode_add16_kernel<<<grid, block, 0, s>>>(dst, ld, K, rows, n, slot_off, cap, (const unsigned char*)in);
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_rowcodec_copy_slots(const void* in, const long* src_off, void* out, const long* dst_off,
+                                         const int* cap, int n, int K, hipStream_t s) {
+  if (n < 0 || K <= 0 || (K & 3) || misaligned(in) || misaligned(out)) return HARP_EBADARG;
+  if (n == 0) return HARP_OK;
+  rowcodec_copy_slots_kernel<<<dim3((n + kMaxWaves - 1) / kMaxWaves), dim3(kMaxWaves * 64), 0, s>>>(
+      (const unsigned char*)in, src_off, (unsigned char*)out, dst_off, cap, n, K);
   return harp_launch_status();
 }

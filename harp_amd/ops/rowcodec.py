@@ -31,6 +31,8 @@ _lib.register({
                                _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
     "harp_rowcodec_decode_add16": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
                                    _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    "harp_rowcodec_copy_slots": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                                 _lib.c_int, _lib.c_int, _lib.c_void_p],
 })
 
 ALIGN = 16
@@ -207,3 +209,25 @@ def decode(dst: torch.Tensor, K: int, rows: torch.Tensor, off: torch.Tensor, cap
     else:
         dst[r, :K] = vals
     return dst
+
+
+def copy_slots(inp: torch.Tensor, src_off: torch.Tensor, out: torch.Tensor, dst_off: torch.Tensor,
+               cap: torch.Tensor, K: int) -> torch.Tensor:
+    """Slot j of ``out`` (at ``dst_off[j]``) := the slot at ``src_off[j]`` of ``inp`` (same
+    capacity ``cap[j]``): the header and used entries of a sparse slot, the whole dense row."""
+    n = cap.numel()
+    if n == 0:
+        return out
+    if _lib.use_native(out):
+        for t in (inp, src_off, dst_off, cap):
+            assert t.device == out.device and t.is_contiguous()
+        assert src_off.dtype == torch.int64 and dst_off.dtype == torch.int64 and cap.dtype == torch.int32
+        st = _lib.kernels().harp_rowcodec_copy_slots(inp.data_ptr(), src_off.data_ptr(), out.data_ptr(),
+                                                     dst_off.data_ptr(), cap.data_ptr(), n, K,
+                                                     _lib.stream_ptr(out.device))
+        _lib.check(st, "rowcodec_copy_slots")
+        return out
+    sz = slot_sizes(cap.long(), K)
+    for a, d, b in zip(src_off.tolist(), dst_off.tolist(), sz.tolist()):
+        out[d:d + b] = inp[a:a + b]
+    return out

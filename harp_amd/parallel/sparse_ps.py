@@ -114,9 +114,33 @@ class SparseRowPS:
             assert self.pull_recv.nbytes == self.pull_send.nbytes and self.push_recv.nbytes == self.push_send.nbytes
             self.pull_recv.buf = self.pull_send.buf
             self.push_recv.buf = self.push_send.buf
+        # owner side: a row wanted by several requesters is encoded ONCE into a canonical
+        # slot (its pull cap is the same for every requester: global tokens) and copied into
+        # each requester's slot -- the row read once, not once per requester
+        self._dedup = None
+        srows = self.pull_send.rows.cpu().long()
+        if P > 1 and srows.numel():
+            uq, inv = torch.unique(srows, return_inverse=True)
+            if uq.numel() < srows.numel():
+                first = torch.full((uq.numel(),), srows.numel(), dtype=torch.int64).scatter_reduce_(
+                    0, inv, torch.arange(srows.numel()), reduce="amin")
+                ucap = self.pull_send.cap.cpu()[first].to(torch.int64)
+                coff, cnb = RC.layout(ucap, self.K)
+                self._dedup = (uq.to(torch.int32).to(dev), coff.to(dev), ucap.to(torch.int32).to(dev),
+                               torch.empty(max(cnb, RC.ALIGN), dtype=torch.uint8, device=dev),
+                               coff[inv].contiguous().to(dev))
         self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.n_rows = int(ids.numel())
         self._pulled = False
+
+    def _encode_pull(self, glob_rows: torch.Tensor) -> None:
+        s = self.pull_send
+        if self._dedup is None:
+            RC.encode(glob_rows, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
+            return
+        urows, coff, ucap, cbuf, src_off = self._dedup
+        RC.encode(glob_rows, self.K, urows, coff, ucap, cbuf, self.overflow)
+        RC.copy_slots(cbuf, src_off, s.buf, s.off, s.cap, self.K)
 
     # -- traffic accounting ---------------------------------------------------------------
     def bytes_per_call(self, remote_only: bool = True) -> Tuple[int, int]:
@@ -137,7 +161,7 @@ class SparseRowPS:
         """``local[i] := glob row of want_ids[i]`` for every wanted row (owners encode from
         ``glob_rows`` [rows, >=K])."""
         s, r = self.pull_send, self.pull_recv
-        RC.encode(glob_rows, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
+        self._encode_pull(glob_rows)
         self._exchange(s, r)
         RC.decode(local, self.K, r.rows, r.off, r.cap, r.buf)
         self._pulled = True
@@ -181,7 +205,7 @@ class SparseRowPS:
         """The pull without its decode: owners encode, one all-to-all; returns the received
         payload (slots per :meth:`row_slots`)."""
         s, r = self.pull_send, self.pull_recv
-        RC.encode(glob_rows, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
+        self._encode_pull(glob_rows)
         self._exchange(s, r)
         self._pulled = True
         return r.buf

@@ -91,6 +91,33 @@ def test_rowcodec_narrow_table_gpu(cuda, K):
     assert torch.equal(wide.cpu(), src + delta)
 
 
+def test_rowcodec_copy_slots_gpu(cuda):
+    """Encode-once pull (parallel.sparse_ps at P > 1): rows encoded once into canonical slots
+    and copied into every requester's slot decode to the same rows as a direct encode."""
+    K, n = 1024, 1500
+    g = torch.Generator().manual_seed(11)
+    src = torch.zeros((n, K), dtype=torch.int32)
+    for r in range(n):
+        k = int(torch.randint(0, 300, (1,), generator=g))
+        if k:
+            src[r, torch.randperm(K, generator=g)[:k]] = torch.randint(1, 100, (k,), generator=g, dtype=torch.int32)
+    caps = RC.slot_caps((src != 0).sum(1) + 1, K).to(torch.int32)
+    req = torch.randint(0, n, (4000,), generator=g)  # requested rows, with repeats
+    uq, inv = torch.unique(req, return_inverse=True)
+    coff, cnb = RC.layout(caps[uq].long(), K)
+    doff, dnb = RC.layout(caps[req].long(), K)
+    ov = torch.zeros(1, dtype=torch.int32, device=cuda)
+    cbuf = torch.zeros(cnb, dtype=torch.uint8, device=cuda)
+    RC.encode(src.to(cuda), K, uq.to(torch.int32).to(cuda), coff.to(cuda), caps[uq].to(cuda), cbuf, ov)
+    out = torch.zeros(dnb, dtype=torch.uint8, device=cuda)
+    RC.copy_slots(cbuf, coff[inv].contiguous().to(cuda), out, doff.to(cuda), caps[req].to(cuda), K)
+    dec = torch.zeros((req.numel(), K), dtype=torch.int32, device=cuda)
+    RC.decode(dec, K, torch.arange(req.numel(), dtype=torch.int32, device=cuda), doff.to(cuda), caps[req].to(cuda), out)
+    torch.cuda.synchronize()
+    assert int(ov) == 0
+    assert torch.equal(dec.cpu(), src[req])
+
+
 def test_rowcodec_overflow_flag_gpu(cuda):
     K = 256
     src = torch.ones((10, K), dtype=torch.int32, device=cuda)

@@ -79,7 +79,7 @@ def _ps_worker(comm):
     ps.push(cur, glob, delta=True)
     ps.check_overflow()
     return {"want": want, "local": local, "pulled": pulled, "delta": cur - pulled, "glob": glob, "owned": owned,
-            "bytes": ps.bytes_per_call()}
+            "bytes": ps.bytes_per_call(), "dedup": ps._dedup is not None}
 
 
 @pytest.mark.parametrize("P", [1, 2, 3])
@@ -93,6 +93,7 @@ def test_sparse_ps_push_pull(P):
         dtot.index_add_(0, r["want"], r["delta"])
     for r in res:
         assert torch.equal(r["pulled"], tot0[r["want"]])  # pull = the owners' summed rows
+        assert r["dedup"] == (P > 1)  # rows wanted by several ranks: encoded once, slots copied
     final = tot0 + dtot
     for r in res:  # owners hold exactly the sum of initial counts and every delta
         for j, b in enumerate(r["owned"]):
