@@ -37,6 +37,16 @@ __device__ __forceinline__ float uni_f(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
+// murmur3 finalizer
+__device__ __forceinline__ unsigned hash32(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -244,6 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
   // int64: start, length | word << 32, the word's pull-slot and push-slot offsets (fused
   // rows; else 0) -- one scalar load instead of the chain bounds -> word -> slot offsets.
   const bool lptm = lpt != nullptr && !det;
+  const unsigned seed32 = hash32((unsigned)seed ^ hash32((unsigned)(seed >> 32) ^ 0x85EBCA6Bu));
   for (long r = 0;; ++r) {
 #ifdef HARP_LDA_STAMPS
     const unsigned long long st_t0 = clock64();
@@ -380,15 +391,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
           z_nx = tz[ix];
         }
         if (d == pd && pnz != pz) {  // this row was loaded before the previous token's move
-          const unsigned m1 = lane == pz / TPL ? 1u << (8 * (pz & 3)) : 0u;
-          r[(pz % TPL) >> 2] -= m1;
-          const unsigned m2 = lane == pnz / TPL ? 1u << (8 * (pnz & 3)) : 0u;
-          r[(pnz % TPL) >> 2] += m2;
+          const unsigned m1 = lane == (int)((unsigned)pz / TPL) ? 1u << (8 * (pz & 3)) : 0u;
+          r[((unsigned)pz % TPL) >> 2] -= m1;  // (topics are >= 0: unsigned index arithmetic)
+          const unsigned m2 = lane == (int)((unsigned)pnz / TPL) ? 1u << (8 * (pnz & 3)) : 0u;
+          r[((unsigned)pnz % TPL) >> 2] += m2;
         }
         // the token's own count is left in the packed row: its removal is the product
         // correction -qw_z (after qw_z's own update) on lane z / TPL, and the walk below
         // takes 1 off topic z when it reads that lane's row
-        const int zl = z / TPL, zt = z % TPL;
+        const int zl = (unsigned)z / TPL, zt = (unsigned)z % TPL;
         const float inv_z = inv_nk[z];
         const bool mez = lane == zl;
         float s;
@@ -403,8 +414,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         for (int t = 0; t < TPL; ++t) s = fmaf((float)((r[t >> 2] >> (8 * (t & 3))) & 0xFFu), qw[t], s);
         const float incl = wave_incl_scan(s, lane);
         const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
-        const unsigned long long rbits = mix64(seed ^ ((unsigned long long)i * 0xD6E8FEB86659FD93ull));
-        const float u = ((float)(unsigned)(rbits >> 40) * (1.f / 16777216.f)) * total;
+        // 32-bit hash of (token, sweep seed): 8 scalar instructions instead of the 64-bit
+        // mix (~20; the loop issues as many SALU as VALU instructions, both pipes ~70 % busy)
+        const unsigned rb = hash32((unsigned)i ^ seed32 ^ ((unsigned)(i >> 32) * 0x9E3779B9u));
+        const float u = ((float)(rb >> 8) * (1.f / 16777216.f)) * total;
         const unsigned long long hit = __ballot(incl > u);
         const int src = hit ? (int)__builtin_ctzll(hit) : 63;
         int found;
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         }
         int nz = src * TPL + found;
         if (nz >= K) nz = K - 1;
-        const int nzl = nz / TPL, nzt = nz % TPL;
+        const int nzl = (unsigned)nz / TPL, nzt = (unsigned)nz % TPL;
         const float inv_nz = inv_nk[nz];
         {
           const bool me = lane == nzl;
