@@ -213,10 +213,11 @@ struct PsRows {
   int* overflow;
 };
 
-// XW: extra waves per SIMD over the compiler's occupancy (a few VGPRs spill; more resident
-// waves hide the random doc-row fetch). A one-token-ahead doc-row prefetch measured slower
-// (0.90e9 vs 1.17e9 tokens/s at K = 1000, profiles/r1_lda/ldapf: its extra VGPRs cost a
-// wave per SIMD) and was removed.
+// Dense sampler: one wave per word chunk, the word's factors qw in registers (TPL topics per
+// lane), the token's doc row read per token. XW: waves per SIMD over six (variant 3: seven,
+// the default). The round-1 doc-row prefetch for float rows measured slower (its VGPRs cost a
+// wave per SIMD, profiles/r1_lda/ldapf); the round-5 packed uint8 path (PK below) keeps a
+// row in 4 VGPRs, so it prefetches the next token's row.
 template <int TPL, class DT, int XW = 0>  // topics per lane; K_pad = 64 * TPL
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 ? 6 + XW : 8, 8))) void lda_cgs_kernel(
     const int* __restrict__ tdoc, const int* __restrict__ tword, int* __restrict__ tz,
@@ -1173,8 +1174,8 @@ static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* 
                         int ldd, int ndk_bits, int* nwk, int ldw, const float* inv_nk, int* nk_delta, int K, float alpha,
                         float beta, unsigned long long seed, int variant, PsRows ps, const long* lpt, hipStream_t s) {
   if (nchunks <= 0) return HARP_OK;
-  // variant 0: six waves per SIMD; 3: seven (the default). The doc-row
-  // prefetch (1) and the other forced occupancies (2, 4, 5) measured slower
+  // variant 0: six waves per SIMD; 3: seven (the default). Round 1's variants (1: a
+  // float-row prefetch; 2, 4, 5: other forced occupancies) measured slower
   // (profiles/r1_lda/occupancy) and are no longer built.
   // variant | 0x100: deterministic one-wave sampling (tests)
   const int det = (variant & 0x100) ? 1 : 0;
