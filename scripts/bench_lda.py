@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--sparse-comm", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--fused-rows", default="on", choices=["on", "off"],
                     help="push_pull with sparse rows: the sampler reads pull slots / writes push slots")
+    ap.add_argument("--slices", type=int, default=0, help="rotation: word slices per worker (0: LDAConfig default)")
     ap.add_argument("--local-server", default="on", choices=["on", "off"],
                     help="push_pull at P=1: off runs the pull / push collectives even on one rank")
     a = ap.parse_args()
@@ -45,6 +46,8 @@ def main():
                     sparse_comm=a.sparse_comm, local_server=a.local_server == "on", fused_rows=a.fused_rows == "on")
     if a.max_chunk:
         cfg.max_chunk = a.max_chunk
+    if a.slices:
+        cfg.num_slices = a.slices
     cls = LDAPushPullMapper if a.strategy == "push_pull" else LDACollectiveMapper
     m = cls(comm, cfg, nd, V, toks)
     del toks

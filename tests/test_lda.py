@@ -35,7 +35,7 @@ def test_lda_rotation_improves(corpus, P):
 
 
 def test_lda_p_invariance(corpus):
-    cfg = LDAConfig(num_topics=10, alpha=0.1, beta=0.01, iterations=30, print_interval=30)
+    cfg = LDAConfig(num_topics=10, alpha=0.1, beta=0.01, iterations=30, print_interval=30, num_slices=2)
     one = launch(_job, 1, args=(cfg, 300, 400, corpus))[0]["loglik"][-1][1]
     two = launch(_job, 2, args=(cfg, 300, 400, corpus), timeout=300)[0]["loglik"][-1][1]
     n_tok = corpus[0].numel()
