@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -191,11 +192,12 @@ def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[
     if os.environ.get("HARP_LDA_ORDER", "lpt") == "identity" or chunks.numel() < 2:
         return None
     # (a rotation slice passes a new view of the same token array every call: keyed by its
-    # address; the entry keeps the view, so the address cannot be reused while cached)
+    # address and length; entries hold weak references, so a cached schedule never keeps a
+    # model's arrays alive, and a hit needs the same, still-live chunk tensor)
     key = (id(chunks), chunks.data_ptr(), chunks.numel(), tword.data_ptr(), tword.numel(),
            None if slots is None else tuple(x.data_ptr() for x in slots))
     hit = _LPT.get(key)
-    if hit is not None and hit[0] is chunks:
+    if hit is not None and hit[0]() is chunks:
         return hit[1]
     order = torch.argsort(chunks[1:] - chunks[:-1], descending=True)
     a = chunks[:-1][order]
@@ -207,9 +209,11 @@ def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[
     if slots is not None:
         d[:, 2] = slots[0][w]
         d[:, 3] = slots[2][w]
+    for k in [k for k, v in _LPT.items() if v[0]() is None]:  # entries of freed layouts
+        del _LPT[k]
     if len(_LPT) >= 16:
         _LPT.pop(next(iter(_LPT)))
-    _LPT[key] = (chunks, d.contiguous(), tword, slots)
+    _LPT[key] = (weakref.ref(chunks), d.contiguous())
     return _LPT[key][1]
 
 
