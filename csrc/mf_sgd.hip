@@ -421,14 +421,15 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
 // window of win[64 + c] ratings starting at win[c], wrapping around the cell — the
 // fixed-fraction mode standing in for the reference's timer-bounded rotation steps.
 //
-// Placement check (chk != NULL): the schedule is only conflict-free if every block of residue
-// x runs on ONE XCD and the 8 residues on 8 different XCDs. Thread 0 of each block reads
-// HW_REG_XCC_ID and tags, for launch number `gen` (host counter, > 0), residue -> XCC and
-// XCC -> residue in a 64-bit word each ((gen << 8) | id + 1; the first block of a launch to
-// see an older generation installs its own pair, so no reset launch is needed). A block
-// whose pair disagrees with the installed one raises chk[kChkErr] (sticky; the host reads it
-// once per epoch, ops.mf.check_placement, and switches to the placed kernel below).
-constexpr int kChkWords = 32;  // [0, 8) residue map | [8, 24) XCC map | [24] error
+// Placement check (chk != NULL): the schedule is only coherent if every block of residue x
+// runs on ONE XCD (its W and H blocks then live in one L2; residues sharing an XCD touch
+// disjoint blocks, and launches are ordered by the stream). Thread 0 of each block reads
+// HW_REG_XCC_ID at the block's end and tags, for launch number `gen` (host counter, > 0),
+// residue -> XCC in a 64-bit word ((gen << 8) | id + 1; the first block of a launch to see an
+// older generation installs its own, so no reset launch is needed). A block whose XCC
+// disagrees with the installed one raises chk[kChkErr] (sticky; the host reads it once per
+// epoch, ops.mf.check_placement, and switches to the placed kernel below).
+constexpr int kChkWords = 32;  // [0, 8) residue map | [24] error
 constexpr int kChkErr = 24;
 
 __device__ __forceinline__ unsigned tag_once(unsigned long long* p, unsigned long long gen, unsigned val) {
@@ -446,12 +447,15 @@ __device__ __forceinline__ int hw_xcc_id() {
   return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;  // HW_REG_XCC_ID
 }
 
+// Called by thread 0 at the END of a block (at the start, every block's first barrier waited
+// on these device-scope atomics, which all blocks of a residue aim at one word: 2.5 % of an
+// epoch). Only residue -> XCC is checked: it is what coherence needs (all of a residue's
+// blocks in one L2); two residues sharing an XCD touch disjoint W / H blocks.
 __device__ __forceinline__ void placement_check(unsigned long long* chk, unsigned long long gen, int x) {
   if (chk == nullptr || threadIdx.x != 0) return;
   const int hw = hw_xcc_id();
-  const bool bad = tag_once(chk + x, gen, (unsigned)hw + 1) != (unsigned)hw + 1 ||
-                   tag_once(chk + 8 + hw, gen, (unsigned)x + 1) != (unsigned)x + 1;
-  if (bad) __hip_atomic_store(chk + kChkErr, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tag_once(chk + x, gen, (unsigned)hw + 1) != (unsigned)hw + 1)
+    __hip_atomic_store(chk + kChkErr, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int R, int CH, int ATOM>
@@ -464,7 +468,6 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
   __shared__ int sR[16 * CH], sC[16 * CH];
   __shared__ float sV[16 * CH];
   const int x = blockIdx.x % XCDS;
-  placement_check(chk, gen, x);
   const long j = blockIdx.x / XCDS;
   const long per_xcd = gridDim.x / XCDS;
   const int cell = x * XCDS + (x + step) % XCDS;
@@ -493,6 +496,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_kernel(const int* __restrict__
       sgd_stream_lds<R, false, ATOM>(sR + sub * CH, sC + sub * CH, sV + sub * CH, mine < CH ? (int)mine : CH, sl, W,
                              (unsigned)ldw, H, (unsigned)ldh, lr, lam);
   }
+  placement_check(chk, gen, x);
 }
 
 // Placement-independent sub-step (the fallback when placement_check fires): a block trains
@@ -940,7 +944,6 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_wide_kernel(const int* __restr
                                                               int ldh, float lr, float lam,
                                                               unsigned long long* chk, unsigned long long gen) {
   const int x = blockIdx.x % XCDS;
-  placement_check(chk, gen, x);
   const long j = blockIdx.x / XCDS;
   const long per_xcd = gridDim.x / XCDS;
   const int cell = x * XCDS + (x + step) % XCDS;
@@ -955,6 +958,7 @@ __global__ __launch_bounds__(256) void mf_sgd_xcd_wide_kernel(const int* __restr
     const long i1 = i0 + CH < n ? i0 + CH : n;
     sgd_stream_wide<Q>(rows, cols, vals, a, w0, ncell, i0, i1, threadIdx.x & 63, R, W, ldw, H, ldh, lr, lam);
   }
+  placement_check(chk, gen, x);
 }
 
 template <int Q>

@@ -11,6 +11,8 @@ import ctypes
 import math
 from typing import List, Optional, Tuple
 
+import os
+
 import torch
 
 from . import _lib
@@ -142,7 +144,9 @@ def check_flow_errors(device: torch.device) -> None:
 PLACED_VARIANT = 2
 # harp_mf_sgd_xcd variant bits 2..3: atomic (no-lost-update) write-back of W (1) / H (2)
 ATOMIC_W, ATOMIC_H = 1, 2
-CHECK_PLACEMENT = True  # default kernel: tag residue <-> XCC per launch, raise an error word on a mismatch
+# default kernel: tag residue <-> XCC per launch, raise an error word on a mismatch
+# (HARP_MF_CHECK_PLACEMENT=0 turns it off: an A/B knob for its cost)
+CHECK_PLACEMENT = os.environ.get("HARP_MF_CHECK_PLACEMENT", "1") != "0"
 _CHK: dict = {}
 
 
