@@ -84,14 +84,16 @@ __device__ __forceinline__ float wave_incl_scan(float v, int) {
 // bytes of the per-token row read that bounds this kernel; updated with 32-bit atomics
 // on the containing dword: counts stay in [0, 65535], so a +-1 on one half never
 // carries or borrows into the other)
-// a relaxed device-scope atomic add by ONE lane through a global-address-space pointer
-// laundered into VGPRs: a uniform address would be rewritten into a wave reduction (mbcnt,
-// popcount and two branches around the atomic) although only one lane is active
-__device__ __forceinline__ void lane_atomic_add(const void* p, unsigned v) {
+// a relaxed device-scope atomic add by ONE lane at a uniform row base + a byte offset that is
+// laundered into a VGPR: a uniform address would be rewritten into a wave reduction (mbcnt,
+// popcount and two branches around the atomic) although only one lane is active, and a
+// laundered 64-bit address costs a scalar 64-bit add chain; base (SGPRs) + 32-bit VGPR
+// offset is the instruction's own addressing mode
+__device__ __forceinline__ void lane_atomic_add(const void* base, unsigned off, unsigned v) {
   typedef __attribute__((address_space(1))) unsigned gu32;
-  unsigned long a = (unsigned long)p;
-  asm volatile("" : "+v"(a));
-  __hip_atomic_fetch_add((gu32*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  typedef __attribute__((address_space(1))) char gchar;
+  asm volatile("" : "+v"(off));
+  __hip_atomic_fetch_add((gu32*)((gchar*)(unsigned long)base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <class DT>
@@ -107,7 +109,7 @@ struct DocRow<int> {
     }
   }
   __device__ static __forceinline__ void add(int* drow, int k, int v) { atomicAdd(drow + k, v); }
-  __device__ static __forceinline__ void add1(int* drow, int k, int v) { lane_atomic_add(drow + k, (unsigned)v); }
+  __device__ static __forceinline__ void add1(int* drow, int k, int v) { lane_atomic_add(drow, 4u * k, (unsigned)v); }
 };
 template <>
 struct DocRow<unsigned short> {
@@ -145,7 +147,7 @@ struct DocRow<unsigned short> {
   // v = +-1 from one lane (two's complement: a -1 on a nonzero count borrows only inside
   // its own field)
   __device__ static __forceinline__ void add1(unsigned short* drow, int k, int v) {
-    lane_atomic_add(drow + (k & ~1), (unsigned)v << ((k & 1) ? 16u : 0u));
+    lane_atomic_add(drow, 2u * (k & ~1), (unsigned)v << ((k & 1) ? 16u : 0u));
   }
 };
 
@@ -192,7 +194,7 @@ struct DocRow<unsigned char> {
     else atomicSub(word, (unsigned)(-v) << sh);
   }
   __device__ static __forceinline__ void add1(unsigned char* drow, int k, int v) {
-    lane_atomic_add(drow + (k & ~3), (unsigned)v << ((unsigned)(k & 3) * 8u));
+    lane_atomic_add(drow, (unsigned)(k & ~3), (unsigned)v << ((unsigned)(k & 3) * 8u));
   }
 };
 
