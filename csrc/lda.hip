@@ -80,10 +80,6 @@ __device__ __forceinline__ float wave_incl_scan(float v, int) {
   return v;
 }
 
-// doc-topic row element: int (32-bit counts) or unsigned short (16-bit counts, half the
-// bytes of the per-token row read that bounds this kernel; updated with 32-bit atomics
-// on the containing dword: counts stay in [0, 65535], so a +-1 on one half never
-// carries or borrows into the other)
 // a relaxed device-scope atomic add by ONE lane at a uniform row base + a byte offset that is
 // laundered into a VGPR: a uniform address would be rewritten into a wave reduction (mbcnt,
 // popcount and two branches around the atomic) although only one lane is active, and a
@@ -96,6 +92,29 @@ __device__ __forceinline__ void lane_atomic_add(const void* base, unsigned off, 
   __hip_atomic_fetch_add((gu32*)((gchar*)(unsigned long)base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a 32-bit load / store at a uniform base + a byte offset in a VGPR (the instruction's base
+// + offset addressing: no per-access 64-bit address arithmetic); ld_at takes an offset the
+// caller has laundered into a VGPR once for several loads
+__device__ __forceinline__ unsigned in_vgpr(unsigned v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ int ld_at(const int* base, unsigned voff) {
+  typedef __attribute__((address_space(1))) const int gi32;
+  typedef __attribute__((address_space(1))) const char gchar;
+  return *(gi32*)((gchar*)(unsigned long)base + voff);
+}
+__device__ __forceinline__ void st_at(int* base, unsigned off, int v) {
+  typedef __attribute__((address_space(1))) int gi32;
+  typedef __attribute__((address_space(1))) char gchar;
+  asm volatile("" : "+v"(off));
+  *(gi32*)((gchar*)(unsigned long)base + off) = v;
+}
+
+// doc-topic row element: int (32-bit counts) or unsigned short (16-bit counts, half the
+// bytes of the per-token row read that bounds this kernel; updated with 32-bit atomics
+// on the containing dword: counts stay in [0, 65535], so a +-1 on one half never
+// carries or borrows into the other)
 template <class DT>
 struct DocRow;
 template <>
@@ -361,37 +380,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
       // loaded for this token missed only the previous token's move: applied in registers
       // when it is of the same document.
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
-      const int d0 = __builtin_amdgcn_readfirstlane(tdoc[a]);
-      int zcur = __builtin_amdgcn_readfirstlane(tz[a]), dcur = d0;
+      // a chunk-relative 32-bit token index: ids are loaded and stored at the chunk's base
+      // pointers + a VGPR byte offset, and bounds are 32-bit scalar compares
+      const int* tdoc_c = tdoc + a;
+      int* tz_c = tz + a;
+      const int n = (int)(b - a);
+      // the draw's random key: a per-chunk hash of the start token, xored with the index
+      const unsigned ckey = hash32((unsigned)a ^ seed32 ^ ((unsigned)(a >> 32) * 0x9E3779B9u));
+      const int d0 = __builtin_amdgcn_readfirstlane(tdoc_c[0]);
+      int zcur = __builtin_amdgcn_readfirstlane(tz_c[0]), dcur = d0;
       v4u rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)d0 * ldd + k0));
       int d_nx, z_nx;  // ids of the token after the current one (vector loads, one token ahead)
       {
-        long ix = a + 1 < b ? a + 1 : a;
-        asm volatile("" : "+v"(ix));
-        d_nx = tdoc[ix];
-        z_nx = tz[ix];
+        const unsigned ix = in_vgpr(1 < n ? 4u : 0u);
+        d_nx = ld_at(tdoc_c, ix);
+        z_nx = ld_at(tz_c, ix);
       }
-      long pi = -1;
       int pd = -1, pz = 0, pnz = 0;
       DT* prow = ndk;
-      for (long i = a; i < b; ++i) {
+      float inv_cur = inv_nk[zcur];  // inv_nk of the token's topic: a scalar load one token ahead
+      for (int j = 0; j < n; ++j) {
         const int d = dcur, z = zcur;
         DT* drow = ndk + (long)d * ldd;
         unsigned r[4] = {rw_nx.x, rw_nx.y, rw_nx.z, rw_nx.w};
         const int dn = __builtin_amdgcn_readfirstlane(d_nx), zn = __builtin_amdgcn_readfirstlane(z_nx);
-        if (pi >= 0 && lane == 0) {
-          tz[pi] = pnz;
+        const float inv_z = inv_cur;
+        inv_cur = *(const float*)((const char*)inv_nk + 4u * (unsigned)zn);
+        if (j > 0 && lane == 0) {
+          st_at(tz_c, 4u * (unsigned)(j - 1), pnz);
           if (pnz != pz) {
             DocRow<DT>::add1(prow, pz, -1);
             DocRow<DT>::add1(prow, pnz, 1);
           }
         }
-        if (i + 1 < b) rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)dn * ldd + k0));
+        if (j + 1 < n) rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)dn * ldd + k0));
         {
-          long ix = i + 2 < b ? i + 2 : i;
-          asm volatile("" : "+v"(ix));
-          d_nx = tdoc[ix];
-          z_nx = tz[ix];
+          const unsigned ix = in_vgpr(4u * (unsigned)(j + 2 < n ? j + 2 : j));
+          d_nx = ld_at(tdoc_c, ix);
+          z_nx = ld_at(tz_c, ix);
         }
         if (d == pd && pnz != pz) {  // this row was loaded before the previous token's move
           const unsigned m1 = lane == (int)((unsigned)pz / TPL) ? 1u << (8 * (pz & 3)) : 0u;
@@ -403,7 +429,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         // correction -qw_z (after qw_z's own update) on lane z / TPL, and the walk below
         // takes 1 off topic z when it reads that lane's row
         const int zl = (unsigned)z / TPL, zt = (unsigned)z % TPL;
-        const float inv_z = inv_nk[z];
         const bool mez = lane == zl;
         float s;
         {
@@ -417,9 +442,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         for (int t = 0; t < TPL; ++t) s = fmaf((float)((r[t >> 2] >> (8 * (t & 3))) & 0xFFu), qw[t], s);
         const float incl = wave_incl_scan(s, lane);
         const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
-        // 32-bit hash of (token, sweep seed): 8 scalar instructions instead of the 64-bit
-        // mix (~20; the loop issues as many SALU as VALU instructions, both pipes ~70 % busy)
-        const unsigned rb = hash32((unsigned)i ^ seed32 ^ ((unsigned)(i >> 32) * 0x9E3779B9u));
+        // 32-bit hash of (chunk key, index): a few scalar instructions (the loop issues about
+        // as many SALU as VALU instructions, both pipes ~70 % busy)
+        const unsigned rb = hash32(ckey ^ (unsigned)j);
         const float u = ((float)(rb >> 8) * (1.f / 16777216.f)) * total;
         const unsigned long long hit = __ballot(incl > u);
         const int src = hit ? (int)__builtin_ctzll(hit) : 63;
@@ -449,7 +474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         int nz = src * TPL + found;
         if (nz >= K) nz = K - 1;
         const int nzl = (unsigned)nz / TPL, nzt = (unsigned)nz % TPL;
-        const float inv_nz = inv_nk[nz];
+        const float inv_nz = *(const float*)((const char*)inv_nk + 4u * (unsigned)nz);
         {
           const bool me = lane == nzl;
           const float qv = qw[nzt];
@@ -464,7 +489,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
           wdel[zi] -= 1;
           wdel[ni] += 1;
         }
-        pi = i;
         pz = z;
         pnz = nz;
         pd = d;
@@ -473,7 +497,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         zcur = zn;
       }
       if (lane == 0) {  // the chunk's last token
-        tz[pi] = pnz;
+        st_at(tz_c, 4u * (unsigned)(n - 1), pnz);
         if (pnz != pz) {
           DocRow<DT>::add1(prow, pz, -1);
           DocRow<DT>::add1(prow, pnz, 1);

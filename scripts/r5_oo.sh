@@ -1,7 +1,7 @@
 #!/bin/bash
 # LDA one-lane doc-row atomics at uniform base + VGPR byte offset: tests, full-size P=1 push-pull and 8-share, twice
 set -o pipefail
-O=gpurun_out/round5_oo
+O=gpurun_out/${1:-round5_oo}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_lda_gpu.py tests/test_rowcodec_gpu.py \
