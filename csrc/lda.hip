@@ -397,18 +397,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         z_nx = ld_at(tz_c, ix);
       }
       int pd = -1, pz = 0, pnz = 0;
-      DT* prow = ndk;
       float inv_cur = inv_nk[zcur];  // inv_nk of the token's topic: a scalar load one token ahead
       for (int j = 0; j < n; ++j) {
         const int d = dcur, z = zcur;
-        DT* drow = ndk + (long)d * ldd;
         unsigned r[4] = {rw_nx.x, rw_nx.y, rw_nx.z, rw_nx.w};
         const int dn = __builtin_amdgcn_readfirstlane(d_nx), zn = __builtin_amdgcn_readfirstlane(z_nx);
         const float inv_z = inv_cur;
         inv_cur = *(const float*)((const char*)inv_nk + 4u * (unsigned)zn);
         if (j > 0 && lane == 0) {
           st_at(tz_c, 4u * (unsigned)(j - 1), pnz);
-          if (pnz != pz) {
+          if (pnz != pz) {  // (the row address only when the token moved)
+            DT* prow = ndk + (long)pd * ldd;
             DocRow<DT>::add1(prow, pz, -1);
             DocRow<DT>::add1(prow, pnz, 1);
           }
@@ -431,11 +430,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         const int zl = (unsigned)z / TPL, zt = (unsigned)z % TPL;
         const bool mez = lane == zl;
         float s;
-        {
-          const float qv = qw[zt];
-          const float qn = qv - inv_z;
-          qw[zt] = mez ? qn : qv;
-          qs -= mez ? inv_z : 0.f;
+        {  // (the lane-selected change is 0 elsewhere: x - 0 == x, no select on the write)
+          const float dz = mez ? inv_z : 0.f;
+          const float qn = qw[zt] - dz;
+          qw[zt] = qn;
+          qs -= dz;
           s = alpha * qs - (mez ? qn : 0.f);
         }
 #pragma unroll
@@ -444,9 +443,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
         // 32-bit hash of (chunk key, index): a few scalar instructions (the loop issues about
         // as many SALU as VALU instructions, both pipes ~70 % busy)
+        // u = (f - 1) * total for f = 1.m in [1, 2) with the hash's top 23 bits as m: the
+        // float is built by scalar bit operations, one fma (no int -> float conversion)
         const unsigned rb = hash32(ckey ^ (unsigned)j);
-        const float u = ((float)(rb >> 8) * (1.f / 16777216.f)) * total;
-        const unsigned long long hit = __ballot(incl > u);
+        const float u = fmaf(__uint_as_float(0x3F800000u | (rb >> 9)), total, -total);
+        const unsigned long long hit = __builtin_amdgcn_ballot_w64(incl > u);
         const int src = hit ? (int)__builtin_ctzll(hit) : 63;
         int found;
         {  // the drawn lane's topics walked by lanes 0..15 (as below, packed counts)
@@ -467,8 +468,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
           c = dpp_add(c, 1);
           c = dpp_add(c, 2);
           c = dpp_add(c, 3);
-          const unsigned long long h = __ballot(lane < TPL && c + ex > u) & ((1ull << TPL) - 1);
-          const unsigned long long nzp = __ballot(pv > 0.f) & ((1ull << TPL) - 1);
+          const unsigned long long h = __builtin_amdgcn_ballot_w64(c + ex > u) & ((1ull << TPL) - 1);
+          const unsigned long long nzp = __builtin_amdgcn_ballot_w64(pv > 0.f) & ((1ull << TPL) - 1);
           found = h ? (int)__builtin_ctzll(h) : (nzp ? 63 - (int)__builtin_clzll(nzp) : TPL - 1);
         }
         int nz = src * TPL + found;
@@ -476,29 +477,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         const int nzl = (unsigned)nz / TPL, nzt = (unsigned)nz % TPL;
         const float inv_nz = *(const float*)((const char*)inv_nk + 4u * (unsigned)nz);
         {
-          const bool me = lane == nzl;
-          const float qv = qw[nzt];
-          qw[nzt] = me ? qv + inv_nz : qv;
-          qs += me ? inv_nz : 0.f;
+          const float dn = lane == nzl ? inv_nz : 0.f;
+          qw[nzt] += dn;
+          qs += dn;
         }
         if (lane == 0 && nz != z) {
-          int zi = z, ni = nz;
-          asm volatile("" : "+v"(zi), "+v"(ni));  // per-lane LDS addresses: no wave-reduction rewrite
-          atomicSub(&s_delta[zi], 1);
-          atomicAdd(&s_delta[ni], 1);
-          wdel[zi] -= 1;
-          wdel[ni] += 1;
+          // byte offsets laundered into VGPRs once (per-lane LDS addresses: no wave-reduction
+          // rewrite) for both rows; returnless LDS adds, no read-modify-write waits
+          const unsigned zo = in_vgpr(4u * (unsigned)z), no = in_vgpr(4u * (unsigned)nz);
+          atomicAdd((int*)((char*)s_delta + zo), -1);
+          atomicAdd((int*)((char*)s_delta + no), 1);
+          atomicAdd((int*)((char*)wdel + zo), -1);
+          atomicAdd((int*)((char*)wdel + no), 1);
         }
         pz = z;
         pnz = nz;
         pd = d;
-        prow = drow;
         dcur = dn;
         zcur = zn;
       }
       if (lane == 0) {  // the chunk's last token
         st_at(tz_c, 4u * (unsigned)(n - 1), pnz);
         if (pnz != pz) {
+          DT* prow = ndk + (long)pd * ldd;
           DocRow<DT>::add1(prow, pz, -1);
           DocRow<DT>::add1(prow, pnz, 1);
         }
