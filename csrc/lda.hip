@@ -251,9 +251,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
   __shared__ int s_delta[KP];
   __shared__ int s_nw0[WAVES][KP];  // per wave: the pulled word row, then the chunk's moves
   __shared__ float4 s_x[WAVES][TPL / 2];  // the drawn lane's doc counts + qw (topic walk)
+  // per wave: the chunk's first kMoves moves (z | nz << 16): a chunk with few moves flushes
+  // only the topics it touched. The LDS row s_nw0[wv] is all zero between chunks (the flush
+  // takes each touched entry by an exchange with 0, or re-zeroes the whole row)
+  constexpr int kMoves = 32;
+  __shared__ unsigned s_mv[WAVES][kMoves];
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
     s_delta[k] = 0;
   }
+  for (int k = threadIdx.x; k < WAVES * KP; k += blockDim.x) (&s_nw0[0][0])[k] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -311,11 +317,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
     float qw[TPL];
     if (ps.pbuf) {
       // the word row from its pull slot into this wave's LDS row (zero, then scatter)
+      // (the row is all zero here: the previous flush left it so)
       int* lrow = &s_nw0[wv][0];
       const unsigned char* slot = ps.pbuf + poff_c;
       const int cap = ps.pcap[w];
-#pragma unroll
-      for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -358,9 +363,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
       qw[t] = (qw[t] + beta) * inv_nk[k0 + t];  // (inv_nk holds K_pad entries, 0 past K)
       qs += qw[t];
     }
+    if (ps.pbuf) {  // the landing row back to zero
 #pragma unroll
-    for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
+      for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
+    }
     int* wdel = &s_nw0[wv][0];
+    int mv = 0;  // the chunk's moves (wave-uniform)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -489,7 +497,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
           atomicAdd((int*)((char*)s_delta + no), 1);
           atomicAdd((int*)((char*)wdel + zo), -1);
           atomicAdd((int*)((char*)wdel + no), 1);
+          if (mv < kMoves) s_mv[wv][mv] = (unsigned)z | ((unsigned)nz << 16);
         }
+        mv += nz != z ? 1 : 0;
         pz = z;
         pnz = nz;
         pd = d;
@@ -596,8 +606,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
             atomicAdd(&s_delta[nz], 1);
             wdel[z] -= 1;
             wdel[nz] += 1;
+            if (mv < kMoves) s_mv[wv][mv] = (unsigned)z | ((unsigned)nz << 16);
           }
         }
+        mv = __builtin_amdgcn_readfirstlane(mv + (nz != z ? 1 : 0));
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's row moves -> every lane
@@ -607,20 +619,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
     st_t2 = clock64();
     st_tok += st_t2 - st_t1;
 #endif
-    // flush this chunk's word-row delta
+    // flush this chunk's word-row delta. Up to kMoves moves: lanes 0 .. 2 mv - 1 take one
+    // touched topic each from the move list and its delta by an LDS exchange with 0 (a topic
+    // touched twice is taken by one lane, the other reads 0); more: every lane its TPL topics
+    // of the row, then zeroes them
+    const bool lst = mv <= kMoves;
+    int lt = 0, ldl = 0;
+    if (lst && lane < 2 * mv) {
+      const unsigned e = s_mv[wv][lane >> 1];
+      lt = (lane & 1) ? (int)(e >> 16) : (int)(e & 0xFFFFu);
+      ldl = atomicExch(&wdel[lt], 0);
+    }
     if (ps.qbuf) {
       unsigned char* slot = ps.qbuf + qoff_c;
       const int cap = ps.qcap[w];
       if (cap < 0) {
+        if (lst) {
+          if (ldl) atomicAdd((int*)slot + lt, ldl);
+        } else {
 #pragma unroll
-        for (int t = 0; t < TPL; ++t) {
-          const int dlt = nw0s[t];
-          if (dlt) atomicAdd((int*)slot + k0 + t, dlt);
+          for (int t = 0; t < TPL; ++t) {
+            const int dlt = nw0s[t];
+            if (dlt) atomicAdd((int*)slot + k0 + t, dlt);
+          }
         }
       } else {
         int mine = 0;
+        if (lst) {
+          mine = ldl != 0 ? 1 : 0;
+        } else {
 #pragma unroll
-        for (int t = 0; t < TPL; ++t) mine += nw0s[t] != 0 ? 1 : 0;
+          for (int t = 0; t < TPL; ++t) mine += nw0s[t] != 0 ? 1 : 0;
+        }
         const float incl = wave_incl_scan((float)mine, lane);
         const int tot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
         int base = 0;
@@ -632,27 +662,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         int* cnt = (int*)(slot + 4);
         unsigned short* top = (unsigned short*)(slot + 4 + 4 * (long)cap);
         bool over = false;
-#pragma unroll
-        for (int t = 0; t < TPL; ++t) {
-          const int dlt = nw0s[t];
-          if (dlt) {
+        if (lst) {
+          if (ldl) {
             if (pos < cap) {
-              cnt[pos] = dlt;
-              top[pos] = (unsigned short)(k0 + t);
+              cnt[pos] = ldl;
+              top[pos] = (unsigned short)lt;
             } else {
               over = true;
             }
-            ++pos;
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < TPL; ++t) {
+            const int dlt = nw0s[t];
+            if (dlt) {
+              if (pos < cap) {
+                cnt[pos] = dlt;
+                top[pos] = (unsigned short)(k0 + t);
+              } else {
+                over = true;
+              }
+              ++pos;
+            }
           }
         }
         if (__ballot(over) && lane == 0) ps.overflow[0] = 1;
       }
+    } else if (lst) {
+      if (ldl) atomicAdd(nwk + (long)w * ldw + lt, ldl);
     } else {
 #pragma unroll
       for (int t = 0; t < TPL; ++t) {
         const int dlt = nw0s[t];
         if (dlt) atomicAdd(wrow + t, dlt);
       }
+    }
+    if (!lst) {
+#pragma unroll
+      for (int t = 0; t < TPL; t += 4) *(int4*)(nw0s + t) = int4{0, 0, 0, 0};
     }
 #ifdef HARP_LDA_STAMPS
     st_fl += clock64() - st_t2;
