@@ -311,16 +311,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
       }
     }
     int* wrow = nwk + (long)w * ldw + k0;
+    // chunk start: every load that depends only on the descriptor is issued before any wait
+    // (the first token's ids, the pull slot's capacity and entry count), then the first doc
+    // row (PK) and the slot's entries: two memory round trips before the token loop instead
+    // of six (vmcnt is in order: a wait for one load waits for every load issued before it)
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const int* tdoc_c = tdoc + a;
+    int* tz_c = tz + a;
+    const int n = (int)(b - a);
+    const unsigned char* slot = ps.pbuf + poff_c;
+    const int* capp = ps.pbuf ? ps.pcap + w : tdoc_c;  // (any valid address without a PS)
+    const int* nnzp = ps.pbuf ? (const int*)slot : tdoc_c;
+    int d_first = tdoc_c[0], z_first = tz_c[0], cap_l = *capp, nnz_l = *nnzp;
+    // (one wait for all four here: the compiler would otherwise sink each load to its use)
+    asm volatile("" : "+v"(d_first), "+v"(z_first), "+v"(cap_l), "+v"(nnz_l));
+    int dcur = 0, zcur = 0;
+    v4u rw_nx = {0u, 0u, 0u, 0u};
+    if constexpr (PK) {
+      dcur = __builtin_amdgcn_readfirstlane(d_first);
+      zcur = __builtin_amdgcn_readfirstlane(z_first);
+      rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)dcur * ldd + k0));
+    }
     // the per-word factor qw_t = (n_wt + beta) / (n_t + V beta) in registers; a token then
     // costs ONE multiply-add per topic, p_t = (n_dt + alpha) * qw_t, and only the two topics
     // a token moves have their qw changed
     float qw[TPL];
     if (ps.pbuf) {
-      // the word row from its pull slot into this wave's LDS row (zero, then scatter)
+      // the word row from its pull slot into this wave's LDS row, scattered
       // (the row is all zero here: the previous flush left it so)
       int* lrow = &s_nw0[wv][0];
-      const unsigned char* slot = ps.pbuf + poff_c;
-      const int cap = ps.pcap[w];
+      const int cap = __builtin_amdgcn_readfirstlane(cap_l);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -330,13 +350,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         // models/lda.py): copy all of it, so topics K - K % 4 .. K - 1 are not left at 0
         for (int q = lane; q < KP / 4; q += 64) ((int4*)lrow)[q] = s4[q];
       } else {
-        int nnz = *(const int*)slot;
+        int nnz = __builtin_amdgcn_readfirstlane(nnz_l);
         nnz = nnz < 0 ? 0 : (nnz > cap ? cap : nnz);
         const int* cnt = (const int*)(slot + 4);
         const unsigned short* top = (const unsigned short*)(slot + 4 + 4 * (long)cap);
         for (int e = lane; e < nnz; e += 64) {
-          const int t = top[e];
-          if (t < K) lrow[t] = cnt[e];
+          int t = top[e], c = cnt[e];
+          asm volatile("" : "+v"(t), "+v"(c));  // (both loads in flight together: e < nnz <= cap)
+          if (t < K) lrow[t] = c;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -387,17 +408,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
       // too, and the compiler's count is conservative over lane 0's branches). The row
       // loaded for this token missed only the previous token's move: applied in registers
       // when it is of the same document.
-      typedef unsigned v4u __attribute__((ext_vector_type(4)));
-      // a chunk-relative 32-bit token index: ids are loaded and stored at the chunk's base
-      // pointers + a VGPR byte offset, and bounds are 32-bit scalar compares
-      const int* tdoc_c = tdoc + a;
-      int* tz_c = tz + a;
-      const int n = (int)(b - a);
+      // a chunk-relative 32-bit token index (tdoc_c, tz_c, n above): ids are loaded and
+      // stored at the chunk's base pointers + a VGPR byte offset, and bounds are 32-bit
+      // scalar compares
       // the draw's random key: a per-chunk hash of the start token, xored with the index
       const unsigned ckey = hash32((unsigned)a ^ seed32 ^ ((unsigned)(a >> 32) * 0x9E3779B9u));
-      const int d0 = __builtin_amdgcn_readfirstlane(tdoc_c[0]);
-      int zcur = __builtin_amdgcn_readfirstlane(tz_c[0]), dcur = d0;
-      v4u rw_nx = __builtin_nontemporal_load((const v4u*)(ndk + (long)d0 * ldd + k0));
       int d_nx, z_nx;  // ids of the token after the current one (vector loads, one token ahead)
       {
         const unsigned ix = in_vgpr(1 < n ? 4u : 0u);
