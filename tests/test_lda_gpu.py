@@ -111,6 +111,43 @@ def test_packed16_doc_topic_counts_consistent(cuda, K):
     assert int(d.sum()) == 0
 
 
+@pytest.mark.parametrize("mc", [16, 4096])
+def test_dense_packed_flush_paths_exact(cuda, mc):
+    """The packed uint8 dense sampler flushes a chunk's word-row moves from its move list
+    (chunks of <= 16 tokens: <= 32 moves) or from the whole LDS row (4096-token chunks): after
+    two sweeps either way the word-topic table, the doc rows and the topic sums equal a
+    recount from the assignments."""
+    from harp_amd.ops import lda as L
+
+    K = 1000
+    g = torch.Generator(device=cuda).manual_seed(3)
+    nd, V, n = 3000, 500, 120000
+    tdoc = torch.randint(0, nd, (n,), generator=g, device=cuda, dtype=torch.int32)
+    tword = torch.randint(0, V, (n,), generator=g, device=cuda, dtype=torch.int32)
+    order = torch.argsort(tword.long() * nd + tdoc.long())
+    tdoc, tword = tdoc[order].contiguous(), tword[order].contiguous()
+    tz = torch.randint(0, K, (n,), generator=g, device=cuda, dtype=torch.int32)
+    Kp = L.padded_topics(K)
+    ndk = torch.zeros((nd, Kp), dtype=torch.uint8, device=cuda)
+    nwk = torch.zeros((V, Kp), dtype=torch.int32, device=cuda)
+    nk = torch.zeros(Kp, dtype=torch.int32, device=cuda)
+    L.count(tdoc, tword, tz, ndk, nwk, nk)
+    chunks = L.build_chunks(tword, mc)
+    before = tz.clone()
+    for sweep in range(2):
+        d = L.cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K, 0.1, 0.01, V * 0.01, 11 + sweep)
+        nk += d
+    torch.cuda.synchronize()
+    assert int((tz != before).sum()) > n // 4  # the sweeps moved tokens
+    r_ndk = torch.zeros((nd, Kp), dtype=torch.int32, device=cuda)
+    r_nwk = torch.zeros_like(nwk)
+    r_nk = torch.zeros_like(nk)
+    L.count(tdoc, tword, tz, r_ndk, r_nwk, r_nk)
+    assert torch.equal(r_nwk, nwk)
+    assert torch.equal(r_ndk, ndk.int())
+    assert torch.equal(r_nk, nk)
+
+
 @pytest.mark.parametrize("K,forced", [(300, True), (2000, False)])
 def test_lda_sparse_sampler_matches_cpu_quality(cuda, K, forced, monkeypatch):
     """The sparse-doc sampler (the K > 1024 path; forced at K = 300) improves the
