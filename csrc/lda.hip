@@ -279,8 +279,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
   // snake order (round r: wave w takes rank r W + w, or r W + W-1-w on odd rounds), so every
   // wave gets about the same number of tokens (the static stride over word order left the
   // waves that drew the longest word chunks running long after the rest). A descriptor is 4
-  // int64: start, length | word << 32, the word's pull-slot and push-slot offsets (fused
-  // rows; else 0) -- one scalar load instead of the chain bounds -> word -> slot offsets.
+  // int64: start, length | sole << 31 | word << 32 (sole: the word's only chunk), the word's
+  // pull-slot and push-slot offsets (fused rows; else 0) -- one scalar load instead of the
+  // chain bounds -> word -> slot offsets.
   const bool lptm = lpt != nullptr && !det;
   const unsigned seed32 = hash32((unsigned)seed ^ hash32((unsigned)(seed >> 32) ^ 0x85EBCA6Bu));
   for (long r = 0;; ++r) {
@@ -289,13 +290,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
 #endif
     long a, b, poff_c = 0, qoff_c = 0;
     int w;
+    bool sole = false;  // the only chunk of its word: its push slot has no other writer
     if (lptm) {
       const long k = r * nwaves + ((r & 1) ? nwaves - 1 - wave_g : wave_g);
       if (k >= nchunks) break;
       const long* dk = lpt + 4 * k;
       a = dk[0];
       const long lw = dk[1];
-      b = a + (lw & 0xFFFFFFFFL);
+      b = a + (lw & 0x7FFFFFFFL);
+      sole = ((lw >> 31) & 1) != 0;
       w = (int)(lw >> 32);
       poff_c = dk[2];
       qoff_c = dk[3];
@@ -670,8 +673,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
         const int tot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
         int base = 0;
         if (tot) {
-          if (lane == 0) base = atomicAdd((int*)slot, tot);
-          base = __builtin_amdgcn_readfirstlane(base);
+          // the sole chunk of its word writes the slot's count (zeroed push payload, no other
+          // writer this sweep): no returning atomic, whose round trip ended every chunk
+          if (sole) {
+            if (lane == 0) *(int*)slot = tot;
+          } else {
+            if (lane == 0) base = atomicAdd((int*)slot, tot);
+            base = __builtin_amdgcn_readfirstlane(base);
+          }
         }
         int pos = base + (int)incl - mine;
         int* cnt = (int*)(slot + 4);

@@ -191,9 +191,15 @@ def chunk_order(chunks: torch.Tensor) -> torch.Tensor:
 _LPT: dict = {}
 
 
+# HARP_LDA_SOLE=0: no chunk is marked the sole chunk of its word (every push slot reserved
+# by an atomic, as before the flag existed)
+SOLE = os.environ.get("HARP_LDA_SOLE", "1") != "0"
+
+
 def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[torch.Tensor]:
     """The dense sampler's chunk schedule: one descriptor per chunk, longest first (int64
-    [n, 4]: start, length | word << 32, the word's pull-slot and push-slot offsets when
+    [n, 4]: start, length | sole << 31 | word << 32 (sole: the word's only chunk, whose push
+    slot then needs no reservation atomic), the word's pull-slot and push-slot offsets when
     ``slots`` (fused rows) are given, else 0), dealt to the resident waves in snake order by
     the kernel. Cached per (chunks, tword, slots) (the layouts are static across sweeps).
     None with HARP_LDA_ORDER=identity (the static word-order stride)."""
@@ -211,9 +217,10 @@ def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[
     a = chunks[:-1][order]
     n = chunks[1:][order] - a
     w = tword[a].long()
+    sole = (torch.bincount(w)[w] == 1).long() * int(SOLE)
     d = torch.zeros((order.numel(), 4), dtype=torch.int64, device=chunks.device)
     d[:, 0] = a
-    d[:, 1] = n | (w << 32)
+    d[:, 1] = n | (sole << 31) | (w << 32)
     if slots is not None:
         d[:, 2] = slots[0][w]
         d[:, 3] = slots[2][w]

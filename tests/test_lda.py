@@ -230,14 +230,16 @@ def test_lda_init_past_the_sort_limit(corpus, monkeypatch):
 
 def test_lpt_desc_longest_first_and_cached():
     """The dense sampler's chunk schedule: every chunk once, longest first, as (start,
-    length | word << 32, pull-slot offset, push-slot offset); cached per layout."""
+    length | sole << 31 | word << 32, pull-slot offset, push-slot offset); cached per layout."""
     words = torch.tensor([0] * 5 + [1] * 2 + [2] * 9 + [3] * 1 + [4] * 3, dtype=torch.int32)
     chunks = L.build_chunks(words, 4)
     poff = torch.arange(5, dtype=torch.int64) * 100
     qoff = torch.arange(5, dtype=torch.int64) * 1000
     cap = torch.zeros(5, dtype=torch.int32)
     d = L.lpt_desc(chunks, words, (poff, cap, qoff, cap))
-    a, ln, w = d[:, 0], d[:, 1] & 0xFFFFFFFF, d[:, 1] >> 32
+    a, ln, w = d[:, 0], d[:, 1] & 0x7FFFFFFF, d[:, 1] >> 32
+    sole = (d[:, 1] >> 31) & 1  # the word's only chunk (words 1, 3, 4 here)
+    assert {int(x): int(y) for x, y in zip(w, sole)} == {0: 0, 1: 1, 2: 0, 3: 1, 4: 1}
     assert ln.tolist() == sorted(ln.tolist(), reverse=True)
     assert sorted(zip(a.tolist(), (a + ln).tolist())) == [(int(chunks[i]), int(chunks[i + 1]))
                                                           for i in range(chunks.numel() - 1)]
