@@ -611,6 +611,18 @@ HARP_EXPORT int harp_sytrd_fused(double* A, long lda, int n, double* d, double* 
   return launch_fused<8>(A, lda, n, d, e, nb_max, ws, wsd, s, V, tau);
 }
 
+// Eigenvalues (ascending) of the tridiagonal (d, e) by multisection into w (n doubles).
+HARP_EXPORT int harp_tridiag_eigvals(const double* d, const double* e, int n, double* w, hipStream_t s) {
+  if (n < 1 || n > kMaxN || !d || !e || !w) return HARP_EBADARG;
+  const size_t lds2 = sizeof(double) * 2 * (size_t)n;
+  if (lds2 > 32 * 1024 &&
+      hipFuncSetAttribute((const void*)tridiag_multisect_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds2) != hipSuccess)
+    return HARP_ELAUNCH;
+  tridiag_multisect_kernel<<<dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), lds2, s>>>(d, e, n, w);
+  return harp_launch_status();
+}
+
 // diagnostic: the next fused launches sum workgroup 0's cycles per phase into stamps[0..3]
 // (w + column update, Householder vector, trailing pass, arrival); nullptr turns it off
 HARP_EXPORT void harp_eig_fused_stamps(long long* stamps) { g_fused_stamps = stamps; }

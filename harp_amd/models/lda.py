@@ -41,7 +41,8 @@ class LDAConfig:
                               # full-size sweep, profiles/r5_lda_slices), else 2 (transfers overlap compute)
     print_interval: int = 5
     seed: int = 0
-    max_chunk: int = 0        # tokens per word chunk; 0 = 2048 (dense sampler) / 65536 (sparse)
+    max_chunk: int = 0        # tokens per word chunk; 0 = ops.lda.max_chunk's default (dense sampler:
+                              # n_tokens / 3072 within [2048, 32768]; sparse sampler: 65536)
     block_words: int = 4096   # push/pull strategy: words per model partition
     sparse_comm: str = "auto"  # push/pull: "on" = fixed-layout sparse rows (parallel.sparse_ps, HIP codec),
                                # "off" = dense word blocks, "auto" = whichever the link/HBM model says is faster

@@ -20,7 +20,7 @@ import os
 import random
 import sys
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from typing import List, Optional, Tuple
 
 import torch
@@ -171,7 +171,8 @@ class SGDCollectiveMapper(CollectiveMapper):
     def __init__(self, comm=None, config: Optional[SGDConfig] = None, n_users: int = 0, n_items: int = 0,
                  train=None, test=None, metrics=None):
         super().__init__(comm, metrics)
-        self.cfg = config or SGDConfig()
+        # a private copy: the placement fallback switches kernels on it, never on the caller's
+        self.cfg = replace(config) if config is not None else SGDConfig()
         self.n_users, self.n_items = n_users, n_items
         self._train, self._test = train, test
         self.rmse_history: List[Tuple[int, float, float]] = []
@@ -392,7 +393,9 @@ class SGDCollectiveMapper(CollectiveMapper):
         launch run blocks of one residue on two XCDs (csrc/mf_sgd.hip placement_check)?
         Then that epoch ran Hogwild across L2s (every rating still trained once) and the
         remaining epochs use a schedule that does not depend on the dispatcher's placement:
-        the placed kernel (ranks <= 256) or the flat kernel (wide ranks)."""
+        the placed kernel (ranks <= 256) or the flat kernel (wide ranks; with train_fraction
+        < 1 the windows need the blocked layout, so that run keeps it and only records the
+        event)."""
         if self.device.type != "cuda" or not self.cfg.xcd_blocks:
             return
         got = MF.check_placement(self.device)
@@ -405,6 +408,8 @@ class SGDCollectiveMapper(CollectiveMapper):
         if MF.storage_rank(self.cfg.rank, self.device) <= 256:
             self.cfg.kernel_variant = MF.PLACED_VARIANT
             what = "placed"
+        elif self.cfg.train_fraction < 1.0 or self.cfg.time_budget_ms > 0:
+            what = "blocked (kept: windowed training needs the XCD-blocked layout)"
         else:
             self.cfg.xcd_blocks = False
             what = "flat"

@@ -1,7 +1,11 @@
 """Symmetric eigen-decomposition of the PCA pass's d x d fp64 correlation matrix.
 
-* :func:`eigvalsh`: cooperative Householder tridiagonalisation on one XCD + multisection
+* the Householder tridiagonalisation: up to n = 1024 the chip-wide register-resident form
+  (``csrc/eig_ll.hip``: rows of the matrix in the VGPRs of ceil(n / 8) workgroups, panel-deferred
+  two-sided updates, one data-tagged granule exchange per column); above that, or if that
+  launch could not get its workgroups co-resident, the one-XCD cooperative form
   (``csrc/eig.hip``);
+* :func:`eigvalsh`: the reduction + multisection (``csrc/eig.hip``);
 * :func:`eigh`: eigenvalues AND eigenvectors -- the same reduction keeping its reflectors,
   divide and conquer on the tridiagonal (``csrc/tridiag_dc.hip``: Cuppen merges with
   Gu-Eisenstat vectors, host reference ``ops/tridiag_dc.py``), and the back-transform
@@ -38,12 +42,22 @@ _lib.register({
     # A, lda, n, d, e, w, nb_max, ws, wsd, stream
     "harp_eig_sym_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                            _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    # d, e, n, w, stream
+    "harp_tridiag_eigvals": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
+    "harp_sytrd_ll_max_n": [],
+    "harp_sytrd_ll_gran_words": [],
+    "harp_sytrd_ll_workgroups": [_lib.c_int],
+    "harp_sytrd_ll_stamps": [_lib.c_void_p],
+    # A, lda, n, d, e, V, ldv, tau, ws, gran, stream
+    "harp_sytrd_ll": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                      _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
 })
 
 NB_DEFAULT = 32  # workgroups (CUs) of XCD 0
-# reduction form: "fused" (one pass over the trailing block and one arrival per column,
+# reduction form: "ll" (chip-wide, register-resident rows, granule exchange; n <= 1024, else
+# "fused"), "fused" (one XCD, one pass over the trailing block and one arrival per column,
 # look-ahead Householder vector) or "twopass" (matrix-vector pass + rank-2 update pass)
-VARIANT = os.environ.get("HARP_EIG_VARIANT", "fused")
+VARIANT = os.environ.get("HARP_EIG_VARIANT", "ll")
 
 
 # crossover to rocSOLVER: the one-XCD reduction costs n steps of ~10-25 us and loses to the
@@ -76,13 +90,21 @@ def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None, native: bool |
     nb = int(k.harp_eig_workgroups(n, nb_max))
     if nb < 1:
         return torch.linalg.eigvalsh(C)
+    if VARIANT == "ll" and stamps is None:
+        r = sytrd_ll(C, vectors=False)
+        if r is not None:
+            d, e = r[0], r[1]
+            w = torch.empty(n, dtype=torch.float64, device=dev)
+            _lib.check(k.harp_tridiag_eigvals(d.data_ptr(), e.data_ptr(), n, w.data_ptr(), _lib.stream_ptr(dev)),
+                       "tridiag_eigvals")
+            return w
     A = C.contiguous().clone()  # symmetric: row-major storage is the column-major matrix
     ws = torch.zeros(int(k.harp_eig_ws_ints()), dtype=torch.int32, device=dev)
     wsd = torch.zeros(3 * n + 4, dtype=torch.float64, device=dev)
     d = torch.empty(n, dtype=torch.float64, device=dev)
     e = torch.empty(n, dtype=torch.float64, device=dev)
     w = torch.empty(n, dtype=torch.float64, device=dev)
-    if VARIANT == "fused" and stamps is None:
+    if VARIANT in ("fused", "ll") == "fused" and stamps is None:
         st = k.harp_eig_sym_fused(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb, ws.data_ptr(),
                                   wsd.data_ptr(), _lib.stream_ptr(dev))
     else:
@@ -95,6 +117,45 @@ def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None, native: bool |
                       "using torch.linalg.eigvalsh")
         return torch.linalg.eigvalsh(C)
     return w
+
+
+def ll_usable(n: int) -> bool:
+    """The chip-wide reduction takes n <= harp_sytrd_ll_max_n() (1024) with one workgroup per
+    8 rows, all co-resident (one per CU)."""
+    k = _lib.kernels()
+    return 0 < n <= int(k.harp_sytrd_ll_max_n())
+
+
+_LL_WARNED = [False]
+
+
+def sytrd_ll(C: torch.Tensor, vectors: bool = True):
+    """Tridiagonalise the symmetric fp64 GPU matrix ``C`` (n <= 1024) with the chip-wide
+    kernel: returns (d, e, Vt, tau) -- Vt row k = v_k, tau_k as :func:`back_transform` takes
+    them (None when ``vectors`` is False) -- or None when the kernel is not applicable or a
+    workgroup timed out (not all of them co-resident)."""
+    n = C.shape[0]
+    if not ll_usable(n):
+        return None
+    dev = C.device
+    k = _lib.kernels()
+    A = C.contiguous()
+    ws = torch.zeros(int(k.harp_eig_ws_ints()), dtype=torch.int32, device=dev)
+    gran = torch.zeros(int(k.harp_sytrd_ll_gran_words()), dtype=torch.int64, device=dev)
+    d = torch.empty(n, dtype=torch.float64, device=dev)
+    e = torch.zeros(max(n, 1), dtype=torch.float64, device=dev)
+    Vt = torch.zeros((n, n), dtype=torch.float64, device=dev) if vectors else None
+    tau = torch.zeros(n, dtype=torch.float64, device=dev) if vectors else None
+    st = k.harp_sytrd_ll(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), _lib.ptr(Vt), n, _lib.ptr(tau),
+                         ws.data_ptr(), gran.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(st, "sytrd_ll")
+    if int(ws[2].item()):
+        if not _LL_WARNED[0]:
+            warnings.warn("chip-wide tridiagonalisation timed out (workgroups not co-resident); "
+                          "using the one-XCD reduction")
+            _LL_WARNED[0] = True
+        return None
+    return d, e, Vt, tau
 
 
 # ------------------------------------------------------------------ eigenvectors
@@ -164,6 +225,12 @@ def eigh(C: torch.Tensor, native: bool | None = None):
     n = C.shape[0]
     dev = C.device
     k = _lib.kernels()
+    if VARIANT == "ll":
+        r = sytrd_ll(C)
+        if r is not None:
+            d, e, Vt, tau = r
+            lam, Z = eigh_tridiag(d, e[:max(n - 1, 0)])
+            return lam, back_transform(Vt, tau, Z)
     nb = int(k.harp_eig_workgroups(n, int(os.environ.get("HARP_EIG_NB", NB_DEFAULT))))
     if nb < 1:
         return torch.linalg.eigh(C)

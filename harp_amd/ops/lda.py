@@ -208,10 +208,14 @@ def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[
     # (a rotation slice passes a new view of the same token array every call: keyed by its
     # address and length; entries hold weak references, so a cached schedule never keeps a
     # model's arrays alive, and a hit needs the same, still-live chunk tensor)
+    # The descriptors embed the slot offsets the kernel stores to, so a hit also needs the
+    # SAME slot tensors (weak references): a rebuilt parameter-server layout that the
+    # allocator placed at the old addresses is a miss, never stale offsets.
     key = (id(chunks), chunks.data_ptr(), chunks.numel(), tword.data_ptr(), tword.numel(),
            None if slots is None else tuple(x.data_ptr() for x in slots))
     hit = _LPT.get(key)
-    if hit is not None and hit[0]() is chunks:
+    if hit is not None and hit[0]() is chunks and (
+            slots is None or (len(hit[2]) == len(slots) and all(r() is x for r, x in zip(hit[2], slots)))):
         return hit[1]
     order = torch.argsort(chunks[1:] - chunks[:-1], descending=True)
     a = chunks[:-1][order]
@@ -228,7 +232,7 @@ def lpt_desc(chunks: torch.Tensor, tword: torch.Tensor, slots=None) -> Optional[
         del _LPT[k]
     if len(_LPT) >= 16:
         _LPT.pop(next(iter(_LPT)))
-    _LPT[key] = (weakref.ref(chunks), d.contiguous())
+    _LPT[key] = (weakref.ref(chunks), d.contiguous(), tuple(weakref.ref(x) for x in slots) if slots is not None else ())
     return _LPT[key][1]
 
 
@@ -370,16 +374,9 @@ def _host_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed, doc_
         if ndk.dtype == torch.int16:
             h_ndk = h_ndk & 0xFFFF
         h_ndk = h_ndk.contiguous()
+        delta = _cpu_sweep(h_doc, h_word, h_tz, h_ndk, h_nwk, h_nk, K, alpha, beta, vbeta, seed)
     else:
-        n_docs = int(doc_index.doc_off.numel() - 1) if doc_index is not None else int(h_doc.max()) + 1
-        # counts of EVERY token of each doc (not only this sweep's): from the doc-order lists
-        off = doc_index.doc_off.cpu()
-        lens = off[1:] - off[:-1]
-        all_doc = torch.repeat_interleave(torch.arange(n_docs), lens)
-        all_z = doc_index.zdoc.cpu().long() & 0xFFFF
-        h_ndk = torch.zeros((n_docs, Kp), dtype=torch.int32)
-        h_ndk.index_put_((all_doc, all_z), torch.ones(all_z.numel(), dtype=torch.int32), accumulate=True)
-    delta = _cpu_sweep(h_doc, h_word, h_tz, h_ndk, h_nwk, h_nk, K, alpha, beta, vbeta, seed)
+        delta = _host_sweep_doc_batches(h_doc, h_word, h_tz, h_nwk, h_nk, Kp, K, alpha, beta, vbeta, seed, doc_index)
     tz.copy_(h_tz.to(dev))
     nwk.copy_(h_nwk.to(dev))
     if ndk is not None:
@@ -387,6 +384,50 @@ def _host_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed, doc_
     if doc_index is not None:
         doc_index.sync(tz, tpos)
     return delta.to(dev)
+
+
+# host bytes one dense doc-topic batch of the GPU worker's host sampler may take (K > 32768)
+HOST_NDK_BYTES = int(os.environ.get("HARP_LDA_HOST_NDK_BYTES", str(1 << 30)))
+
+
+def _host_sweep_doc_batches(h_doc, h_word, h_tz, h_nwk, h_nk, Kp, K, alpha, beta, vbeta, seed, doc_index):
+    """The host sweep of a worker that keeps no dense doc-topic table: the docs of this sweep
+    are taken in batches whose dense [docs, Kp] int32 rows fit HOST_NDK_BYTES, each batch's
+    counts rebuilt from the doc-order topic lists (EVERY token of those docs, not only this
+    sweep's), and the batch's tokens (in their word order) sampled sequentially against the
+    shared word-topic rows and topic totals carried from batch to batch. Every token is
+    resampled once from its exact collapsed conditional, so the sweep stays a systematic-scan
+    Gibbs sweep whatever the batching; with one batch it is the plain sequential sweep."""
+    off = doc_index.doc_off.cpu()
+    lens = off[1:] - off[:-1]
+    zdoc = doc_index.zdoc.cpu().long() & 0xFFFF
+    docs = torch.unique(h_doc.long())
+    per = max(1, HOST_NDK_BYTES // (Kp * 4))
+    delta = torch.zeros_like(h_nk)
+    nk_cur = h_nk.clone()
+    tdoc_l = h_doc.long()
+    for q, s0 in enumerate(range(0, docs.numel(), per)):
+        bd = docs[s0:s0 + per]
+        if docs.numel() <= per:
+            idx = None
+            local = torch.searchsorted(bd, tdoc_l)
+        else:
+            idx = torch.isin(tdoc_l, bd).nonzero().squeeze(1)
+            local = torch.searchsorted(bd, tdoc_l[idx])
+        bl = lens[bd]
+        pos = torch.arange(int(bl.sum())) + torch.repeat_interleave(off[bd] - (torch.cumsum(bl, 0) - bl), bl)
+        b_ndk = torch.zeros((bd.numel(), Kp), dtype=torch.int32)
+        b_ndk.index_put_((torch.repeat_interleave(torch.arange(bd.numel()), bl), zdoc[pos]),
+                         torch.ones(pos.numel(), dtype=torch.int32), accumulate=True)
+        b_tz = h_tz if idx is None else h_tz[idx].contiguous()
+        b_word = h_word if idx is None else h_word[idx].contiguous()
+        d = _cpu_sweep(local.int().contiguous(), b_word, b_tz, b_ndk, h_nwk, nk_cur, K, alpha, beta, vbeta,
+                       seed + 0x9E3779B9 * q)
+        nk_cur += d
+        delta += d
+        if idx is not None:
+            h_tz[idx] = b_tz
+    return delta
 
 
 def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: float, vbeta: float, seed: int,

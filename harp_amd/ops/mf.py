@@ -179,8 +179,9 @@ def _chk(device: torch.device) -> _Chk:
 def check_placement(device: torch.device) -> dict:
     """Read (host sync) and clear the placement words of every stream on ``device``:
     ``{"violation": bool, "drained": n}`` -- a violation means a default-kernel launch had
-    blocks of one residue on two XCDs, or two residues on one XCD (that pass ran Hogwild
-    across L2s: every rating was still trained once); ``drained`` counts cells the placed
+    blocks of one residue on two XCDs (that pass ran Hogwild across L2s: every rating was
+    still trained once; two residues sharing one XCD is not checked -- it only slows that
+    XCD, it shares no cell); ``drained`` counts cells the placed
     kernel trained in its last block because their XCD received no block."""
     out = {"violation": False, "drained": 0}
     for (idx, _), c in _CHK.items():

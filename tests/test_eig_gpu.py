@@ -25,7 +25,7 @@ def test_random_symmetric(cuda, n):
     assert float((w - ref).abs().max()) <= 1e-12 * scale * max(1, n) ** 0.5
 
 
-@pytest.mark.parametrize("variant", ["fused", "twopass"])
+@pytest.mark.parametrize("variant", ["ll", "fused", "twopass"])
 @pytest.mark.parametrize("n", [3, 130, 1000])
 def test_reduction_variants(cuda, variant, n, monkeypatch):
     """Both reduction forms (fused look-ahead default, two-pass) against rocSOLVER."""
@@ -34,6 +34,32 @@ def test_reduction_variants(cuda, variant, n, monkeypatch):
     w = EIG.eigvalsh(C)
     ref = torch.linalg.eigvalsh(C)
     assert float((w - ref).abs().max()) <= 1e-12 * max(1.0, float(ref.abs().max())) * max(1, n) ** 0.5
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 17, 64, 65, 130, 513, 1000, 1024])
+def test_sytrd_ll_eigh(cuda, n):
+    """The chip-wide reduction (csrc/eig_ll.hip) runs (no fallback) and eigh through it
+    matches rocSOLVER: eigenvalues, |V^T V - I| and the residual |C V - V L| / |C|."""
+    C = _sym(n, 3 * n + 1, cuda)
+    assert EIG.sytrd_ll(C) is not None
+    lam, V = EIG.eigh(C, native=True)
+    ref = torch.linalg.eigvalsh(C)
+    nc = float(torch.linalg.matrix_norm(C, 2))
+    I = torch.eye(n, dtype=torch.float64, device=cuda)
+    assert float((lam - ref).abs().max()) <= 1e-12 * nc * n ** 0.5
+    assert float((V.t() @ V - I).abs().max()) <= 1e-13 * max(1.0, n / 100)
+    assert float((C @ V - V * lam).abs().max()) <= 1e-13 * nc * max(1.0, n / 100)
+
+
+def test_sytrd_ll_repeated_calls(cuda):
+    """Back-to-back calls reuse nothing stale (tags restart from zeroed granules each call)
+    and give bit-identical tridiagonals."""
+    C = _sym(700, 5, cuda)
+    r1 = EIG.sytrd_ll(C)
+    r2 = EIG.sytrd_ll(C)
+    assert r1 is not None and r2 is not None
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
 
 
 def test_degenerate_structure(cuda):

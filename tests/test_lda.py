@@ -246,3 +246,33 @@ def test_lpt_desc_longest_first_and_cached():
     assert torch.equal(w, words[a].long()) and torch.equal(d[:, 2], w * 100) and torch.equal(d[:, 3], w * 1000)
     assert L.lpt_desc(chunks, words, (poff, cap, qoff, cap)) is d
     assert L.lpt_desc(chunks, words)[:, 2:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("budget", [1 << 40, 40064 * 4 * 7])  # one batch; batches of 7 docs
+def test_host_sweep_doc_batches_keeps_counts_exact(monkeypatch, budget):
+    """The GPU worker's host path at K > 32768 builds dense doc-topic rows only for one batch
+    of documents at a time (a whole n_docs x Kp table does not fit at 1M docs).
+    Whatever the batching, every token is resampled once and the word-topic rows, topic
+    totals and doc-order lists stay exactly consistent with the assignments."""
+    if L._lib.runtime() is None:
+        pytest.skip("libharp_runtime.so not built")
+    monkeypatch.setattr(L, "HOST_NDK_BYTES", budget)
+    g = torch.Generator().manual_seed(5)
+    nd, V, n, K = 30, 50, 2000, 40000
+    Kp = L.padded_topics(K)
+    tword = torch.sort(torch.randint(0, V, (n,), generator=g)).values.to(torch.int32)
+    tdoc = torch.randint(0, nd, (n,), generator=g, dtype=torch.int32)
+    tz = torch.randint(0, K, (n,), generator=g, dtype=torch.int32)
+    nwk = torch.zeros((V, Kp), dtype=torch.int32)
+    nk = torch.zeros(Kp, dtype=torch.int32)
+    L.count(None, tword, tz, None, nwk, nk)
+    di = L.DocIndex.build(tdoc, tz, nd)
+    before = tz.clone()
+    delta = L._host_sweep(tdoc, tword, tz, None, nwk, nk, K, 0.01, 0.01, 0.01 * V, 7, di, di.tpos)
+    nwk2 = torch.zeros_like(nwk)
+    nk2 = torch.zeros_like(nk)
+    L.count(None, tword, tz, None, nwk2, nk2)
+    assert torch.equal(nwk, nwk2)
+    assert torch.equal(nk + delta, nk2)
+    assert torch.equal(di.zdoc.long() & 0xFFFF, tz[torch.argsort(di.tpos)].long())
+    assert int((tz != before).sum()) > n // 2  # at K = 40000 almost every token moves
