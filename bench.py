@@ -341,6 +341,50 @@ def bench_kmeans(args, comm, torch):
     return rec
 
 
+def _coll_breakdown(metrics, iters: int, comm, torch) -> dict:
+    """Per collective kind, per timed iteration: calls, stream milliseconds (HIP events; the
+    MAX over ranks), bytes on this rank, achieved GB/s and the xGMI link model's ideal time
+    (``utils.metrics.ideal_collective_s``), so a multi-GPU record says which collective cost
+    what. Kinds: pull / push (all-to-all of parameter-server rows),
+    allreduce, broadcast, rotate / rotate_wait (model rotation; rotate_wait = compute-stream
+    time stalled on an arrival, i.e. the rotation NOT hidden)."""
+    from harp_amd.utils.metrics import ideal_collective_s
+
+    metrics.resolve()
+    agg = {}
+    for c in metrics.collectives:
+        a = agg.setdefault(c["kind"], {"calls": 0, "s": 0.0, "bytes": 0, "ideal_s": 0.0})
+        a["calls"] += 1
+        a["s"] += c["s"]
+        a["bytes"] += c["bytes"]
+        a["ideal_s"] += ideal_collective_s(c["kind"], c["bytes"], comm.world_size)
+    # one MAX-allreduce over a fixed kind list: every rank takes part whatever it recorded
+    kinds = ("allgather", "allreduce", "broadcast", "join", "pull", "push", "reduce", "regroup", "rotate",
+             "rotate_wait")
+    v = torch.tensor([[agg.get(k, {}).get("calls", 0), agg.get(k, {}).get("s", 0.0)] for k in kinds],
+                     dtype=torch.float64, device=comm.device)
+    if comm.world_size > 1:
+        import torch.distributed as dist
+
+        comm.all_reduce(v, op=dist.ReduceOp.MAX)
+    v = v.cpu().tolist()
+    out = {}
+    it = max(iters, 1)
+    for kind, (calls_max, s_max) in zip(kinds, v):
+        if calls_max <= 0:
+            continue
+        a = agg.get(kind, {"calls": 0, "s": 0.0, "bytes": 0, "ideal_s": 0.0})
+        e = {"calls_per_iter": round(a["calls"] / it, 3), "ms_per_iter": round(s_max * 1e3 / it, 4),
+             "bytes_per_iter": int(a["bytes"] / it)}
+        if s_max > 0 and a["bytes"]:
+            e["gbps"] = round(a["bytes"] / s_max / 1e9, 3)
+        if a["ideal_s"] > 0:
+            e["ideal_ms_per_iter"] = round(a["ideal_s"] * 1e3 / it, 4)
+            e["eff_vs_xgmi_model"] = round(a["ideal_s"] / s_max, 4) if s_max > 0 else None
+        out[kind] = e
+    return out
+
+
 def _window_bytes(metrics, kinds=None) -> int:
     """Bytes of the collectives a mapper recorded (optionally of the given kinds)."""
     return sum(c["bytes"] for c in metrics.collectives if kinds is None or c["kind"] in kinds)
@@ -380,7 +424,7 @@ def bench_sgd(args, comm, torch):
     dt = reduce_max(comm, torch, time.perf_counter() - t0)
     ep_s = clock.durations()
     rot_bytes = _window_bytes(m.metrics, ("rotate_wait",))
-    m.metrics.resolve()
+    coll = _coll_breakdown(m.metrics, args.sgd_epochs, comm, torch)
     # compute-stream time stalled on slice arrivals (HIP events around each stream-level
     # wait): the part of the model rotation NOT hidden behind the SGD kernels
     rot_exposed = reduce_max(comm, torch, sum(c["s"] for c in m.metrics.collectives if c["kind"] == "rotate_wait"))
@@ -406,6 +450,7 @@ def bench_sgd(args, comm, torch):
         "n_gpus": P,
         "sync_bytes_per_iter": int(rot_bytes / max(args.sgd_epochs, 1)),
         "rotation_exposed_s_per_epoch": round(rot_exposed / max(args.sgd_epochs, 1), 6),
+        "collectives": coll,
         "rotation_strides": [s.stride for s in m.schedules],
         "xcd_placement": placement,
         "atomic_writeback": cfg.atomic,
@@ -447,11 +492,17 @@ def bench_pca(args, comm, torch):
         data = torch.rand((n, d), generator=g)
         syrk = lambda: data.t() @ data  # noqa: E731
 
+    from harp_amd.utils.metrics import Metrics
+
+    met = Metrics(rank=r, world=P)
+
     def one_pass():
-        return ST.pca(data, comm, dtype="bf16")
+        return ST.pca(data, comm, dtype="bf16", metrics=met)
 
     res = one_pass()
     sync(comm, torch)
+    met.resolve()
+    met.collectives.clear()
     clock = StepClock(comm, torch)
     t0 = time.perf_counter()
     clock.mark()
@@ -461,6 +512,7 @@ def bench_pca(args, comm, torch):
     sync(comm, torch)
     dt = reduce_max(comm, torch, time.perf_counter() - t0) / args.pca_steps
     st = step_stats(clock.durations())
+    coll = _coll_breakdown(met, args.pca_steps, comm, torch)
     sclock = StepClock(comm, torch)  # the SYRK alone (device time on GPUs)
     sclock.mark()
     syrk()
@@ -499,7 +551,7 @@ def bench_pca(args, comm, torch):
             "eig": "eigenvalues + eigenvectors (ops.eig.eigh)", "eigvec_orth_err": orth, "eig_residual": res_rel,
             "N": N, "d": d, "steps": args.pca_steps, "n_gpus": P,
             "syrk_tflops": round(flop / syrk_s / 1e12, 1) if syrk_s > 0 else None,
-            "syrk_flop_per_rank": flop, "sync_bytes_per_iter": int(sync_bytes),
+            "syrk_flop_per_rank": flop, "sync_bytes_per_iter": int(sync_bytes), "collectives": coll,
             "max_eigenvalue": round(float(ev.max()), 6),
             "dtype": "bf16 in / fp32 acc / fp64 finalize" if dev.type == "cuda" else "bf16-rounded fp32 (CPU rehearsal)",
             "data": "synthetic U[0,1) generated on device", "scaling": "strong"}
@@ -541,9 +593,8 @@ def _lda_run(args, comm, torch, local_server: bool, iters: int) -> dict:
     sync(comm, torch)
     dt = reduce_max(comm, torch, time.perf_counter() - t0)
     st = step_stats(clock.durations())
-    coll = _window_bytes(m.metrics)
-    if P > 1:
-        coll += iters * m.Kp * 8  # the topic-sum delta allreduce (fp64) of every iteration
+    coll = _window_bytes(m.metrics)  # pull / push / rotate and the topic-delta allreduce
+    breakdown = _coll_breakdown(m.metrics, iters, comm, torch)
     ll = m.log_likelihood(1 + iters)
     nt = torch.tensor([float(n)], dtype=torch.float64, device=comm.device)
     if P > 1:
@@ -551,7 +602,8 @@ def _lda_run(args, comm, torch, local_server: bool, iters: int) -> dict:
     n = float(nt.item())
     out = {"tokens_per_sec": round(n / dt, 1), "s_per_iter": round(dt / iters, 6),
            "median_s_per_iter": round(st["median"], 6), "iter_s": st, "iters": iters,
-           "sync_bytes_per_iter": int(coll / max(iters, 1)), "loglik_end": ll, "setup_s": round(setup_s, 3),
+           "sync_bytes_per_iter": int(coll / max(iters, 1)), "collectives": breakdown,
+           "loglik_end": ll, "setup_s": round(setup_s, 3),
            "local_server": bool(getattr(m, "local_server", False)), "tokens_per_iter": int(n) // iters,
            "comm_mode": getattr(m, "comm_mode", "rotation"), "fused_rows": bool(getattr(m, "fused", False)),
            "sampler": "sparse" if getattr(m, "sparse", False) else "dense"}

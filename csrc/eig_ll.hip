@@ -130,7 +130,7 @@ template <int RW, int NBP>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void sytrd_ll_kernel(
     const double* __restrict__ A, long lda, int n, double* __restrict__ dout, double* __restrict__ eout,
     double* __restrict__ vout, long ldv, double* __restrict__ tauout, int* __restrict__ ws, u64* __restrict__ gran_,
-    long long* __restrict__ stamps) {
+    long long* __restrict__ stamps, long long* __restrict__ trace) {
   static_assert(1 + RW + 2 * (NBP - 1) <= kSlots, "butterfly slots");
   constexpr int kBc = 1 + RW + 2 * NBP;  // alpha, A_ps[r][k+1] (own rows), V[k+1][l], W[k+1][l]
   __shared__ double sP[kT / 64][kSlots];
@@ -186,9 +186,36 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   };
 
+  // diagnostic (trace != nullptr): thread 0 of every workgroup records the chip-wide 100 MHz
+  // clock at four points of every 64th column: trace[(k / 64) NB 4 + b 4 + {start, p stored,
+  // exchange done, step done}]
+  const bool tr = trace != nullptr && tid == 0;
+  auto tmark = [&](int k, int i) {
+    if (tr && (k & 63) == 0) trace[((long)(k >> 6) * NB + b) * 4 + i] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+
+  // A_ps[k+1][own indices] for the coming step, prefetched one step ahead as raw granule pairs
+  // (checked only in that step's exchange, so the loads fly under its local phase)
+  u64 clo[kIPT], chi[kIPT];
+  auto prefetch_col = [&](int kk) {
+    const int pn = kk / NBP, jn = kk % NBP;
+    const gu64* gc = gran + kOffCol + ((long)(pn & 1) * NBP + jn) * kN * 2;
+#pragma unroll
+    for (int m = 0; m < kIPT; ++m) {
+      const int t = t0 + m;
+      clo[m] = chi[m] = 0;
+      if (pn > 0 && t >= kk + 1 && t < n) {
+        clo[m] = gload(gc + 2 * t);
+        chi[m] = gload(gc + 2 * t + 1);
+      }
+    }
+  };
+  prefetch_col(0);
+
   for (int k = 0; k + 2 < n; ++k) {
     const int j = k % NBP, panel = k / NBP, par = k & 1;
     if (r0 + RW - 1 < k + 1 && !last) return;  // every own row reduced: nobody polls us again
+    tmark(k, 0);
     const int k1 = k + 1;
     // ---- S1: the owner of index k+1 posts alpha, A_ps[own rows][k+1], V / W[k+1][l < j]
     if (tid == k1 / kIPT) {
@@ -291,6 +318,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       if (h == 0) put_d(gran + kOffPV + (long)par * kMaxWG * 2 + 2L * b, (unsigned)k1, pv);
     }
     mark(1);
+    tmark(k, 1);
     // ---- S3: the exchange. p_k at own indices, A_ps[k+1][own indices], partial p.v sums
     double p[kIPT], col[kIPT];
     {
@@ -298,44 +326,73 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       const gu64* gc = gran + kOffCol + ((long)(panel & 1) * NBP + j) * kN * 2;
       const gu64* gv = gran + kOffPV + (long)par * kMaxWG * 2;
       const int blo = k1 / RW;
-      double pvs = 0.0;
+      double pvs = 0.0, pvq[kMaxWG / 64];
+      // what this lane still waits for (bit m: p[m], bit 4 + m: col[m], bit 8 + q: partial q);
+      // a granule pair once seen with its tag is kept and never re-read
+      unsigned need = 0;
+#pragma unroll
+      for (int m = 0; m < kIPT; ++m) {
+        const int t = t0 + m;
+        p[m] = col[m] = 0.0;
+        if (t >= k1 && t < n) {
+          need |= 1u << m;
+          if (panel == 0)
+            col[m] = A[t + (long)k1 * lda];
+          else if (tagged(clo[m], chi[m], (unsigned)panel + 1))
+            col[m] = join_d(clo[m], chi[m]);
+          else
+            need |= 1u << (4 + m);
+        }
+      }
+      if (wv == 0) {
+#pragma unroll
+        for (int q = 0; q < kMaxWG / 64; ++q) {
+          pvq[q] = 0.0;
+          const int bb = lane + 64 * q;
+          if (bb >= blo && bb < NB) need |= 1u << (8 + q);
+        }
+      }
       long spins = 0;
       for (;;) {
-        bool ok = true;
 #pragma unroll
         for (int m = 0; m < kIPT; ++m) {
           const int t = t0 + m;
-          p[m] = col[m] = 0.0;
-          if (t >= k1 && t < n) {
+          if (need & (1u << m)) {
             const u64 lo = gload(gp + 2 * t), hi = gload(gp + 2 * t + 1);
-            ok &= tagged(lo, hi, (unsigned)k1);
-            p[m] = join_d(lo, hi);
-            if (panel == 0) {
-              col[m] = A[t + (long)k1 * lda];
-            } else {
-              const u64 clo = gload(gc + 2 * t), chi = gload(gc + 2 * t + 1);
-              ok &= tagged(clo, chi, (unsigned)panel + 1);
-              col[m] = join_d(clo, chi);
+            if (tagged(lo, hi, (unsigned)k1)) {
+              p[m] = join_d(lo, hi);
+              need &= ~(1u << m);
+            }
+          }
+          if (need & (1u << (4 + m))) {
+            const u64 lo = gload(gc + 2 * t), hi = gload(gc + 2 * t + 1);
+            if (tagged(lo, hi, (unsigned)panel + 1)) {
+              col[m] = join_d(lo, hi);
+              need &= ~(1u << (4 + m));
             }
           }
         }
         if (wv == 0) {
-          pvs = 0.0;
 #pragma unroll
           for (int q = 0; q < kMaxWG / 64; ++q) {
-            const int bb = lane + 64 * q;
-            if (bb >= blo && bb < NB) {
+            if (need & (1u << (8 + q))) {
+              const int bb = lane + 64 * q;
               const u64 lo = gload(gv + 2 * bb), hi = gload(gv + 2 * bb + 1);
-              ok &= tagged(lo, hi, (unsigned)k1);
-              pvs += join_d(lo, hi);
+              if (tagged(lo, hi, (unsigned)k1)) {
+                pvq[q] = join_d(lo, hi);
+                need &= ~(1u << (8 + q));
+              }
             }
           }
         }
+        const bool ok = need == 0;
         if (stamp) ++ph[5];
         if (__all(ok)) break;
         if (spin_fail(spins, err)) return;
       }
       if (wv == 0) {
+#pragma unroll
+        for (int q = 0; q < kMaxWG / 64; ++q) pvs += pvq[q];
         pvs = wave_sum_d_dpp(pvs);
         if (lane == 0) sB2[0] = pvs;
       }
@@ -346,6 +403,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     mark(2);
+    tmark(k, 2);
     __syncthreads();
     const double c = 0.5 * tau * sB2[0];
 #pragma unroll
@@ -389,6 +447,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     mark(3);
+    tmark(k, 3);
     if (k + 3 >= n) {  // last Householder step: e[n-2] = x[n-1], d[n-1] from A_ps
       if (last) {
 #pragma unroll
@@ -435,21 +494,24 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             a[i][m] = y;
           }
         }
-        // rows k0n + 1 .. k0n + NBP of the new A_ps that this workgroup owns
+        // columns k0n + 1 .. k0n + NBP of the new A_ps at this workgroup's rows (by symmetry
+        // the rows the consumers need): posted by the threads owning those column indices,
+        // RW values each, so no workgroup bursts a whole row
         const int np = panel + 1;
         gu64* gc = gran + kOffCol + (long)(np & 1) * NBP * kN * 2;
 #pragma unroll
-        for (int i = 0; i < RW; ++i) {
-          const int r = r0 + i, jj = r - (k0n + 1);
-          if (jj < 0 || jj >= NBP || r >= n) continue;
+        for (int m = 0; m < kIPT; ++m) {
+          const int c = t0 + m, jj = c - (k0n + 1);
+          if (jj < 0 || jj >= NBP || c >= n) continue;
 #pragma unroll
-          for (int m = 0; m < kIPT; ++m) {
-            const int t = t0 + m;
-            if (t >= r && t < n) put_d(gc + ((long)jj * kN + t) * 2, (unsigned)np + 1, a[i][m]);
+          for (int i = 0; i < RW; ++i) {
+            const int r = r0 + i;
+            if (r >= c && r < n) put_d(gc + ((long)jj * kN + r) * 2, (unsigned)np + 1, a[i][m]);
           }
         }
       }
     }
+    prefetch_col(k + 1);
     mark(4);
   }
   if (stamp)
@@ -458,10 +520,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 
 template <int RW, int NBP>
 int launch_ll(const double* A, long lda, int n, double* d, double* e, double* V, long ldv, double* tau, int* ws,
-              u64* gran, long long* stamps, hipStream_t s) {
+              u64* gran, long long* stamps, long long* trace, hipStream_t s) {
   const int nb = (n + RW - 1) / RW;
   if (nb > kMaxWG) return HARP_EUNSUPPORTED;
-  sytrd_ll_kernel<RW, NBP><<<dim3((unsigned)nb), dim3(kT), 0, s>>>(A, lda, n, d, e, V, ldv, tau, ws, gran, stamps);
+  sytrd_ll_kernel<RW, NBP><<<dim3((unsigned)nb), dim3(kT), 0, s>>>(A, lda, n, d, e, V, ldv, tau, ws, gran, stamps,
+                                                                                          trace);
   return harp_launch_status();
 }
 
@@ -469,6 +532,10 @@ int launch_ll(const double* A, long lda, int n, double* d, double* e, double* V,
 
 constexpr int kLLRW = 8, kLLNBP = 4;
 static long long* g_ll_stamps = nullptr;  // diagnostic phase cycles (harp_sytrd_ll_stamps)
+static long long* g_ll_trace = nullptr;   // diagnostic per-workgroup clock marks (harp_sytrd_ll_trace)
+// diagnostic: the next launches record every workgroup's 100 MHz clock at four points of every
+// 64th column (ceil((n - 2) / 64) x workgroups x 4 int64)
+HARP_EXPORT void harp_sytrd_ll_trace(long long* trace) { g_ll_trace = trace; }
 // diagnostic: the next launches sum the last workgroup's cycles per phase into stamps[0..5]
 HARP_EXPORT void harp_sytrd_ll_stamps(long long* stamps) { g_ll_stamps = stamps; }
 
@@ -485,5 +552,5 @@ HARP_EXPORT int harp_sytrd_ll_workgroups(int n) { return n < 1 ? 0 : (n + kLLRW 
 HARP_EXPORT int harp_sytrd_ll(const double* A, long lda, int n, double* d, double* e, double* V, long ldv, double* tau,
                               int* ws, unsigned long long* gran, hipStream_t s) {
   if (n < 1 || n > kN || lda < n || !ws || !gran || !d || !e || (V && ldv < n)) return HARP_EBADARG;
-  return launch_ll<kLLRW, kLLNBP>(A, lda, n, d, e, V, ldv, tau, ws, gran, g_ll_stamps, s);
+  return launch_ll<kLLRW, kLLNBP>(A, lda, n, d, e, V, ldv, tau, ws, gran, g_ll_stamps, g_ll_trace, s);
 }

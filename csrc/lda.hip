@@ -282,7 +282,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6 + XW < 8 
   // int64: start, length | sole << 31 | word << 32 (sole: the word's only chunk), the word's
   // pull-slot and push-slot offsets (fused rows; else 0) -- one scalar load instead of the
   // chain bounds -> word -> slot offsets.
-  const bool lptm = lpt != nullptr && !det;
+  // det == 2: the one wave walks the descriptors in their (longest-first) order -- the
+  // production schedule, sequentially (the exact-distribution test)
+  const bool lptm = lpt != nullptr && det != 1;
   const unsigned seed32 = hash32((unsigned)seed ^ hash32((unsigned)(seed >> 32) ^ 0x85EBCA6Bu));
   for (long r = 0;; ++r) {
 #ifdef HARP_LDA_STAMPS
@@ -1275,8 +1277,9 @@ static int lda_cgs_impl(const int* tdoc, const int* tword, int* tz, const long* 
   // variant 0: six waves per SIMD; 3: seven (the default). Round 1's variants (1: a
   // float-row prefetch; 2, 4, 5: other forced occupancies) measured slower
   // (profiles/r1_lda/occupancy) and are no longer built.
-  // variant | 0x100: deterministic one-wave sampling (tests)
-  const int det = (variant & 0x100) ? 1 : 0;
+  // variant | 0x100: deterministic one-wave sampling in chunk order (tests); | 0x200: one
+  // wave in the chunk-descriptor order of lpt (tests of the production schedule)
+  const int det = (variant & 0x200) ? 2 : (variant & 0x100) ? 1 : 0;
   variant &= 0xff;
   if (K <= 0 || K > 1024 || ldw % 4 || (variant != 0 && variant != 3)) return HARP_EBADARG;
 #define CGS_ARGS tdoc, tword, tz, chunk_start, nchunks

@@ -261,7 +261,8 @@ class LDACollectiveMapper(CollectiveMapper):
                 self.rot.start(k, self.schedules[k].rotation_map(it, s))
         # topic sums: allreduce the iteration's deltas (LDAMPCollectiveMapper.java:439-461)
         if P > 1:
-            dt = reduce_partials(self.comm, {"d": delta_total}, dtype=torch.float64)["d"].round().to(torch.int32)
+            with self.metrics.time_collective("allreduce", "lda", "topic-delta", self.Kp * 8, self.device):
+                dt = reduce_partials(self.comm, {"d": delta_total}, dtype=torch.float64)["d"].round().to(torch.int32)
         else:
             dt = delta_total
         self.nk += dt
@@ -627,7 +628,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
                  if n else torch.zeros(self.Kp, dtype=torch.int32, device=self.device))
             self._timed_ps("push", lambda: self.ps.push_payload(self._glob_rows()), push_b)
             if self.get_num_workers() > 1:
-                d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
+                with self.metrics.time_collective("allreduce", "lda", "topic-delta", self.Kp * 8, self.device):
+                    d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
             self.nk += d
             return n
         if self.ps is not None:
@@ -649,7 +651,8 @@ class LDAPushPullMapper(LDACollectiveMapper):
             slab -= self.before.view(-1, self.Kp)
             self._push_delta()
         if self.get_num_workers() > 1:
-            d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
+            with self.metrics.time_collective("allreduce", "lda", "topic-delta", self.Kp * 8, self.device):
+                d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
         self.nk += d
         return n
 

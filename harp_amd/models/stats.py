@@ -120,13 +120,30 @@ def covariance_finalize(p: Dict[str, torch.Tensor], bias: bool = False) -> Dict[
     return {"mean": mean, "covariance": cov}
 
 
+def _timed(metrics, kind: str, op: str, nbytes: int, device):
+    """``metrics.time_collective`` (HIP events on GPUs) when a Metrics object is given."""
+    import contextlib
+
+    if metrics is None:
+        return contextlib.nullcontext()
+    return metrics.time_collective(kind, "pca", op, nbytes, device)
+
+
 def covariance(X, comm: Optional[Communicator] = None, bias: bool = False,
-               dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
-    return covariance_finalize(reduce_partials(_local(comm), covariance_partial(X, dtype), dtype=torch.float64), bias)
+               dtype: Optional[str] = None, metrics=None) -> Dict[str, torch.Tensor]:
+    """``metrics`` (optional :class:`utils.metrics.Metrics`): the partial-result allreduce is
+    recorded as an "allreduce" collective (op "gram") with its bytes and stream time."""
+    comm = _local(comm)
+    part = covariance_partial(X, dtype)
+    nbytes = sum(v.numel() for v in part.values()) * 8 if comm.world_size > 1 else 0
+    with _timed(metrics, "allreduce", "gram", nbytes, comm.device):
+        red = reduce_partials(comm, part, dtype=torch.float64)
+    return covariance_finalize(red, bias)
 
 
-def correlation(X, comm: Optional[Communicator] = None, dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
-    r = covariance(X, comm, dtype=dtype)
+def correlation(X, comm: Optional[Communicator] = None, dtype: Optional[str] = None,
+                metrics=None) -> Dict[str, torch.Tensor]:
+    r = covariance(X, comm, dtype=dtype, metrics=metrics)
     sd = r["covariance"].diagonal().clamp_min(0).sqrt()
     r["correlation"] = r["covariance"] / torch.outer(sd, sd).clamp_min(1e-300)
     return r
@@ -180,7 +197,7 @@ def low_order_moments(X: torch.Tensor, comm: Optional[Communicator] = None,
 
 
 # ------------------------------------------------------------------ PCA
-def pca_step2(corr: torch.Tensor, comm: Optional[Communicator] = None):
+def pca_step2(corr: torch.Tensor, comm: Optional[Communicator] = None, metrics=None):
     """Step 2 of the correlation method on the master (PCADaalCollectiveMapper.java:136-154):
     eigenvalues AND eigenvectors of the d x d fp64 correlation matrix -- on a GPU the one-XCD
     reduction + divide and conquer of ``ops.eig.eigh`` -- then broadcast. Returns
@@ -195,23 +212,25 @@ def pca_step2(corr: torch.Tensor, comm: Optional[Communicator] = None):
         packed = torch.cat([evals.reshape(1, d), evecs]).contiguous()
     else:
         packed = None
-    packed = broadcast_tensor(comm, packed, (d + 1, d), torch.float64).to(dev)
+    with _timed(metrics, "broadcast", "eigvecs", (d + 1) * d * 8 if comm.world_size > 1 else 0, comm.device):
+        packed = broadcast_tensor(comm, packed, (d + 1, d), torch.float64).to(dev)
     return packed[0], packed[1:]
 
 
 def pca(X, comm: Optional[Communicator] = None, method: str = "correlation",
-        n_components: Optional[int] = None, dtype: Optional[str] = None) -> Dict[str, torch.Tensor]:
+        n_components: Optional[int] = None, dtype: Optional[str] = None, metrics=None) -> Dict[str, torch.Tensor]:
     """PCA of the (standardized) data: eigenvalues descending + eigenvectors (rows).
 
     ``correlation``: eigen-decomposition of the distributed correlation matrix (``X`` may
     be a :class:`ops.linalg.FeatureMajor` block: the one-pass MFMA SYRK path).
     ``svd``: z-score the data with global moments, distributed TSQR, SVD of R
     (the DAAL svdDense method); both yield the correlation-PCA spectrum. ``dtype``: the
-    step-1 precision (see :func:`covariance`)."""
+    step-1 precision (see :func:`covariance`). ``metrics``: the correlation method's Gram
+    allreduce and eigenvector broadcast are recorded as collectives (bench attribution)."""
     comm = _local(comm)
     if method == "correlation":
-        r = correlation(X, comm, dtype=dtype)
-        evals, evecs = pca_step2(r["correlation"], comm)
+        r = correlation(X, comm, dtype=dtype, metrics=metrics)
+        evals, evecs = pca_step2(r["correlation"], comm, metrics=metrics)
         order = torch.argsort(evals, descending=True)
         evals, evecs = evals[order], evecs[:, order].t()
     elif method == "svd":

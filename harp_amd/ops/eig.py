@@ -48,6 +48,7 @@ _lib.register({
     "harp_sytrd_ll_gran_words": [],
     "harp_sytrd_ll_workgroups": [_lib.c_int],
     "harp_sytrd_ll_stamps": [_lib.c_void_p],
+    "harp_sytrd_ll_trace": [_lib.c_void_p],
     # A, lda, n, d, e, V, ldv, tau, ws, gran, stream
     "harp_sytrd_ll": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                       _lib.c_long, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],

@@ -327,8 +327,10 @@ def cgs_sample(tdoc, tword, tz, chunks, ndk, nwk, nk, K: int, alpha: float, beta
         st = _lib.kernels().harp_lda_cgs(tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(),
                                          chunks.numel() - 1, ndk.data_ptr(), ndk.stride(0), _bits(ndk), nwk.data_ptr(),
                                          nwk.stride(0), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
-                                         seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0),
-                                         _lib.ptr(None if deterministic else lpt_desc(chunks, tword)), _lib.stream_ptr(dev))
+                                         seed & 0xFFFFFFFFFFFFFFFF,
+                                         SAMPLER_VARIANT | (0x200 if deterministic == "lpt" else 0x100 if deterministic else 0),
+                                         _lib.ptr(lpt_desc(chunks, tword) if deterministic in (False, "lpt") else None),
+                                         _lib.stream_ptr(dev))
         _lib.check(st, "lda_cgs")
         return delta
     delta = _cpu_sweep(tdoc, tword, tz, ndk, nwk, nk, K, alpha, beta, vbeta, seed)
@@ -437,7 +439,9 @@ def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: 
     word-row deltas written into the (zeroed) push payload -- no dense local table
     (``parallel.sparse_ps.SparseRowPS.row_slots`` gives ``slots``). Dense sampler (``ndk``,
     K <= 1024), or with ``doc_index`` (and no ``ndk``) the sparse doc-span sampler
-    (K <= :data:`MAX_TOPICS`). Returns the topic-count delta."""
+    (K <= :data:`MAX_TOPICS`). Returns the topic-count delta. ``deterministic``: True -- one
+    wave, chunks in index order; "lpt" (dense sampler) -- one wave walking the production
+    longest-first chunk descriptors in order (sole-chunk flags and slot offsets included)."""
     dev = tz.device
     poff, pcap, qoff, qcap = slots
     if doc_index is not None:
@@ -470,9 +474,10 @@ def cgs_sample_ps(tdoc, tword, tz, chunks, ndk, nk, K: int, alpha: float, beta: 
     st = _lib.kernels().harp_lda_cgs_ps(
         tdoc.data_ptr(), tword.data_ptr(), tz.data_ptr(), chunks.data_ptr(), chunks.numel() - 1, ndk.data_ptr(),
         ndk.stride(0), _bits(ndk), inv.data_ptr(), delta.data_ptr(), K, float(alpha), float(beta),
-        seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x100 if deterministic else 0), pull_buf.data_ptr(),
-        poff.data_ptr(), pcap.data_ptr(), push_buf.data_ptr(), qoff.data_ptr(), qcap.data_ptr(), overflow.data_ptr(),
-        _lib.ptr(None if deterministic else lpt_desc(chunks, tword, slots)), _lib.stream_ptr(dev))
+        seed & 0xFFFFFFFFFFFFFFFF, SAMPLER_VARIANT | (0x200 if deterministic == "lpt" else 0x100 if deterministic else 0),
+        pull_buf.data_ptr(), poff.data_ptr(), pcap.data_ptr(), push_buf.data_ptr(), qoff.data_ptr(), qcap.data_ptr(),
+        overflow.data_ptr(),
+        _lib.ptr(lpt_desc(chunks, tword, slots) if deterministic in (False, "lpt") else None), _lib.stream_ptr(dev))
     _lib.check(st, "lda_cgs_ps")
     return delta
 

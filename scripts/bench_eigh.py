@@ -52,6 +52,33 @@ def main():
     k.harp_sytrd_ll_stamps(None)
     rec["ll_phase_cycles_per_col"] = [round(v / max(n - 2, 1), 1) for v in st.tolist()[:5]]
     rec["ll_polls_per_col"] = round(st.tolist()[5] / max(n - 2, 1), 2)
+    # per-workgroup clock marks (100 MHz) at every 64th column: skew of the p stores across
+    # workgroups vs the time from the LAST store to each workgroup's exchange done
+    nwg = int(k.harp_sytrd_ll_workgroups(n))
+    ns = (n - 2 + 63) // 64
+    trc = torch.zeros(ns * nwg * 4, dtype=torch.int64, device=dev)
+    k.harp_sytrd_ll_trace(trc.data_ptr())
+    E.sytrd_ll(C)
+    torch.cuda.synchronize()
+    k.harp_sytrd_ll_trace(None)
+    trc = trc.view(ns, nwg, 4).cpu().double() * 10.0  # ns
+    rows = []
+    for si in range(ns):
+        kk = si * 64
+        live = [b for b in range(nwg) if 8 * b + 7 >= kk + 1 or b == nwg - 1]
+        t = trc[si, live]
+        if float(t[:, 0].min()) <= 0:
+            continue
+        st_ = t[:, 1]
+        rows.append({"k": kk, "wgs": len(live), "start_skew_ns": round(float(t[:, 0].max() - t[:, 0].min())),
+                     "store_skew_ns": round(float(st_.max() - st_.min())),
+                     "last_store_to_done_ns": [round(float((t[:, 2] - st_.max()).min())),
+                                               round(float((t[:, 2] - st_.max()).median())),
+                                               round(float((t[:, 2] - st_.max()).max()))],
+                     "s1_ns_median": round(float((t[:, 1] - t[:, 0]).median())),
+                     "s4_ns_median": round(float((t[:, 3] - t[:, 2]).median())),
+                     "step_ns": round(float(t[:, 3].max() - t[:, 0].min()))})
+    rec["ll_trace"] = rows
 
     def fused():
         nb = int(k.harp_eig_workgroups(n, E.NB_DEFAULT))

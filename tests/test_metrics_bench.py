@@ -194,6 +194,22 @@ def _check_full_record(rec, P, slices=1):
     assert p["eig_s"] is not None and p["eigvec_orth_err"] <= 1e-10 and p["eig_residual"] <= 1e-10
     lda = rec["lda"]
     assert lda["iter_s"]["n"] == 10 and lda["tokens_per_sec"] > 0 and lda["local_server"] is False
+    # every nested record attributes its time per collective kind
+    def kinds(sub, need):
+        c = sub["collectives"]
+        for k in need:
+            assert k in c, (k, c)
+            e = c[k]
+            assert e["calls_per_iter"] > 0 and e["ms_per_iter"] >= 0 and e["bytes_per_iter"] >= 0, (k, e)
+            if e["bytes_per_iter"] > 0:  # (rotate_wait is the exposed part of a transfer: no ideal)
+                assert "gbps" in e and (k == "rotate_wait" or "ideal_ms_per_iter" in e), (k, e)
+        return c
+    kinds(lda, ("pull", "push", "allreduce"))
+    assert lda["collectives"]["allreduce"]["calls_per_iter"] == 1.0
+    pc = kinds(p, ("allreduce", "broadcast"))
+    assert pc["allreduce"]["calls_per_iter"] == 1.0 and pc["broadcast"]["calls_per_iter"] == 1.0
+    kinds(s, ("rotate_wait",))
+    assert "allreduce" in rec["collectives"]
 
 
 @pytest.mark.slow

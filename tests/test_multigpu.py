@@ -236,3 +236,61 @@ def test_planned_push_pull_over_rccl():
         assert all(torch.equal(sp_push[i].cpu(), dn_push[i].cpu()) for i in dn_push)
         for x, y in zip(sp_pull, dn_pull):
             assert all(torch.equal(x[i].cpu(), y[i].cpu()) for i in y)
+
+
+def _pca_rccl(comm, n_per, d):
+    from harp_amd.models import stats as ST
+    from harp_amd.utils.metrics import Metrics
+
+    P, r = comm.world_size, comm.rank
+    blocks = [torch.rand((n_per, d), generator=torch.Generator().manual_seed(100 + q)) for q in range(P if P > 1 else 3)]
+    X = (blocks[r] if P > 1 else torch.cat(blocks)).to(comm.device)
+    met = Metrics(rank=r, world=P)
+    res = ST.pca(X, comm, dtype="bf16", metrics=met)
+    kinds = sorted({c["kind"] for c in met.collectives})
+    return res["eigenvalues"].cpu(), res["eigenvectors"].cpu(), kinds
+
+
+@pytest.mark.skipif(NGPU < 3, reason=f"needs >= 3 GPUs ({NGPU} visible)")
+def test_pca_over_rccl_all_ranks_hold_the_same_eigenpairs():
+    """stats.pca over RCCL: the MFMA SYRK partials allreduced, step 2 on the
+    master, its eigenvalues + eigenvectors broadcast -- every rank holds bit-identical
+    eigenpairs, equal to one rank's PCA of the concatenated rows (bf16 operands, fp32
+    accumulation: summation-order differences only), and both collectives are recorded."""
+    d, n_per = 200, 20000
+    one = launch(_pca_rccl, 1, args=(n_per, d), backend="nccl", timeout=300)[0]
+    res = launch(_pca_rccl, 3, args=(n_per, d), backend="nccl", timeout=300)
+    for lam, V, kinds in res:
+        assert torch.equal(lam, res[0][0]) and torch.equal(V, res[0][1])
+        assert kinds == ["allreduce", "broadcast"]
+        assert float((V @ V.t() - torch.eye(d, dtype=V.dtype)).abs().max()) < 1e-12
+    assert float((res[0][0] - one[0]).abs().max()) < 1e-5
+
+
+def _lda_fused_rccl(comm, fused):
+    from harp_amd.models.lda import LDAConfig, LDAPushPullMapper, synthetic_corpus
+    from harp_amd.runtime.mapper import KeyValReader
+
+    toks = synthetic_corpus(3000, 2500, 20, 40, seed=13)
+    cfg = LDAConfig(num_topics=256, alpha=0.1, beta=0.01, iterations=4, print_interval=4, block_words=256,
+                    sparse_comm="on", local_server=False, seed=3, deterministic=True, fused_rows=fused)
+    m = LDAPushPullMapper(comm, cfg, 3000, 2500, toks)
+    m.run(KeyValReader([]))
+    return {"tz": m.tz.cpu(), "ok": m.check_counts(), "fused": m.result["fused_rows"], "nk": m.nk.cpu(),
+            "dedup": m.ps is not None and m.ps._dedup is not None}
+
+
+@pytest.mark.skipif(NGPU < 3, reason=f"needs >= 3 GPUs ({NGPU} visible)")
+def test_lda_fused_sparse_ps_over_rccl_three_ranks():
+    """LDA push-pull with fused parameter-server rows over RCCL at P = 3: rows
+    wanted by several ranks are encoded once and fanned out by copy_slots; in the
+    deterministic sampler the fused run takes exactly the unfused run's trajectory, counts
+    stay exact, and every rank holds the same topic sums."""
+    a = launch(_lda_fused_rccl, 3, args=(True,), backend="nccl", timeout=300)
+    b = launch(_lda_fused_rccl, 3, args=(False,), backend="nccl", timeout=300)
+    assert any(r["dedup"] for r in a), "no owner-side dedup (copy_slots) exercised"
+    for ra, rb in zip(a, b):
+        assert ra["fused"] and not rb["fused"]
+        assert ra["ok"] and rb["ok"]
+        assert torch.equal(ra["tz"], rb["tz"])
+        assert torch.equal(ra["nk"], a[0]["nk"])
