@@ -453,7 +453,8 @@ def bench_sgd(args, comm, torch):
         "collectives": coll,
         "rotation_strides": [s.stride for s in m.schedules],
         "xcd_placement": placement,
-        "atomic_writeback": cfg.atomic,
+        "atomic_writeback": m.atomic,
+        "hot_items": m.hot_items,
         "blocks_per_xcd": m.bpx,
         "cell_sum_p2": round(getattr(m, "cell_sum_p2", 0.0), 6),  # the concurrency cap's input (SGDConfig)
         "train_rmse": round(train_rmse, 6),

@@ -113,6 +113,17 @@ __device__ __forceinline__ int butterfly_slot(int lane) {
   return ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
 }
 
+// 1 / x by v_rcp_f64 and two Newton steps (the IEEE divide is a ~10-instruction dependent chain)
+__device__ __forceinline__ double rcp_d(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+// workgroup barrier for LDS traffic only: __syncthreads() also drains vmcnt, i.e. waits for
+// the granule stores and for the column prefetch issued a phase earlier
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ bool spin_fail(long& spins, int* err) {
   if (++spins > kSpinLimit) {
     __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -133,9 +144,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     long long* __restrict__ stamps, long long* __restrict__ trace) {
   static_assert(1 + RW + 2 * (NBP - 1) <= kSlots, "butterfly slots");
   constexpr int kBc = 1 + RW + 2 * NBP;  // alpha, A_ps[r][k+1] (own rows), V[k+1][l], W[k+1][l]
-  __shared__ double sP[kT / 64][kSlots];
+  __shared__ double sP[2][kT / 64][kSlots];  // parity: no barrier separates a column's read from the next write
   __shared__ double sBc[2][kBc];
-  __shared__ double sB2[2 + 2 * RW];    // p.v total, p[k+1], then p and v of the own rows
+  __shared__ double sB2[2 + 2 * RW];    // (2 unused), then p and v of the own rows
   __shared__ double sRow[RW][NBP][2];   // V / W of the own rows over the panel
   gu64* gran = (gu64*)gran_;
   int* err = ws + 2;
@@ -211,6 +222,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   };
   prefetch_col(0);
+  // the loop's first uses of a / x must not look like they wait on loads still in flight
+  // (the waitcnt pass merges the loop header conservatively: one drain here, none per column)
+  __builtin_amdgcn_s_waitcnt(0);
 
   for (int k = 0; k + 2 < n; ++k) {
     const int j = k % NBP, panel = k / NBP, par = k & 1;
@@ -252,21 +266,21 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           }
       }
       const double tot = butterfly16(s, lane);
-      if ((lane & 3) == 0) sP[wv][butterfly_slot(lane)] = tot;
+      if ((lane & 3) == 0) sP[par][wv][butterfly_slot(lane)] = tot;
     } else if (lane < kSlots) {
-      sP[wv][lane] = 0.0;
+      sP[par][wv][lane] = 0.0;
     }
     mark(0);
-    __syncthreads();
+    lds_barrier();
     double tot = 0.0;
-    if (lane < kSlots) tot = (sP[0][lane] + sP[1][lane]) + (sP[2][lane] + sP[3][lane]);
+    if (lane < kSlots) tot = (sP[par][0][lane] + sP[par][1][lane]) + (sP[par][2][lane] + sP[par][3][lane]);
     const double sigma = readlane_d(tot, 0);
     const double alpha = sBc[par][0];
     double beta = alpha, tau = 0.0, scl = 0.0;
     if (sigma != 0.0) {
       beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-      tau = (beta - alpha) / beta;
-      scl = 1.0 / (alpha - beta);
+      tau = (beta - alpha) * rcp_d(beta);
+      scl = rcp_d(alpha - beta);
     }
     const double gam = sigma != 0.0 ? -beta * scl : 1.0;  // v = scl x' + gam e_{k+1}
     double v[kIPT];
@@ -320,7 +334,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     mark(1);
     tmark(k, 1);
     // ---- S3: the exchange. p_k at own indices, A_ps[k+1][own indices], partial p.v sums
-    double p[kIPT], col[kIPT];
+    double p[kIPT], col[kIPT], pv_tot, p_k1;
     {
       const gu64* gp = gran + kOffP + (long)par * kN * 2;
       const gu64* gc = gran + kOffCol + ((long)(panel & 1) * NBP + j) * kN * 2;
@@ -344,14 +358,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             need |= 1u << (4 + m);
         }
       }
-      if (wv == 0) {
 #pragma unroll
-        for (int q = 0; q < kMaxWG / 64; ++q) {
-          pvq[q] = 0.0;
-          const int bb = lane + 64 * q;
-          if (bb >= blo && bb < NB) need |= 1u << (8 + q);
-        }
+      for (int q = 0; q < kMaxWG / 64; ++q) {
+        pvq[q] = 0.0;
+        const int bb = lane + 64 * q;
+        if (bb >= blo && bb < NB) need |= 1u << (8 + q);
       }
+      double pk1 = 0.0;  // p[k+1]: every lane reads the same granule pair
+      need |= 1u << 12;
       long spins = 0;
       for (;;) {
 #pragma unroll
@@ -372,17 +386,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             }
           }
         }
-        if (wv == 0) {
 #pragma unroll
-          for (int q = 0; q < kMaxWG / 64; ++q) {
-            if (need & (1u << (8 + q))) {
-              const int bb = lane + 64 * q;
-              const u64 lo = gload(gv + 2 * bb), hi = gload(gv + 2 * bb + 1);
-              if (tagged(lo, hi, (unsigned)k1)) {
-                pvq[q] = join_d(lo, hi);
-                need &= ~(1u << (8 + q));
-              }
+        for (int q = 0; q < kMaxWG / 64; ++q) {
+          if (need & (1u << (8 + q))) {
+            const int bb = lane + 64 * q;
+            const u64 lo = gload(gv + 2 * bb), hi = gload(gv + 2 * bb + 1);
+            if (tagged(lo, hi, (unsigned)k1)) {
+              pvq[q] = join_d(lo, hi);
+              need &= ~(1u << (8 + q));
             }
+          }
+        }
+        if (need & (1u << 12)) {
+          const u64 lo = gload(gp + 2 * k1), hi = gload(gp + 2 * k1 + 1);
+          if (tagged(lo, hi, (unsigned)k1)) {
+            pk1 = join_d(lo, hi);
+            need &= ~(1u << 12);
           }
         }
         const bool ok = need == 0;
@@ -390,22 +409,18 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         if (__all(ok)) break;
         if (spin_fail(spins, err)) return;
       }
-      if (wv == 0) {
 #pragma unroll
-        for (int q = 0; q < kMaxWG / 64; ++q) pvs += pvq[q];
-        pvs = wave_sum_d_dpp(pvs);
-        if (lane == 0) sB2[0] = pvs;
-      }
-      if (tid == k1 / kIPT) {
-#pragma unroll
-        for (int m = 0; m < kIPT; ++m)
-          if (t0 + m == k1) sB2[1] = p[m];
-      }
+      for (int q = 0; q < kMaxWG / 64; ++q) pvs += pvq[q];
+      pv_tot = wave_sum_d_dpp(pvs);
+      p_k1 = pk1;
     }
     mark(2);
     tmark(k, 2);
-    __syncthreads();
-    const double c = 0.5 * tau * sB2[0];
+    // the only barrier left in the column's second half: at a panel end every thread reads
+    // the own rows' p and v (sB2) that their owners wrote after this column's first barrier
+    const bool pend = j == NBP - 1 && k + 3 < n;
+    if (pend) lds_barrier();
+    const double c = 0.5 * tau * pv_tot;
 #pragma unroll
     for (int m = 0; m < kIPT; ++m) Ww[j][m] = t0 + m >= k1 ? fma(-c, v[m], p[m]) : 0.0;
     if (h >= 0 && h < kOwn) {
@@ -423,7 +438,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int l = 0; l < NBP; ++l)
       if (l == j) {
         Vk[l] = 1.0;
-        Wk[l] = fma(-c, 1.0, sB2[1]);
+        Wk[l] = fma(-c, 1.0, p_k1);
       }
     double xn[kIPT];
 #pragma unroll

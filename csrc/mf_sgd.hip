@@ -294,15 +294,22 @@ constexpr int XCDS = 8;
 // stream's total change to it (w - w at load; one add per factor per user run). Bit 1:
 // the H write of every rating is an L2 atomic add of that rating's change (measured 60x
 // slower on the skewed Netflix-shape bench: hot rows serialise in the L2 atomic units).
-// With both no update is lost -- concurrent updates are merely stale.
+// With both no update is lost -- concurrent updates are merely stale. Bit 2 (hot H): only
+// the items flagged hot by the host (bit 31 of the column index: the few items that carry
+// most of a cell's sum of squared shares, where concurrent streams collide) take the atomic
+// add; every other H row keeps the plain store, so a skewed set pays atomics only on the
+// rows whose updates would otherwise be lost (ops/mf.py hot_flags).
 template <int R, bool WL2 = false, int ATOM = 0>
 __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, const float* sV, int n, int sl,
                                                float* __restrict__ W, unsigned ldw, float* __restrict__ H,
                                                unsigned ldh, float lr, float lam) {
   constexpr int EPL = R / 16;
   constexpr int PAIRS = EPL / 2;
-  constexpr bool AW = (ATOM & 1) != 0, AH = (ATOM & 2) != 0;
+  constexpr bool AW = (ATOM & 1) != 0, AH = (ATOM & 2) != 0, HH = (ATOM & 4) != 0 && !AH;
   constexpr int W0 = AW ? EPL : 1;
+  // hot-H mode: the column index carries the hot flag in bit 31 (addresses drop it; the
+  // flag is a property of the item, so equal indices still mean equal rows)
+  auto hrow = [&](unsigned c) -> unsigned { return HH ? (c & 0x7fffffffu) : c; };
   const float decay = 1.0f - lr * lam;
   const unsigned lo = lane_off<EPL>(sl);
   float w[EPL], h[EPL], hp[EPL], hA[EPL], hB[EPL];
@@ -330,12 +337,12 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
   float v1 = sV[i1c];
   load_w<EPL, WL2>(W + (cur * ldw + lo), w);
   keep_w0();
-  load_row_l2<EPL>(H + (col0 * ldh + lo), h);
-  load_row_l2<EPL>(H + (col1 * ldh + lo), hB);
+  load_row_l2<EPL>(H + (hrow(col0) * ldh + lo), h);
+  load_row_l2<EPL>(H + (hrow(col1) * ldh + lo), hB);
 #pragma unroll
   for (int k = 0; k < EPL; ++k) hp[k] = 0.f;
   int i = 0;
-  float dh[AH ? EPL : 1];  // AH: this rating's change of its H row
+  float dh[AH || HH ? EPL : 1];  // AH / HH: this rating's change of its H row
   const float dm1 = -lr * lam;
   auto step = [&](float(&hl)[EPL], float(&hx)[EPL]) -> bool {
     floatx2 d2 = {0.f, 0.f};
@@ -350,7 +357,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     for (int p = 0; p < PAIRS; ++p) {
       const floatx2 wk = {w[2 * p], w[2 * p + 1]}, hk = {h[2 * p], h[2 * p + 1]};
       const floatx2 wn = __builtin_elementwise_fma(g, hk, dc * wk);
-      if constexpr (AH) {
+      if constexpr (AH || HH) {
         const floatx2 d = __builtin_elementwise_fma(g, wk, floatx2{dm1, dm1} * hk);
         dh[2 * p] = d[0];
         dh[2 * p + 1] = d[1];
@@ -367,7 +374,7 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     if constexpr (EPL % 2) {
       const float wk = w[EPL - 1], hk = h[EPL - 1];
       w[EPL - 1] = fmaf(ge, hk, decay * wk);
-      if constexpr (AH) {
+      if constexpr (AH || HH) {
         dh[EPL - 1] = fmaf(ge, wk, dm1 * hk);
         h[EPL - 1] = hk + dh[EPL - 1];
       } else {
@@ -384,11 +391,17 @@ __device__ __forceinline__ void sgd_stream_lds(const int* sR, const int* sC, con
     const int i2 = i + 2 < n ? i + 2 : n - 1;  // clamped: the last prefetch is a harmless re-read
     const unsigned row2 = (unsigned)sR[i2], col2 = (unsigned)sC[i2];
     const float v2 = sV[i2];
-    load_row_l2<EPL>(H + (col2 * ldh + lo), hl);
-    if constexpr (AH)
+    load_row_l2<EPL>(H + (hrow(col2) * ldh + lo), hl);
+    if constexpr (AH) {
       add_row<EPL>(H + (col0 * ldh + lo), dh);
-    else
+    } else if constexpr (HH) {
+      if (col0 >> 31)
+        add_row<EPL>(H + (hrow(col0) * ldh + lo), dh);
+      else
+        store_row<EPL>(H + (col0 * ldh + lo), h);
+    } else {
       store_row<EPL>(H + (col0 * ldh + lo), h);
+    }
     if (last) return false;
     // row of rating i+1: just updated (same item as i), updated one rating ago (same item as
     // i-1, its store was issued after the prefetch), or the prefetched copy
@@ -784,7 +797,7 @@ int launch_sgd(const int* rows, const int* cols, const float* vals, long n, int 
   return harp_launch_status();
 }
 
-constexpr int kAtomBits = 12;  // variant bits 2..3: ATOM write-back mode (sgd_stream_lds: 4 = W, 8 = H)
+constexpr int kAtomBits = 28;  // variant bits 2..4: ATOM write-back mode (sgd_stream_lds: 4 = W, 8 = H, 16 = hot H)
 
 // variant 0: blockIdx-placed sub-steps (+ placement check when chk != NULL; `gen` is the
 // first launch's generation, one per sub-step); 2: mf_sgd_xcd_placed_kernel (pws)
@@ -793,7 +806,7 @@ int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const lo
                    int blocks_per_xcd, float* W, int ldw, float* H, int ldh, float lr, float lam, int variant,
                    unsigned long long* chk, unsigned long long gen, int* pws, hipStream_t s) {
   const dim3 grid((unsigned)(blocks_per_xcd * XCDS));
-  const int atom = (variant >> 2) & 3;
+  const int atom = (variant >> 2) & 7;
   const bool placed = (variant & 3) == 2;
   for (int step = 0; step < steps; ++step) {
     const unsigned long long g = gen + (unsigned long long)step;
@@ -810,6 +823,8 @@ int launch_sgd_xcd(const int* rows, const int* cols, const float* vals, const lo
       case 1: XCD_LAUNCH(1); break;
       case 2: XCD_LAUNCH(2); break;
       case 3: XCD_LAUNCH(3); break;
+      case 4: XCD_LAUNCH(4); break;
+      case 5: XCD_LAUNCH(5); break;
       default: XCD_LAUNCH(0); break;
     }
 #undef XCD_LAUNCH

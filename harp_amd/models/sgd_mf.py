@@ -44,6 +44,13 @@ class SGDConfig:
                                # 100M-rating epoch at skew 2, profiles/r3_sgd_hot_balance); 0 = equal counts
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel (upper bound, see conflicts_per_rating)
+    conflict_mode: str = "hot"  # GPU, when a cell's expected collisions S sum p^2 exceed conflicts_per_rating:
+                               # "hot" keeps every block and flags the cell's most popular items for lossless
+                               # (atomic) H write-back, plus atomic W, until at most hot_residual collisions per
+                               # rating remain on plain rows; "cap" lowers blocks_per_xcd instead (round 5)
+    hot_residual: float = 0.1  # "hot" mode: expected collisions per rating left on plain-stored H rows
+                               # (ML-10M at 128 blocks/XCD: 0.5 -> test RMSE 0.8367, 0.1 -> 0.8360, all-atomic
+                               # 0.8355; profiles/r6_sgd)
     conflicts_per_rating: float = 5.0  # GPU: cap the XCD's concurrent streams S (16 x blocks_per_xcd) at
                                # this / sum_i p_i^2 of a cell (expected same-item concurrent updates per rating;
                                # two streams updating one H row at once lose one update). The reference's ML-10M
@@ -129,7 +136,8 @@ class _Buckets:
     (``ops.mf.sgd_update_blocked``), user-sorted inside a cell; ``cell_off[s]`` holds the
     65 cell offsets of slice s (relative to the slice start)."""
 
-    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device, cells=None, hot=0.0):
+    def __init__(self, rows, cols, vals, slice_of_item, local_of_item, n_slices, device, cells=None, hot=0.0,
+                 hot_items=None):
         g = slice_of_item[cols]
         lc = local_of_item[cols]
         span = int(rows.max().item()) + 1 if rows.numel() else 1
@@ -145,7 +153,12 @@ class _Buckets:
             key = g * span + rows
         order = torch.argsort(key)
         self.rows = rows[order].to(torch.int32).contiguous().to(device)
-        self.cols = lc[order].to(torch.int32).contiguous().to(device)
+        lcs = lc[order]
+        self.flagged = hot_items is not None
+        if hot_items is not None:  # bit 31: the item's H row takes atomic write-back (ops.mf.hot_items)
+            flag = hot_items.to(lcs.device)[g[order], lcs]
+            lcs = lcs | (flag.long() << 31)
+        self.cols = (lcs - ((lcs >> 31) << 32)).to(torch.int32).contiguous().to(device)
         self.vals = vals[order].to(torch.float32).contiguous().to(device)
         counts = torch.bincount(g, minlength=n_slices).cpu()
         self.offsets = [0] + torch.cumsum(counts, 0).tolist()
@@ -158,9 +171,12 @@ class _Buckets:
             self.cell_off_host = off.tolist()
             self.cell_off = off.to(device)
 
-    def get(self, s: int):
+    def get(self, s: int, plain: bool = False):
         a, b = self.offsets[s], self.offsets[s + 1]
-        return self.rows[a:b], self.cols[a:b], self.vals[a:b]
+        c = self.cols[a:b]
+        if plain and self.flagged:
+            c = c & 0x7FFFFFFF
+        return self.rows[a:b], c, self.vals[a:b]
 
     def get_cells(self, s: int):
         """(rows, cols, vals, device cell offsets, host cell offsets) of slice s."""
@@ -212,24 +228,33 @@ class SGDCollectiveMapper(CollectiveMapper):
         # another on its item with probability ~ sum_i p_i^2 (p_i: item i's share of the cell's
         # ratings), so the expected concurrent same-item updates per rating are ~ S sum p^2
         self.bpx = cfg.blocks_per_xcd
+        hot = None
+        self.hot_items = 0
         if cfg.conflicts_per_rating > 0 and dev.type == "cuda":
             key = self.slice_of_item[i] * self.ips + self.local_of_item[i]
             cnt = torch.bincount(key, minlength=n_slices * self.ips).view(n_slices, self.ips).double()
+            if P > 1:  # every rank's ratings meet on the slice's rows when it is resident there
+                self.comm.all_reduce(cnt)
             tot = cnt.sum(1).clamp_min(1.0)
             # a cell holds 1/8 of a slice's items with ~1/8 of its ratings (equal-work item
             # blocks): its sum of squared shares is ~8 x the slice's
-            sp2 = float((MF.XCDS * ((cnt / tot[:, None]) ** 2).sum(1)).mean())
-            if P > 1:
-                import torch.distributed as dist
-
-                t = torch.tensor([sp2], dtype=torch.float64, device=dev)
-                self.comm.all_reduce(t, op=dist.ReduceOp.MAX)
-                sp2 = float(t.item())
+            sp2 = float((MF.XCDS * ((cnt / tot[:, None]) ** 2).sum(1)).max())
             self.cell_sum_p2 = sp2
-            self.bpx = max(2, min(cfg.blocks_per_xcd, int(cfg.conflicts_per_rating / max(sp2, 1e-12) / 16)))
+            # (the per-sub-step and placed kernels take the hot flag; the persistent flow kernel
+            # and the wide-rank kernels keep plain write-back)
+            if (cfg.conflict_mode == "hot" and cfg.xcd_blocks and MF.storage_rank(cfg.rank, dev) <= 256
+                    and cfg.kernel_variant != MF.FLOW_VARIANT):
+                hot = MF.hot_items(cnt.cpu(), 16 * cfg.blocks_per_xcd, cfg.conflicts_per_rating, cfg.hot_residual)
+                self.hot_items = int(hot.sum())
+                if not self.hot_items:
+                    hot = None
+            elif cfg.conflict_mode == "cap":
+                self.bpx = max(2, min(cfg.blocks_per_xcd, int(cfg.conflicts_per_rating / max(sp2, 1e-12) / 16)))
         trace("user / item maps")
         self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells,
-                              hot=cfg.hot_balance)
+                              hot=cfg.hot_balance, hot_items=hot)
+        # lossless write-back where collisions are frequent: atomic W rows + flagged H rows
+        self.atomic = cfg.atomic | (MF.ATOMIC_W | MF.ATOMIC_HOT if hot is not None else 0)
         trace("rating buckets")
         if self._test is not None:
             tu, ti, tv = self._test
@@ -277,6 +302,12 @@ class SGDCollectiveMapper(CollectiveMapper):
         self.budget = StepBudget(cfg.time_budget_ms / 1e3, dev) if cfg.time_budget_ms > 0 else None
         self.budget_history = [self.budget.budget_s] if self.budget is not None else []
         self._cursor = {}
+        # placement pre-flight: one launch over empty cells tags every residue's XCC, so a
+        # dispatcher that splits a residue over two XCDs switches the schedule BEFORE the
+        # first epoch (otherwise the first epoch would run Hogwild across L2s)
+        if dev.type == "cuda" and cfg.xcd_blocks and cfg.kernel_variant == 0:
+            MF.placement_probe(self.W, slabs[0], self.bpx)
+            self._check_placement(-1)
 
     def _padded(self, M: torch.Tensor) -> torch.Tensor:
         """``M`` [n, r] on the device with zero columns up to the storage rank."""
@@ -316,11 +347,11 @@ class SGDCollectiveMapper(CollectiveMapper):
                         win = MF.cell_windows(hoff, cfg.train_fraction, epoch) if cfg.train_fraction < 1.0 else None
                         n += MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
                                                    self.bpx, host_off=hoff, variant=cfg.kernel_variant,
-                                                   window=win, atomic=cfg.atomic)
+                                                   window=win, atomic=self.atomic)
                     else:
                         if cfg.train_fraction < 1.0:
                             raise ValueError("train_fraction < 1 needs the XCD-blocked layout")
-                        n += MF.sgd_update(*self.train.get(gs), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
+                        n += MF.sgd_update(*self.train.get(gs, plain=True), self.W, slab, cfg.lr, cfg.lam, cfg.chunk)
                 with timer.phase("rotate"):
                     self.rot.start(k, self.schedules[k].rotation_map(epoch, s))
         self.trained += n
@@ -341,7 +372,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             r_, c_, v_, off, hoff = self.train.get_cells(gs)
             sizes = [hoff[c + 1] - hoff[c] for c in range(len(hoff) - 1)]
         else:
-            r_, c_, v_ = self.train.get(gs)
+            r_, c_, v_ = self.train.get(gs, plain=True)
             sizes = [r_.numel()]
         P = max(1, cfg.budget_pieces)
         # piece q covers [q*m/P, (q+1)*m/P) of every cell (an exact partition); the next
@@ -354,7 +385,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             if cfg.xcd_blocks:
                 return MF.sgd_update_blocked(r_, c_, v_, off, self.W, slab, cfg.lr, cfg.lam, cfg.chunk,
                                              self.bpx, host_off=hoff, variant=cfg.kernel_variant,
-                                             window=(starts, L), atomic=cfg.atomic)
+                                             window=(starts, L), atomic=self.atomic)
             a, m = starts[0], L[0]
             return MF.sgd_update(r_[a:a + m], c_[a:a + m], v_[a:a + m], self.W, slab, cfg.lr, cfg.lam,
                                  cfg.chunk) if m else 0
@@ -386,7 +417,8 @@ class SGDCollectiveMapper(CollectiveMapper):
         if self.cfg.model_dir:
             self.save_models(self.cfg.model_dir)
         self.result = {"rmse": self.rmse_history, "epoch_s": self.epoch_times, "trained": self.trained,
-                       "start_epoch": start, "placement": self.placement_events, "blocks_per_xcd": self.bpx}
+                       "start_epoch": start, "placement": self.placement_events, "blocks_per_xcd": self.bpx,
+                       "hot_items": self.hot_items, "atomic": self.atomic}
 
     def _check_placement(self, ep: int) -> None:
         """Once per epoch (the epoch is already synchronised): did a default XCD-blocked
@@ -510,7 +542,7 @@ class SGDCollectiveMapper(CollectiveMapper):
             for k in range(S):
                 slab = self.rot.get(k)
                 gs = block * S + k
-                tr = self.train.get(gs)
+                tr = self.train.get(gs, plain=True)
                 acc[0] += MF.sse(*tr, self.W, slab)
                 acc[1] += tr[0].numel()
                 if self.test is not None:

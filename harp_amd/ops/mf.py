@@ -144,6 +144,34 @@ def check_flow_errors(device: torch.device) -> None:
 PLACED_VARIANT = 2
 # harp_mf_sgd_xcd variant bits 2..3: atomic (no-lost-update) write-back of W (1) / H (2)
 ATOMIC_W, ATOMIC_H = 1, 2
+# hot-H write-back: H rows of the items flagged in bit 31 of their column index (hot_items)
+# take L2 atomic adds, every other H row the plain store (csrc/mf_sgd.hip, ATOM bit 2)
+ATOMIC_HOT = 4
+HOT_BIT = 1 << 31
+
+
+def hot_items(counts: torch.Tensor, streams: int, trigger: float, residual: float) -> torch.Tensor:
+    """Hot-item flags of a blocked SGD pass (bool, same shape as ``counts``: ratings per
+    (slice, local item)). A cell holds ~1/8 of a slice's items with ~1/8 of its ratings, so
+    its item shares are p_i ~ 8 c_i / T and two of the XCD's ``streams`` concurrent streams
+    meet on one H row at ~ streams * sum_i p_i^2 expected collisions per rating (each one a
+    lost update under plain write-back). A slice whose collisions exceed ``trigger`` gets
+    its most popular items flagged -- in popularity order, until the collisions left on
+    unflagged rows are at most ``residual``; below the trigger nothing is flagged (plain
+    write-back everywhere: the Netflix-shape bench, sum p^2 ~ 0.0015)."""
+    c = counts.double()
+    T = c.sum(1, keepdim=True).clamp_min(1.0)
+    p2 = XCDS * (c / T) ** 2                      # per item: its share of the cell's sum p^2
+    flags = torch.zeros_like(counts, dtype=torch.bool)
+    for s in range(counts.shape[0]):
+        tot = float(p2[s].sum()) * streams
+        if tot <= trigger:
+            continue
+        order = torch.argsort(c[s], descending=True)
+        left = tot - torch.cumsum(p2[s][order], 0) * streams  # collisions left after flagging the top k + 1
+        k = int((left > residual).sum()) + 1
+        flags[s, order[:k]] = True
+    return flags
 # default kernel: tag residue <-> XCC per launch, raise an error word on a mismatch
 # (HARP_MF_CHECK_PLACEMENT=0 turns it off: an A/B knob for its cost)
 CHECK_PLACEMENT = os.environ.get("HARP_MF_CHECK_PLACEMENT", "1") != "0"
@@ -174,6 +202,26 @@ def _chk(device: torch.device) -> _Chk:
     if c is None:
         c = _CHK[key] = _Chk(device)
     return c
+
+
+def placement_probe(W: torch.Tensor, H: torch.Tensor, blocks_per_xcd: int) -> None:
+    """One default XCD-blocked launch over EMPTY cells (every block only tags its residue ->
+    XCC and exits): the placement check runs before any rating is trained, so a dispatcher
+    that spreads a residue over two XCDs is caught by :func:`check_placement` before the
+    first epoch instead of after a lossy one. Ranks <= 256 (the narrow
+    kernels); wide ranks keep the per-epoch check."""
+    r = W.shape[1]
+    if not _lib.use_native(W) or not CHECK_PLACEMENT or r > 256 or not supported_rank(r):
+        return
+    dev = W.device
+    z = torch.zeros(1, dtype=torch.int32, device=dev)
+    off = torch.zeros(XCDS * XCDS + 1, dtype=torch.int64, device=dev)
+    ck = _chk(dev)
+    gen = ck.next_gen(XCDS)
+    st = _lib.kernels().harp_mf_sgd_xcd(z.data_ptr(), z.data_ptr(), z.data_ptr(), off.data_ptr(), None, r, XCDS, 8,
+                                        blocks_per_xcd, 0, W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), 0.0,
+                                        0.0, ck.words.data_ptr(), gen, ck.pws.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(st, "mf_sgd_xcd (placement probe)")
 
 
 def check_placement(device: torch.device) -> dict:
@@ -326,7 +374,7 @@ def sgd_update_blocked(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tenso
             ck = _chk(W.device)
             words = ck.words if (CHECK_PLACEMENT and not placed) else None
             gen = ck.next_gen(nb) if words is not None else 0
-            kv = (PLACED_VARIANT if placed else 0) | ((int(atomic) & 3) << 2 if r <= 256 else 0)
+            kv = (PLACED_VARIANT if placed else 0) | ((int(atomic) & 7) << 2 if r <= 256 else 0)
             st = lib.harp_mf_sgd_xcd(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), cell_off.data_ptr(),
                                      _lib.ptr(win), r, nb, chunk, blocks_per_xcd, kv,
                                      W.data_ptr(), W.stride(0), H.data_ptr(), H.stride(0), float(lr), float(lam),

@@ -269,3 +269,28 @@ def generate_dense_csv(path: str, n: int, d: int, files: int = 1, seed: int = 0,
         np.savetxt(fn, A, delimiter=",", fmt="%.6f")
         out.append(fn)
     return out
+
+
+ML10M_TEXT = "/root/reference/datasets/daal_als"  # the reference's movielens-{train,test} (read-only text)
+ML10M_PACKED = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                            "data", "ml10m", "ml10m.npz")  # the same split: u int32, i uint16, 2 x rating uint8
+
+
+def load_ml10m():
+    """The reference's MF-SGD gate split (ml/java/test_scripts/mfsgd.sh:64): train / test
+    (user, item, rating) triples, 0-based int64 ids and float32 ratings, plus (n_users,
+    n_items). From the reference's text files when the checkout is present, else from the
+    packed copy shipped in-tree (plain arrays, no pickle). Returns None if neither exists."""
+    if os.path.isdir(ML10M_TEXT):
+        u, i, v = load_coo(os.path.join(ML10M_TEXT, "movielens-train"), sep=" ")
+        tu, ti, tv = load_coo(os.path.join(ML10M_TEXT, "movielens-test"), sep=" ")
+        v, tv = v.float(), tv.float()
+    elif os.path.exists(ML10M_PACKED):
+        z = np.load(ML10M_PACKED)
+        col = lambda k, dt: torch.from_numpy(z[k].astype(dt))  # noqa: E731
+        u, i, v = col("train_u", np.int64), col("train_i", np.int64), col("train_v2", np.float32) / 2
+        tu, ti, tv = col("test_u", np.int64), col("test_i", np.int64), col("test_v2", np.float32) / 2
+    else:
+        return None
+    nu, ni = int(max(u.max(), tu.max())) + 1, int(max(i.max(), ti.max())) + 1
+    return (u, i, v), (tu, ti, tv), nu, ni

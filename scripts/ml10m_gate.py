@@ -39,7 +39,8 @@ def job(comm, cfg, nu, ni, train, test, device):
     wall = time.perf_counter() - t0
     res = m.result
     return {"rmse": res["rmse"], "trained": res["trained"], "epoch_s": res["epoch_s"], "wall_s": wall,
-            "placement": res["placement"], "storage_rank": int(m.W.shape[1]), "blocks_per_xcd": m.bpx}
+            "placement": res["placement"], "storage_rank": int(m.W.shape[1]), "blocks_per_xcd": m.bpx,
+            "hot_items": m.hot_items, "atomic": m.atomic}
 
 
 def als_job(comm, cfg, nu, ni, train, test, device):
@@ -67,6 +68,8 @@ def main():
     ap.add_argument("--rank", type=int, default=40)
     ap.add_argument("--atomic", type=int, default=-1, help="GPU: atomic write-back 0 none / 1 W / 2 H / 3 both (-1 = model default)")
     ap.add_argument("--blocks-per-xcd", type=int, default=0)
+    ap.add_argument("--conflict-mode", default="", help="GPU: hot (default) / cap")
+    ap.add_argument("--hot-residual", type=float, default=-1.0)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--als", action="store_true",
                     help="DAAL implicit ALS instead (harp-daal-als.sh:51-63: Dim 100, lambda 0.05, 5 iterations)")
@@ -126,13 +129,18 @@ def main():
         cfg.atomic = args.atomic
     if args.blocks_per_xcd:
         cfg.blocks_per_xcd = args.blocks_per_xcd
+    if args.conflict_mode:
+        cfg.conflict_mode = args.conflict_mode
+    if args.hot_residual >= 0:
+        cfg.hot_residual = args.hot_residual
     res = launch(job, args.workers, args=(cfg, nu, ni, (u, i, v.float()), (tu, ti, tv.float()), args.device),
                  timeout=1100)
     r0 = res[0]
     test_rmse = r0["rmse"][-1][2]
     out = {
         "gate": "mfsgd.sh:64 r=40 lambda=0.05 eps=0.002 200 iters 2 workers, test RMSE in (0.80, 0.84)",
-        "data": src, "device": args.device, "atomic": cfg.atomic, "blocks_per_xcd": r0["blocks_per_xcd"],
+        "data": src, "device": args.device, "atomic": r0.get("atomic", cfg.atomic), "blocks_per_xcd": r0["blocks_per_xcd"],
+        "conflict_mode": cfg.conflict_mode, "hot_residual": cfg.hot_residual, "hot_items": r0.get("hot_items"),
         "chunk": cfg.chunk, "workers": args.workers, "rank": args.rank, "storage_rank": r0["storage_rank"],
         "train_ratings": int(u.numel()), "test_ratings": int(tu.numel()),
         "test_rmse": test_rmse, "pass": 0.80 < test_rmse < 0.84, "reference_run": 0.8345,
