@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   constexpr int kBc = 1 + RW + 2 * NBP;  // alpha, A_ps[r][k+1] (own rows), V[k+1][l], W[k+1][l]
   __shared__ double sP[2][kT / 64][kSlots];  // parity: no barrier separates a column's read from the next write
   __shared__ double sBc[2][kBc];
-  __shared__ double sB2[2 + 2 * RW];    // (2 unused), then p and v of the own rows
+  __shared__ double sB2[2 + 2 * RW];    // p.v total, p[k+1], then p and v of the own rows
   __shared__ double sRow[RW][NBP][2];   // V / W of the own rows over the panel
   gu64* gran = (gu64*)gran_;
   int* err = ws + 2;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     mark(1);
     tmark(k, 1);
     // ---- S3: the exchange. p_k at own indices, A_ps[k+1][own indices], partial p.v sums
-    double p[kIPT], col[kIPT], pv_tot, p_k1;
+    double p[kIPT], col[kIPT];
     {
       const gu64* gp = gran + kOffP + (long)par * kN * 2;
       const gu64* gc = gran + kOffCol + ((long)(panel & 1) * NBP + j) * kN * 2;
@@ -358,14 +358,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             need |= 1u << (4 + m);
         }
       }
+      if (wv == 0) {  // wave 0 sums the partial p.v of every live workgroup
 #pragma unroll
-      for (int q = 0; q < kMaxWG / 64; ++q) {
-        pvq[q] = 0.0;
-        const int bb = lane + 64 * q;
-        if (bb >= blo && bb < NB) need |= 1u << (8 + q);
+        for (int q = 0; q < kMaxWG / 64; ++q) {
+          pvq[q] = 0.0;
+          const int bb = lane + 64 * q;
+          if (bb >= blo && bb < NB) need |= 1u << (8 + q);
+        }
       }
-      double pk1 = 0.0;  // p[k+1]: every lane reads the same granule pair
-      need |= 1u << 12;
       long spins = 0;
       for (;;) {
 #pragma unroll
@@ -386,22 +386,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             }
           }
         }
+        if (wv == 0) {
 #pragma unroll
-        for (int q = 0; q < kMaxWG / 64; ++q) {
-          if (need & (1u << (8 + q))) {
-            const int bb = lane + 64 * q;
-            const u64 lo = gload(gv + 2 * bb), hi = gload(gv + 2 * bb + 1);
-            if (tagged(lo, hi, (unsigned)k1)) {
-              pvq[q] = join_d(lo, hi);
-              need &= ~(1u << (8 + q));
+          for (int q = 0; q < kMaxWG / 64; ++q) {
+            if (need & (1u << (8 + q))) {
+              const int bb = lane + 64 * q;
+              const u64 lo = gload(gv + 2 * bb), hi = gload(gv + 2 * bb + 1);
+              if (tagged(lo, hi, (unsigned)k1)) {
+                pvq[q] = join_d(lo, hi);
+                need &= ~(1u << (8 + q));
+              }
             }
-          }
-        }
-        if (need & (1u << 12)) {
-          const u64 lo = gload(gp + 2 * k1), hi = gload(gp + 2 * k1 + 1);
-          if (tagged(lo, hi, (unsigned)k1)) {
-            pk1 = join_d(lo, hi);
-            need &= ~(1u << 12);
           }
         }
         const bool ok = need == 0;
@@ -409,18 +404,24 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         if (__all(ok)) break;
         if (spin_fail(spins, err)) return;
       }
+      if (wv == 0) {
 #pragma unroll
-      for (int q = 0; q < kMaxWG / 64; ++q) pvs += pvq[q];
-      pv_tot = wave_sum_d_dpp(pvs);
-      p_k1 = pk1;
+        for (int q = 0; q < kMaxWG / 64; ++q) pvs += pvq[q];
+        pvs = wave_sum_d_dpp(pvs);
+        if (lane == 0) sB2[0] = pvs;
+      }
+      if (tid == k1 / kIPT) {
+#pragma unroll
+        for (int m = 0; m < kIPT; ++m)
+          if (t0 + m == k1) sB2[1] = p[m];
+      }
     }
     mark(2);
     tmark(k, 2);
-    // the only barrier left in the column's second half: at a panel end every thread reads
-    // the own rows' p and v (sB2) that their owners wrote after this column's first barrier
-    const bool pend = j == NBP - 1 && k + 3 < n;
-    if (pend) lds_barrier();
-    const double c = 0.5 * tau * pv_tot;
+    // (measured: letting every wave poll the partial sums itself to drop this barrier on
+    // non-panel columns cost more polling traffic than the barrier: 6.8 -> 7.8 ms)
+    lds_barrier();
+    const double c = 0.5 * tau * sB2[0];
 #pragma unroll
     for (int m = 0; m < kIPT; ++m) Ww[j][m] = t0 + m >= k1 ? fma(-c, v[m], p[m]) : 0.0;
     if (h >= 0 && h < kOwn) {
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int l = 0; l < NBP; ++l)
       if (l == j) {
         Vk[l] = 1.0;
-        Wk[l] = fma(-c, 1.0, p_k1);
+        Wk[l] = fma(-c, 1.0, sB2[1]);
       }
     double xn[kIPT];
 #pragma unroll

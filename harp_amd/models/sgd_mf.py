@@ -44,10 +44,19 @@ class SGDConfig:
                                # 100M-rating epoch at skew 2, profiles/r3_sgd_hot_balance); 0 = equal counts
     xcd_blocks: bool = True    # 8 x 8 cell schedule, one XCD per cell (ops.mf.sgd_update_blocked)
     blocks_per_xcd: int = 128  # workgroups per XCD of the blocked kernel (upper bound, see conflicts_per_rating)
-    conflict_mode: str = "hot"  # GPU, when a cell's expected collisions S sum p^2 exceed conflicts_per_rating:
+    conflict_mode: str = "cap"  # GPU, when a cell's expected collisions S sum p^2 exceed conflicts_per_rating:
+                               # "cap" lowers blocks_per_xcd (plain Hogwild write-back: stable at any step size);
                                # "hot" keeps every block and flags the cell's most popular items for lossless
                                # (atomic) H write-back, plus atomic W, until at most hot_residual collisions per
-                               # rating remain on plain rows; "cap" lowers blocks_per_xcd instead (round 5)
+                               # rating remain on plain rows -- the reference ML-10M gate at 128 blocks / XCD:
+                               # 0.8360 vs 0.8377 capped (profiles/r6_sgd). Lossless accumulation ADDS the steps
+                               # of streams that read one stale row, which diverged on an 800-item toy at lr 0.01
+                               # (scripts/sgd_toy_diag.py), so it is opt-in
+    hot_step_budget: float = 0.1  # "hot" mode: lossless write-back ADDS every concurrent stream's step (all
+                               # computed from one stale row), so the effective step grows with the collisions:
+                               # blocks_per_xcd is capped so that lr x S sum p^2 <= this (ML-10M, lr 0.002,
+                               # sum p^2 0.022: 141 >= 128 blocks, no cap; an 800-item toy at lr 0.01 diverged
+                               # at 0.25 and at no cap)
     hot_residual: float = 0.1  # "hot" mode: expected collisions per rating left on plain-stored H rows
                                # (ML-10M at 128 blocks/XCD: 0.5 -> test RMSE 0.8367, 0.1 -> 0.8360, all-atomic
                                # 0.8355; profiles/r6_sgd)
@@ -238,17 +247,20 @@ class SGDCollectiveMapper(CollectiveMapper):
             tot = cnt.sum(1).clamp_min(1.0)
             # a cell holds 1/8 of a slice's items with ~1/8 of its ratings (equal-work item
             # blocks): its sum of squared shares is ~8 x the slice's
-            sp2 = float((MF.XCDS * ((cnt / tot[:, None]) ** 2).sum(1)).max())
+            sp2 = float((MF.XCDS * ((cnt / tot[:, None]) ** 2).sum(1)).mean())
             self.cell_sum_p2 = sp2
             # (the per-sub-step and placed kernels take the hot flag; the persistent flow kernel
             # and the wide-rank kernels keep plain write-back)
-            if (cfg.conflict_mode == "hot" and cfg.xcd_blocks and MF.storage_rank(cfg.rank, dev) <= 256
-                    and cfg.kernel_variant != MF.FLOW_VARIANT):
-                hot = MF.hot_items(cnt.cpu(), 16 * cfg.blocks_per_xcd, cfg.conflicts_per_rating, cfg.hot_residual)
+            use_hot = (cfg.conflict_mode == "hot" and cfg.xcd_blocks and MF.storage_rank(cfg.rank, dev) <= 256
+                       and cfg.kernel_variant != MF.FLOW_VARIANT)
+            if use_hot:
+                self.bpx = max(2, min(cfg.blocks_per_xcd, int(cfg.hot_step_budget / max(cfg.lr, 1e-12)
+                                                              / max(sp2, 1e-12) / 16)))
+                hot = MF.hot_items(cnt.cpu(), 16 * self.bpx, cfg.conflicts_per_rating, cfg.hot_residual)
                 self.hot_items = int(hot.sum())
                 if not self.hot_items:
                     hot = None
-            elif cfg.conflict_mode == "cap":
+            elif cfg.conflict_mode in ("hot", "cap"):  # (kernels without the hot flag: the cap)
                 self.bpx = max(2, min(cfg.blocks_per_xcd, int(cfg.conflicts_per_rating / max(sp2, 1e-12) / 16)))
         trace("user / item maps")
         self.train = _Buckets(rows, i, v, self.slice_of_item, self.local_of_item, n_slices, dev, cells=cells,

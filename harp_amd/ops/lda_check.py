@@ -262,3 +262,27 @@ if __name__ == "__main__":
                 print(json.dumps(run(K, N, "dense", 0, dev, ndk_dtype=torch.uint8)), flush=True)
         for w in (1, 8):
             print(json.dumps(run(K, N, "sparse", w, dev)), flush=True)
+
+
+# --------------------------------------------------------------------------- likelihood spread
+def loglik_spread(dev, K: int, seeds=(0, 1, 2, 3), iterations: int = 20) -> dict:
+    """Per-token log-likelihood after ``iterations`` sweeps of the GPU sampler and of the
+    exact sequential CPU sampler on the test corpus of tests/test_lda_gpu.py, for several
+    sampler seeds: the run-to-run spread of each, and the GPU - CPU gap of the means, in
+    nats per token (what the GPU-vs-CPU quality test bounds)."""
+    from ..models.lda import LDAConfig, run_lda, synthetic_corpus
+    from ..parallel.comm import Communicator
+
+    toks = synthetic_corpus(2000, 3000, 20, 60, seed=4)
+    n = toks[0].numel()
+    out = {"K": K, "tokens": n}
+    for name, d in (("gpu", dev), ("cpu", torch.device("cpu"))):
+        vals = []
+        for s in seeds:
+            cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=iterations,
+                            print_interval=iterations, seed=s)
+            vals.append(run_lda(Communicator(None, d), cfg, 2000, 3000, toks)["loglik"][-1][1] / n)
+        out[name] = [round(v, 5) for v in vals]
+        out[name + "_spread"] = round(max(vals) - min(vals), 5)
+    out["gap_of_means"] = round(abs(sum(out["gpu"]) / len(seeds) - sum(out["cpu"]) / len(seeds)), 5)
+    return out

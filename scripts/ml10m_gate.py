@@ -68,7 +68,7 @@ def main():
     ap.add_argument("--rank", type=int, default=40)
     ap.add_argument("--atomic", type=int, default=-1, help="GPU: atomic write-back 0 none / 1 W / 2 H / 3 both (-1 = model default)")
     ap.add_argument("--blocks-per-xcd", type=int, default=0)
-    ap.add_argument("--conflict-mode", default="", help="GPU: hot (default) / cap")
+    ap.add_argument("--conflict-mode", default="hot", help="GPU: hot (lossless hot items, full concurrency) / cap / none")
     ap.add_argument("--hot-residual", type=float, default=-1.0)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--als", action="store_true",

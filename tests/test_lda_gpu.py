@@ -10,13 +10,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("K", [20, 300, 1000])
 def test_lda_gpu_matches_cpu_quality(cuda, K):
-    toks = synthetic_corpus(2000, 3000, 20, 60, seed=4)
-    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=20, print_interval=20)
-    g = run_lda(Communicator(None, cuda), cfg, 2000, 3000, toks)
-    c = run_lda(Communicator(None, torch.device("cpu")), cfg, 2000, 3000, toks)
-    n = toks[0].numel()
-    lg, lc = g["loglik"][-1][1], c["loglik"][-1][1]
-    assert abs(lg - lc) / n < 0.1, (lg, lc)
+    """Per-token log-likelihood after 20 sweeps, GPU vs the exact sequential CPU sampler, as
+    the MEAN over 4 sampler seeds: measured gap of the means <= 0.020 nats / token at K = 20 /
+    300 / 1000, while a single seed moves by up to 0.097 (K = 20; profiles/r6_lda_exact
+    spread.jsonl) -- the bound is 0.05 (2.5x the largest gap; round 5 used 0.1 on one seed)."""
+    from harp_amd.ops.lda_check import loglik_spread
+
+    r = loglik_spread(cuda, K)
+    print(r)
+    assert r["gap_of_means"] < 0.05, r
 
 
 @pytest.mark.parametrize("strategy", ["rotation", "push_pull"])

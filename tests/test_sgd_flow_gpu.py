@@ -14,8 +14,10 @@ pytestmark = pytest.mark.gpu
 def _train(cuda, variant, epochs=6, slices=4, fraction=1.0, n=600000):
     nu, ni = 20000, 3000
     u, i, v = synthetic_ratings(nu, ni, n, seed=5)
+    # conflict_mode "cap": both launch forms at the same concurrency (the flow kernel takes
+    # no hot-item flags, so "hot" would run the two at different block counts)
     cfg = SGDConfig(rank=128, epochs=epochs, test_every=0, num_slices=slices, kernel_variant=variant, chunk=0,
-                    train_fraction=fraction, lr=0.005)
+                    train_fraction=fraction, lr=0.005, conflict_mode="cap")
     m = SGDCollectiveMapper(Communicator(None, cuda), cfg, nu, ni, (u, i, v), None)
     m.init_model(KeyValReader([]))
     trained = sum(m.train_epoch(ep) for ep in range(epochs))

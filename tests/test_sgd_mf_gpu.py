@@ -223,3 +223,23 @@ def test_sgd_one_slice_per_rank_like_two(cuda):
     assert out[1][0] == out[2][0] == 5 * n
     assert abs(out[1][1] - out[2][1]) / out[2][1] < 0.01, out
 
+
+
+@pytest.mark.parametrize("atomic", [1, 2, 3, 5])
+@pytest.mark.parametrize("r", [16, 32, 48, 128])
+def test_sgd_xcd_atomic_writeback_one_stream_matches_plain(cuda, r, atomic):
+    """One stream per cell (no concurrency): the atomic write-back modes (W adds, H adds, hot
+    H adds for flagged items) must train exactly what the plain stores train."""
+    R, C, V, off, W0, H0 = _cells(64, 48, 4000, r, 2)
+    out = {}
+    for a in (0, atomic):
+        Cf = C.clone()
+        if a & MF.ATOMIC_HOT:  # every other item hot
+            Cf = torch.where(Cf % 2 == 0, Cf | MF.HOT_BIT, Cf).int()
+        Wg, Hg = W0.clone().to(cuda), H0.clone().to(cuda)
+        MF.sgd_update_blocked(R.to(cuda), Cf.to(cuda), V.to(cuda), off.to(cuda), Wg, Hg, 0.01, 0.05, chunk=128,
+                              blocks_per_xcd=1, atomic=a)
+        torch.cuda.synchronize()
+        out[a] = (Wg.cpu(), Hg.cpu())
+    assert torch.isfinite(out[atomic][0]).all() and torch.isfinite(out[atomic][1]).all()
+    assert torch.allclose(out[atomic][0], out[0][0], atol=1e-5) and torch.allclose(out[atomic][1], out[0][1], atol=1e-5)
