@@ -20,7 +20,8 @@
 //  3. dc_loewner_kernel, one wave per kept j: zhat_j as a product of ratios over the roots.
 //  4. dc_vectors_kernel, one wave per root: the normalised column of U.
 //  5. dc_gemm_kernel: Q_new[block] = Q[block rows, kept columns] x U (64 x 64 tiles over
-//     LDS, fp64 FMA), deflated columns copied; Q ping-pongs between two buffers.
+//     LDS, fp64 MFMA, each half's rows over that half's columns only), deflated columns
+//     copied; Q ping-pongs between two buffers.
 // Eigenvalues are carried as (origin pole, tau) while the vectors are formed, so every
 // difference d_j - lambda_i is computed as (d_j - d_o) - tau without cancellation.
 #include "common.h"
@@ -61,6 +62,9 @@ __device__ __forceinline__ double block_max_1k(double v, double* red) {
   return s;
 }
 
+// workgroup barrier for LDS traffic only (__syncthreads() also drains outstanding global loads)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // merge holding position c (merges sorted by lo, nm of them)
 __device__ __forceinline__ int find_merge(const int* __restrict__ mg, int nm, int c) {
   int a = 0, b = nm - 1;
@@ -72,9 +76,21 @@ __device__ __forceinline__ int find_merge(const int* __restrict__ mg, int nm, in
   return a;
 }
 
+// diagnostic: thread 0 of the last launch's first merge records s_memtime at its phase ends
+// (harp_dc_prep_stamps)
+__device__ long long g_prep_t[10];
+#define PREP_MARK(i) \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_prep_t[i] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
 struct DcWs {
   double *dd, *zz, *tau, *zh, *rho, *U, *rotc, *rots, *sortbuf;
   int *colsrc, *org, *kcnt, *rotp, *rotq;
+  // kept secular positions whose Q column has entries in the upper (lower) half of the
+  // merge: jl / jr (ascending, at lo), counts kl / kr at [lo]. A column is one-sided unless
+  // a deflation rotation mixed it with a column of the other half.
+  int *jl, *jr, *kl, *kr;
   long ldu;  // U of the merge at lo starts at lo * ldu (ldu >= the level's largest block)
 };
 
@@ -91,9 +107,12 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
   int* src = (int*)(sm + 2 * s);   // [s] local source column of sorted position
   int* keep = src + s;             // [s]
   int* defl = keep + s;            // [s]
+  int* hm = defl + s;              // [s] halves holding the column's entries (bit 0 upper, bit 1 lower)
   __shared__ double red[16];
   __shared__ int s_k, s_nd, s_nrot, s_serial;
+  __shared__ unsigned long long passm[kMaxN / 64];
   const int tid = threadIdx.x, T = blockDim.x;
+  PREP_MARK(0);
   const double beta = e[mid - 1];
   const double sgn = beta < 0.0 ? -1.0 : 1.0;
   // raw values: left block's last row, right block's first row (sign of beta folded in)
@@ -102,27 +121,56 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
     sz[j] = j < s1 ? Q[(long)(lo + j) * ldq + (mid - 1)] : sgn * Q[(long)(lo + j) * ldq + mid];
   }
   __syncthreads();
-  // ranks (ties by index) -> the sorted lists go through global scratch (3 s doubles at 3 lo)
-  double* tmp = w.sortbuf + 3L * lo;
-  for (int j = tid; j < s; j += T) {
-    const double v = sd[j];
-    int r = 0;
-    for (int i = 0; i < s; ++i) {
-      const double u = sd[i];
-      r += (u < v) || (u == v && i < j);
+  PREP_MARK(1);
+  // sort (value, index) pairs ascending, ties by index, in place in LDS: bitonic network in
+  // the all-ascending (flip) form, where a comparator always keeps the smaller key at the
+  // lower position -- so the positions past s act as +inf and are never touched (no padding
+  // storage). log2(P2) (log2(P2) + 1) / 2 barrier stages instead of s compares per thread.
+  for (int j = tid; j < s; j += T) src[j] = j;
+  __syncthreads();
+  int P2 = 1;
+  while (P2 < s) P2 <<= 1;
+  auto cmpswap = [&](int i, int l) {
+    if (l >= s) return;
+    const double a = sd[i], b = sd[l];
+    const int ai = src[i], bi = src[l];
+    if (b < a || (b == a && bi < ai)) {
+      sd[i] = b;
+      sd[l] = a;
+      src[i] = bi;
+      src[l] = ai;
     }
-    tmp[r] = v;
-    tmp[s + r] = sz[j];
-    ((int*)(tmp + 2 * s))[r] = j;
+  };
+  for (int lp = 1; (1 << lp) <= P2; ++lp) {  // blocks of p = 2^lp (shifts, no integer divides)
+    const int hm1 = (1 << (lp - 1)) - 1;
+    for (int c = tid; c < (P2 >> 1); c += T) {  // flip: i <-> mirror within the block of p
+      const int base = (c >> (lp - 1)) << lp, o = c & hm1;
+      cmpswap(base + o, base + (1 << lp) - 1 - o);
+    }
+    lds_sync();
+    for (int lq = lp - 2; lq >= 0; --lq) {  // half-cleaners at distance q = 2^lq
+      const int qm1 = (1 << lq) - 1;
+      for (int c = tid; c < (P2 >> 1); c += T) {
+        const int i = ((c >> lq) << (lq + 1)) + (c & qm1);
+        cmpswap(i, i + (1 << lq));
+      }
+      lds_sync();
+    }
   }
-  __threadfence_block();
-  __syncthreads();
+  PREP_MARK(2);
+  // z in the sorted order, through keep / defl (free until the deflation) as 32-bit halves
   for (int j = tid; j < s; j += T) {
-    sd[j] = tmp[j];
-    sz[j] = tmp[s + j];
-    src[j] = ((int*)(tmp + 2 * s))[j];
+    const double z = sz[src[j]];
+    keep[j] = __double2loint(z);
+    defl[j] = __double2hiint(z);
+  }
+  lds_sync();
+  for (int j = tid; j < s; j += T) {
+    sz[j] = __hiloint2double(defl[j], keep[j]);
+    hm[j] = src[j] < s1 ? 1 : 2;
   }
   __syncthreads();
+  PREP_MARK(3);
   double nz2 = 0.0, dmax = 0.0;
   for (int j = tid; j < s; j += T) {
     nz2 = fma(sz[j], sz[j], nz2);
@@ -138,6 +186,7 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
     zmax = fmax(zmax, fabs(sz[j]));
   }
   zmax = block_max_1k(zmax, red);
+  PREP_MARK(4);
   const double tol = 8.0 * kEps * fmax(dmax, rho * zmax);
   // parallel pre-check: does any pair of consecutive small-z survivors pass the rotation
   // test? If not, the walk below reduces to a compaction (done in parallel)
@@ -155,6 +204,7 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
     }
   }
   __syncthreads();
+  PREP_MARK(5);
   if (rho == 0.0) {  // decoupled halves: everything deflates, in sorted order
     for (int j = tid; j < s; j += T) defl[j] = j;
     if (tid == 0) {
@@ -183,63 +233,142 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
         s_nrot = 0;
       }
     }
-  } else if (tid == 0) {
+  } else {
     // the dependent walk (LAPACK dlaed2 order): a rotated pair keeps d_pj c^2 + d_j s^2 at
-    // pj (deflated) and continues with j
-    int kk = 0, nd = 0, nr = 0, pj = -1;
-    for (int j = 0; j < s; ++j) {
-      if (rho * fabs(sz[j]) <= tol) {
-        defl[nd++] = j;
-        continue;
+    // pj (deflated) and continues with j. A pair whose first member was not rotated into
+    // sees its original values, so its test is precomputed in parallel (passm bits); the
+    // one-thread walk jumps between set bits and evaluates only inside rotation chains.
+    if (tid < 64) {  // survivors (large z) in order -> keep[0 .. ns)
+      int kk = 0;
+      for (int b = 0; b < s; b += 64) {
+        const int j = b + tid;
+        const bool sv = j < s && rho * fabs(sz[j]) > tol;
+        const unsigned long long mk = __ballot(sv);
+        if (sv) keep[kk + __popcll(mk & ((1ull << tid) - 1ull))] = j;
+        kk += __popcll(mk);
       }
-      if (pj < 0) {
-        pj = j;
-        continue;
+      if (tid == 0) s_k = kk;
+    }
+    __syncthreads();
+    const int ns = s_k;
+    for (int b = (tid >> 6) * 64; b < ns; b += T) {  // one 64-pair word per wave
+      const int i = b + (tid & 63);
+      bool ps = false;
+      if (i >= 1 && i < ns) {
+        const int pj = keep[i - 1], j = keep[i];
+        const double ss = sz[pj], cc = sz[j];
+        const double t2 = hypot(cc, ss);
+        ps = fabs((sd[j] - sd[pj]) * (cc / t2) * (-ss / t2)) <= tol;
       }
-      double ss = sz[pj], cc = sz[j];
-      const double t2 = hypot(cc, ss);
-      const double t = sd[j] - sd[pj];
-      cc /= t2;
-      ss = -ss / t2;
-      if (fabs(t * cc * ss) <= tol) {
-        sz[j] = t2;
-        sz[pj] = 0.0;
-        w.rotp[lo + nr] = lo + src[pj];
-        w.rotq[lo + nr] = lo + src[j];
-        w.rotc[lo + nr] = cc;
-        w.rots[lo + nr] = ss;
-        ++nr;
-        const double tt = sd[pj] * cc * cc + sd[j] * ss * ss;
-        sd[j] = sd[pj] * ss * ss + sd[j] * cc * cc;
-        sd[pj] = tt;
-        defl[nd++] = pj;
-        pj = j;
-      } else {
-        keep[kk++] = pj;
-        pj = j;
+      const unsigned long long m = __ballot(ps);
+      if ((tid & 63) == 0) passm[b >> 6] = m;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int nw = (ns + 63) >> 6;
+      int nr = 0, i = 1;
+      bool chain = false;  // keep[i - 1] was rotated into at the previous step
+      while (i < ns) {
+        if (!chain) {  // next precomputed rotation
+          int wi = i >> 6;
+          unsigned long long m = passm[wi] & (~0ull << (i & 63));
+          while (!m && ++wi < nw) m = passm[wi];
+          if (!m) break;
+          i = (wi << 6) + __builtin_ctzll(m);
+          if (i >= ns) break;
+        }
+        const int pj = keep[i - 1], j = keep[i];
+        double ss = sz[pj], cc = sz[j];
+        const double t2 = hypot(cc, ss);
+        const double t = sd[j] - sd[pj];
+        cc /= t2;
+        ss = -ss / t2;
+        if (fabs(t * cc * ss) <= tol) {
+          sz[j] = t2;
+          sz[pj] = 0.0;
+          hm[j] |= hm[pj];
+          hm[pj] |= 4;  // rotated away: deflated
+          w.rotp[lo + nr] = lo + src[pj];
+          w.rotq[lo + nr] = lo + src[j];
+          w.rotc[lo + nr] = cc;
+          w.rots[lo + nr] = ss;
+          ++nr;
+          const double tt = sd[pj] * cc * cc + sd[j] * ss * ss;
+          sd[j] = sd[pj] * ss * ss + sd[j] * cc * cc;
+          sd[pj] = tt;
+          chain = true;
+        } else {
+          chain = false;
+        }
+        ++i;
+      }
+      s_nrot = nr;
+    }
+    __syncthreads();
+    if (tid < 64) {  // keep = survivors not rotated away (in place), defl = the rest in j order
+      int kk = 0, nd = 0;
+      const unsigned long long below = (1ull << tid) - 1ull;
+      for (int b = 0; b < ns; b += 64) {
+        const int i = b + tid;
+        const int j = i < ns ? keep[i] : 0;
+        const bool kp = i < ns && !(hm[j] & 4);
+        const unsigned long long mk = __ballot(kp);
+        if (kp) keep[kk + __popcll(mk & below)] = j;
+        kk += __popcll(mk);
+      }
+      for (int b = 0; b < s; b += 64) {
+        const int j = b + tid;
+        const bool dj = j < s && (rho * fabs(sz[j]) <= tol || (hm[j] & 4));
+        const unsigned long long md = __ballot(dj);
+        if (dj) defl[nd + __popcll(md & below)] = j;
+        nd += __popcll(md);
+      }
+      if (tid == 0) {
+        s_k = kk;
+        s_nd = nd;
       }
     }
-    if (pj >= 0) keep[kk++] = pj;
-    s_k = kk;
-    s_nd = nd;
-    s_nrot = nr;
   }
   __threadfence_block();
   __syncthreads();
+  PREP_MARK(6);
   const int k = s_k, nd = s_nd, nrot = s_nrot;
-  // deflation rotations on Q's columns, in order (each row independent)
+  // deflation rotations on Q's columns, in order (each row independent). A column takes part
+  // in at most two rotations, consecutive ones (y of step q = x of step q + 1, a chain), so
+  // the chained value stays in a register and every other operand can be loaded ahead: the
+  // loads of a batch of 16 rotations are in flight together (one round trip per batch, not
+  // one per rotation).
   if (nrot) {
+    constexpr int kRB = 16;
     for (int r = lo + tid; r < hi; r += T) {
-      for (int q = 0; q < nrot; ++q) {
-        double* x = Q + (long)w.rotp[lo + q] * ldq + r;
-        double* y = Q + (long)w.rotq[lo + q] * ldq + r;
-        const double c = w.rotc[lo + q], sn = w.rots[lo + q];
-        const double xv = *x, yv = *y;
-        *x = c * xv + sn * yv;
-        *y = c * yv - sn * xv;
+      double carry = 0.0;
+      int cy = -1;
+      for (int q0 = 0; q0 < nrot; q0 += kRB) {
+        double xv[kRB], yv[kRB];
+#pragma unroll
+        for (int u = 0; u < kRB; ++u) {
+          if (q0 + u < nrot) {
+            xv[u] = Q[(long)w.rotp[lo + q0 + u] * ldq + r];
+            yv[u] = Q[(long)w.rotq[lo + q0 + u] * ldq + r];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kRB; ++u) {
+          const int q = q0 + u;
+          if (q < nrot) {
+            const int xc = w.rotp[lo + q], yc = w.rotq[lo + q];
+            const double c = w.rotc[lo + q], sn = w.rots[lo + q];
+            const double xo = xc == cy ? carry : xv[u];
+            Q[(long)xc * ldq + r] = c * xo + sn * yv[u];
+            carry = c * yv[u] - sn * xo;
+            cy = yc;
+            if (!(q + 1 < nrot && w.rotp[lo + q + 1] == yc)) Q[(long)yc * ldq + r] = carry;
+          }
+        }
       }
     }
   }
+  PREP_MARK(7);
   for (int i = tid; i < k; i += T) {
     const int j = keep[i];
     w.dd[lo + i] = sd[j];
@@ -251,6 +380,24 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
     w.colsrc[lo + k + t] = lo + src[j];
     D[lo + k + t] = sd[j];  // final for this merge
   }
+  if (tid < 64) {  // one-sided lists, in kept order (ballots)
+    int nl = 0, nr2 = 0;
+    const unsigned long long below = (1ull << tid) - 1ull;
+    for (int b = 0; b < k; b += 64) {
+      const int i = b + tid;
+      const int h = i < k ? hm[keep[i]] : 0;
+      const unsigned long long ml = __ballot(h & 1), mr = __ballot(h & 2);
+      if (h & 1) w.jl[lo + nl + __popcll(ml & below)] = i;
+      if (h & 2) w.jr[lo + nr2 + __popcll(mr & below)] = i;
+      nl += __popcll(ml);
+      nr2 += __popcll(mr);
+    }
+    if (tid == 0) {
+      w.kl[lo] = nl;
+      w.kr[lo] = nr2;
+    }
+  }
+  PREP_MARK(8);
   if (tid == 0) {
     w.kcnt[lo] = k;
     w.rho[lo] = rho;
@@ -258,28 +405,43 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
 }
 
 // ---------------------------------------------------------------------------------------
-// 2. secular roots: one wave per root; 4 roots per 256-thread workgroup over positions
-__global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__ mg, int nm, int n, double* __restrict__ D,
-                                                         DcWs w) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= n) return;
-  const int m = find_merge(mg, nm, c);
-  const int lo = mg[3 * m];
-  if (c < lo || c >= mg[3 * m + 2]) return;  // position not merged at this level
-  const int i = c - lo;
-  const int k = w.kcnt[lo];
-  if (i >= k) return;
-  const double rho = w.rho[lo];
+// 2. secular roots: one wave per root; 4 roots per 256-thread workgroup over positions.
+// For k <= 64 kSecR the wave keeps d_j - d_o and z_j^2 in registers for the whole solve
+// (the iterations re-read them from L2 otherwise) and forms 1 / (d_j - d_o - tau) with
+// v_rcp_f64 + two Newton steps instead of the IEEE divide chain.
+constexpr int kSecR = 16;
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+template <bool kReg>
+__device__ __forceinline__ void secular_solve(int i, int k, int lane, double rho, const double* __restrict__ dd,
+                                              const double* __restrict__ zz, int& o_out, double& tau_out) {
   const double irho = 1.0 / rho;
-  const double* dd = w.dd + lo;
-  const double* zz = w.zz + lo;
+  double dr[kReg ? kSecR : 1], z2r[kReg ? kSecR : 1];
+  if (kReg) {
+#pragma unroll
+    for (int q = 0; q < kSecR; ++q) {
+      const int j = lane + 64 * q;
+      dr[q] = j < k ? dd[j] : 0.0;
+      z2r[q] = j < k ? zz[j] * zz[j] : 0.0;
+    }
+  }
   int o;
   double lo_t, hi_t;
+  const double ddi = dd[i];
   if (i < k - 1) {
-    const double mid = 0.5 * (dd[i + 1] - dd[i]);
+    const double mid = 0.5 * (dd[i + 1] - ddi);
     double f = 0.0;
-    for (int j = lane; j < k; j += 64) f += zz[j] * zz[j] / ((dd[j] - dd[i]) - mid);
+    if (kReg) {
+#pragma unroll
+      for (int q = 0; q < kSecR; ++q)
+        if (lane + 64 * q < k) f += z2r[q] / ((dr[q] - ddi) - mid);
+    } else {
+      for (int j = lane; j < k; j += 64) f += zz[j] * zz[j] / ((dd[j] - ddi) - mid);
+    }
     f = wave_sum_d_dpp(f) + irho;
     if (f >= 0.0) {
       o = i;
@@ -292,24 +454,52 @@ __global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__
     }
   } else {
     double z2 = 0.0;
-    for (int j = lane; j < k; j += 64) z2 += zz[j] * zz[j];
+    if (kReg) {
+#pragma unroll
+      for (int q = 0; q < kSecR; ++q) z2 += z2r[q];
+    } else {
+      for (int j = lane; j < k; j += 64) z2 += zz[j] * zz[j];
+    }
     o = i;
     lo_t = 0.0;
     hi_t = rho * wave_sum_d_dpp(z2);
   }
   const double dor = dd[o];
+  if (kReg) {
+#pragma unroll
+    for (int q = 0; q < kSecR; ++q) dr[q] -= dor;
+  }
+  const double D1o = ddi - dor, D2o = i < k - 1 ? dd[i + 1] - dor : 0.0;
   double tau = 0.5 * (lo_t + hi_t);
   for (int it = 0; it < 64; ++it) {
     double psi = 0.0, phi = 0.0, dpsi = 0.0, dphi = 0.0;
-    for (int j = lane; j < k; j += 64) {
-      const double r = 1.0 / ((dd[j] - dor) - tau);
-      const double t = zz[j] * zz[j] * r;
-      if (j <= i) {
-        psi += t;
-        dpsi = fma(t, r, dpsi);
-      } else {
-        phi += t;
-        dphi = fma(t, r, dphi);
+    if (kReg) {
+#pragma unroll
+      for (int q = 0; q < kSecR; ++q) {
+        const int j = lane + 64 * q;
+        if (j < k) {
+          const double r = rcp_nr(dr[q] - tau);
+          const double t = z2r[q] * r;
+          if (j <= i) {
+            psi += t;
+            dpsi = fma(t, r, dpsi);
+          } else {
+            phi += t;
+            dphi = fma(t, r, dphi);
+          }
+        }
+      }
+    } else {
+      for (int j = lane; j < k; j += 64) {
+        const double r = 1.0 / ((dd[j] - dor) - tau);
+        const double t = zz[j] * zz[j] * r;
+        if (j <= i) {
+          psi += t;
+          dpsi = fma(t, r, dpsi);
+        } else {
+          phi += t;
+          dphi = fma(t, r, dphi);
+        }
       }
     }
     psi = wave_sum_d_dpp(psi);
@@ -321,13 +511,13 @@ __global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__
     if (fabs(f) <= erretm || hi_t - lo_t <= 2.0 * kEps * fmax(fabs(lo_t), fabs(hi_t))) break;
     if (f < 0.0) lo_t = tau;
     else hi_t = tau;
-    const double D1 = (dd[i] - dor) - tau;
+    const double D1 = D1o - tau;
     const double b1 = dpsi * D1 * D1;
     double cc = irho + (psi - b1 / D1);
     double eta = 0.0;
     bool ok = false;
     if (i < k - 1) {
-      const double D2 = (dd[i + 1] - dor) - tau;
+      const double D2 = D2o - tau;
       const double b2 = dphi * D2 * D2;
       cc += phi - b2 / D2;
       const double B = cc * (D1 + D2) + b1 + b2;
@@ -372,10 +562,31 @@ __global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__
       if (fabs(eta) <= 2.0 * kEps * fabs(tau)) break;
     }
   }
+  o_out = o;
+  tau_out = tau;
+}
+
+__global__ __launch_bounds__(256) void dc_secular_kernel(const int* __restrict__ mg, int nm, int n, double* __restrict__ D,
+                                                         DcWs w) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= n) return;
+  const int m = find_merge(mg, nm, c);
+  const int lo = mg[3 * m];
+  if (c < lo || c >= mg[3 * m + 2]) return;  // position not merged at this level
+  const int i = c - lo;
+  const int k = w.kcnt[lo];
+  if (i >= k) return;
+  int o;
+  double tau;
+  if (k <= 64 * kSecR)
+    secular_solve<true>(i, k, lane, w.rho[lo], w.dd + lo, w.zz + lo, o, tau);
+  else
+    secular_solve<false>(i, k, lane, w.rho[lo], w.dd + lo, w.zz + lo, o, tau);
   if (lane == 0) {
     w.org[lo + i] = o;
     w.tau[lo + i] = tau;
-    D[lo + i] = dor + tau;
+    D[lo + i] = w.dd[lo + o] + tau;
   }
 }
 
@@ -425,74 +636,116 @@ __global__ __launch_bounds__(256) void dc_vectors_kernel(const int* __restrict__
   for (int j = lane; j < k; j += 64) U[j] *= inv;
 }
 
-// 5. Qn[lo.., lo + c] = sum_j Q[lo.., colsrc[j]] U[j, c] (c < k), Q[lo.., colsrc[c]] (c >= k)
-constexpr int TM = 64, TK = 16;
+// 5. Qn[lo.., lo + c] = sum_j Q[lo.., colsrc[j]] U[j, c] (c < k), Q[lo.., colsrc[c]] (c >= k).
+// Q is block diagonal before the merge: a tile of upper-half rows sums only over the kept
+// columns with upper entries (jl), a lower tile over jr -- about half the products skipped,
+// every skipped one an exact zero (same sums in the same order).
+// fp64 MFMA (v_mfma_f64_16x16x4_f64) on 64 x 64 output tiles, 4 waves of 32 x 32. The product
+// is formed transposed, Qn^T = U^T Q^T, so the accumulator's lane index runs along Q's rows
+// and the stores are coalesced. Row tiles start at 0 and at the split s1 (no tile straddles
+// the two halves, so every tile sums over its own half's list only). Per slab of TK inner
+// indices every thread loads 16 + 16 values one slab ahead into registers (the gathers'
+// index lists live in LDS), so the global round trip overlaps the MFMAs of the current slab.
+// LDS: sA[k][r] rows of kPA doubles (2-way banks for the B-operand reads), sBt[c][k] rows of
+// kPB (the A-operand reads; the transposed stores stay contiguous).
+constexpr int TM = 64, TK = 64, kFetch = TK * TM / 256, kPA = TM + 16, kPB = TK + 4;
+constexpr size_t kGemmTileLds = sizeof(double) * (size_t)(TK * kPA + TM * kPB);
+typedef double dc_d4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void dc_gemm_kernel(const double* __restrict__ Q, double* __restrict__ Qn, long ldq,
-                                                      const int* __restrict__ mg, DcWs w) {
-  __shared__ double sA[TK][TM + 1];
-  __shared__ double sB[TK][TM + 1];
-  const int lo = mg[3 * blockIdx.y], hi = mg[3 * blockIdx.y + 2];
-  const int s = hi - lo;
-  const int tiles = (s + TM - 1) / TM;
-  if ((int)blockIdx.x >= tiles * tiles) return;
-  const int r0 = (blockIdx.x % tiles) * TM, c0 = (blockIdx.x / tiles) * TM;
+                                                      const int* __restrict__ mg, DcWs w, int rtm) {
+  extern __shared__ double gsm[];
+  double* sA = gsm;              // [TK][kPA]: Q[rows r0.., list entry j0 + k]
+  double* sBt = gsm + TK * kPA;  // [TM][kPB]: U[list entry j0 + k, column c0 + c]
+  int* sidx = (int*)(sBt + TM * kPB);  // [smax] Q column, [smax] U row of list entry t
+  const int lo = mg[3 * blockIdx.y], mid = mg[3 * blockIdx.y + 1], hi = mg[3 * blockIdx.y + 2];
+  const int s = hi - lo, s1 = mid - lo;
+  const int nu = (s1 + TM - 1) / TM, rtiles = nu + (s - s1 + TM - 1) / TM, ctiles = (s + TM - 1) / TM;
+  const int rt = (int)blockIdx.x % rtm, ct = (int)blockIdx.x / rtm;
+  if (rt >= rtiles || ct >= ctiles) return;
+  const bool upper = rt < nu;
+  const int r0 = upper ? rt * TM : s1 + (rt - nu) * TM;
+  const int rend = upper ? (r0 + TM < s1 ? r0 + TM : s1) : (r0 + TM < s ? r0 + TM : s);
+  const int c0 = ct * TM;
   const int k = w.kcnt[lo];
-  const int tid = threadIdx.x;
-  const int tr = (tid & 15) * 4, tc = (tid >> 4) * 4;  // 4 x 4 outputs per thread
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int* cs = w.colsrc + lo;
   if (c0 >= k) {  // deflated columns only: copies
     for (int q = tid; q < TM * TM; q += 256) {
       const int r = r0 + (q & 63), c = c0 + (q >> 6);
-      if (r < s && c < s) Qn[(long)(lo + c) * ldq + lo + r] = Q[(long)cs[c] * ldq + lo + r];
+      if (r < rend && c < s) Qn[(long)(lo + c) * ldq + lo + r] = Q[(long)cs[c] * ldq + lo + r];
     }
     return;
   }
-  double acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+  const int* jlist = upper ? w.jl + lo : w.jr + lo;
+  const int kk = upper ? w.kl[lo] : w.kr[lo];
+  int* sJ = sidx;
+  int* sU = sidx + s;
+  for (int t = tid; t < kk; t += 256) {
+    const int j = jlist[t];
+    sU[t] = j;
+    sJ[t] = cs[j];
+  }
+  __syncthreads();
   const double* U = w.U + (long)lo * w.ldu;
-  for (int j0 = 0; j0 < k; j0 += TK) {
-    for (int q = tid; q < TK * TM; q += 256) {
+  double ra[kFetch], rb[kFetch];
+  auto fetch = [&](int j0) {
+#pragma unroll
+    for (int i = 0; i < kFetch; ++i) {
+      const int q = tid + 256 * i;
       {  // A: rows r0.. (consecutive threads, consecutive rows), inner j0.. (column gather)
-        const int jj = q / TM, rr = q % TM;
-        const int j = j0 + jj, r = r0 + rr;
-        sA[jj][rr] = (j < k && r < s) ? Q[(long)cs[j] * ldq + lo + r] : 0.0;
+        const int t = j0 + q / TM, r = r0 + q % TM;
+        ra[i] = (t < kk && r < rend) ? Q[(long)sJ[t] * ldq + lo + r] : 0.0;
       }
       {  // B: inner j0.. (consecutive threads along a column of U), columns c0..
-        const int jj = q % TK, cc = q / TK;
-        const int j = j0 + jj, c = c0 + cc;
-        sB[jj][cc] = (j < k && c < k) ? U[(long)c * k + j] : 0.0;
+        const int t = j0 + q % TK, c = c0 + q / TK;
+        rb[i] = (t < kk && c < k) ? U[(long)c * k + sU[t]] : 0.0;
       }
     }
+  };
+  dc_d4 acc[2][2];
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = dc_d4{0.0, 0.0, 0.0, 0.0};
+  const int wr = wv & 1, wc = wv >> 1;  // this wave's 32 x 32: rows wr 32.., columns wc 32..
+  const int l15 = lane & 15, l4 = lane >> 4;
+  fetch(0);
+  for (int j0 = 0; j0 < kk; j0 += TK) {
+#pragma unroll
+    for (int i = 0; i < kFetch; ++i) {
+      const int q = tid + 256 * i;
+      sA[(q / TM) * kPA + q % TM] = ra[i];
+      sBt[(q / TK) * kPB + q % TK] = rb[i];
+    }
     __syncthreads();
+    if (j0 + TK < kk) fetch(j0 + TK);  // in flight under this slab's MFMAs
 #pragma unroll
-    for (int jj = 0; jj < TK; ++jj) {
-      double a[4], b[4];
+    for (int kq = 0; kq < TK / 4; ++kq) {
+      const int kb = 4 * kq + l4;
+      double av[2], bv[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = sA[jj][tr + q];
-        b[q] = sB[jj][tc + q];
+      for (int h = 0; h < 2; ++h) {
+        av[h] = sBt[(wc * 32 + 16 * h + l15) * kPB + kb];  // A' = U^T: row c, inner k
+        bv[h] = sA[kb * kPA + wr * 32 + 16 * h + l15];      // B' = Q^T: inner k, column r
       }
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
+      for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = fma(a[x], b[y], acc[x][y]);
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], bv[bj], acc[bi][bj], 0, 0, 0);
     }
     __syncthreads();
   }
+  // D[i][j]: i = column c (row of the accumulator tile) = l4 + 4 reg, j = row r = lane & 15
 #pragma unroll
-  for (int y = 0; y < 4; ++y) {
-    const int c = c0 + tc + y;
-    if (c >= s) continue;
+  for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int r = r0 + tr + x;
-      if (r >= s) continue;
-      Qn[(long)(lo + c) * ldq + lo + r] = c < k ? acc[x][y] : Q[(long)cs[c] * ldq + lo + r];
-    }
-  }
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = c0 + wc * 32 + 16 * bi + l4 + 4 * g;
+        const int r = r0 + wr * 32 + 16 * bj + l15;
+        if (c < s && r < rend) Qn[(long)(lo + c) * ldq + lo + r] = c < k ? acc[bi][bj][g] : Q[(long)cs[c] * ldq + lo + r];
+      }
 }
 
 // the merged blocks of Qn back into Q (positions not merged at this level keep theirs)
@@ -506,15 +759,19 @@ __global__ __launch_bounds__(256) void dc_copyback_kernel(const double* __restri
   }
 }
 
-size_t prep_lds(int smax) { return (size_t)smax * (2 * sizeof(double) + 3 * sizeof(int)); }
+size_t prep_lds(int smax) { return (size_t)smax * (2 * sizeof(double) + 4 * sizeof(int)); }
 
 }  // namespace
 
 HARP_EXPORT int harp_dc_max_n() { return kMaxN; }
 
+HARP_EXPORT int harp_dc_prep_stamps(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prep_t), sizeof(long long) * 9) == hipSuccess ? HARP_OK : HARP_ELAUNCH;
+}
+
 // doubles of the workspace for size n: Qb n^2, U n^2, dd/zz/tau/zh/rho/rotc/rots 7 n, sort
-// scratch 3 n; ints (colsrc/org/kcnt/rotp/rotq 5 n) follow as 3 n doubles
-HARP_EXPORT long harp_dc_ws_doubles(int n) { return 2L * n * n + 10L * n + 3L * n + 16; }
+// scratch 3 n; ints (colsrc/org/kcnt/rotp/rotq/jl/jr/kl/kr 9 n) follow as 5 n doubles
+HARP_EXPORT long harp_dc_ws_doubles(int n) { return 2L * n * n + 10L * n + 5L * n + 16; }
 
 // Eigen-decomposition of the symmetric tridiagonal (dmod, e): dmod is the diagonal with
 // |e[mid - 1]| already subtracted at d[mid - 1] and d[mid] for every merge (harp_amd/ops/eig.py),
@@ -545,6 +802,10 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
   w.kcnt = ip + 2 * n;
   w.rotp = ip + 3 * n;
   w.rotq = ip + 4 * n;
+  w.jl = ip + 5 * n;
+  w.jr = ip + 6 * n;
+  w.kl = ip + 7 * n;
+  w.kr = ip + 8 * n;
   for (int l = 0; l < nlevels; ++l) {
     const int m0 = level_off[l], nm = level_off[l + 1] - m0;
     const int smax = level_smax[l];
@@ -563,8 +824,12 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
     dc_secular_kernel<<<dim3(wg), dim3(256), 0, st>>>(mg, nm, n, dmod, w);
     dc_loewner_kernel<<<dim3(wg), dim3(256), 0, st>>>(mg, nm, n, w);
     dc_vectors_kernel<<<dim3(wg), dim3(256), 0, st>>>(mg, nm, n, w);
-    const int tiles = (smax + TM - 1) / TM;
-    dc_gemm_kernel<<<dim3((unsigned)(tiles * tiles), (unsigned)nm), dim3(256), 0, st>>>(Q, Qb, n, mg, w);
+    const int tiles = (smax + TM - 1) / TM, rtm = tiles + 1;  // row tiles: + 1 for the split
+    const size_t glds = kGemmTileLds + 2 * sizeof(int) * (size_t)smax;
+    if (glds > 65536 && hipFuncSetAttribute((const void*)dc_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)glds) != hipSuccess)
+      return HARP_ELAUNCH;
+    dc_gemm_kernel<<<dim3((unsigned)(rtm * tiles), (unsigned)nm), dim3(256), glds, st>>>(Q, Qb, n, mg, w, rtm);
     const long per = (long)smax * smax;
     const unsigned cb = (unsigned)((per + 256 * 4 - 1) / (256 * 4));
     dc_copyback_kernel<<<dim3(cb, (unsigned)nm), dim3(256), 0, st>>>(Qb, Q, n, mg);

@@ -35,6 +35,7 @@ _lib.register({
     "harp_sytrd_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                          _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
     "harp_dc_max_n": [],
+    "harp_dc_prep_stamps": [_lib.c_void_p],
     "harp_dc_ws_doubles": [_lib.c_int],
     # dmod, e, n, Q, merges, level_off, level_smax, nlevels, ws, stream
     "harp_dc_tridiag": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
@@ -92,20 +93,21 @@ def eigvalsh(C: torch.Tensor, stamps: torch.Tensor | None = None, native: bool |
     if nb < 1:
         return torch.linalg.eigvalsh(C)
     if VARIANT == "ll" and stamps is None:
-        r = sytrd_ll(C, vectors=False)
+        r = sytrd_ll(C, vectors=False, check=False)
         if r is not None:
-            d, e = r[0], r[1]
+            d, e, ws = r[0], r[1], r[4]
             w = torch.empty(n, dtype=torch.float64, device=dev)
             _lib.check(k.harp_tridiag_eigvals(d.data_ptr(), e.data_ptr(), n, w.data_ptr(), _lib.stream_ptr(dev)),
                        "tridiag_eigvals")
-            return w
+            if _ll_ok(ws):
+                return w
     A = C.contiguous().clone()  # symmetric: row-major storage is the column-major matrix
     ws = torch.zeros(int(k.harp_eig_ws_ints()), dtype=torch.int32, device=dev)
     wsd = torch.zeros(3 * n + 4, dtype=torch.float64, device=dev)
     d = torch.empty(n, dtype=torch.float64, device=dev)
     e = torch.empty(n, dtype=torch.float64, device=dev)
     w = torch.empty(n, dtype=torch.float64, device=dev)
-    if VARIANT in ("fused", "ll") == "fused" and stamps is None:
+    if VARIANT in ("fused", "ll") and stamps is None:
         st = k.harp_eig_sym_fused(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), w.data_ptr(), nb, ws.data_ptr(),
                                   wsd.data_ptr(), _lib.stream_ptr(dev))
     else:
@@ -130,11 +132,25 @@ def ll_usable(n: int) -> bool:
 _LL_WARNED = [False]
 
 
-def sytrd_ll(C: torch.Tensor, vectors: bool = True):
+def _ll_ok(ws: torch.Tensor) -> bool:
+    """Host check of the chip-wide reduction's error word (a workgroup timed out)."""
+    if int(ws[2].item()):
+        if not _LL_WARNED[0]:
+            warnings.warn("chip-wide tridiagonalisation timed out (workgroups not co-resident); "
+                          "using the one-XCD reduction")
+            _LL_WARNED[0] = True
+        return False
+    return True
+
+
+def sytrd_ll(C: torch.Tensor, vectors: bool = True, check: bool = True):
     """Tridiagonalise the symmetric fp64 GPU matrix ``C`` (n <= 1024) with the chip-wide
     kernel: returns (d, e, Vt, tau) -- Vt row k = v_k, tau_k as :func:`back_transform` takes
     them (None when ``vectors`` is False) -- or None when the kernel is not applicable or a
-    workgroup timed out (not all of them co-resident)."""
+    workgroup timed out (not all of them co-resident). ``check=False``: no host sync; returns
+    (d, e, Vt, tau, ws) and the caller checks ``ws`` with :func:`_ll_ok` after queueing
+    the work that follows (so its launches overlap the reduction; the outputs of a timed-out
+    call are finite: zero-initialised and partly written)."""
     n = C.shape[0]
     if not ll_usable(n):
         return None
@@ -143,18 +159,16 @@ def sytrd_ll(C: torch.Tensor, vectors: bool = True):
     A = C.contiguous()
     ws = torch.zeros(int(k.harp_eig_ws_ints()), dtype=torch.int32, device=dev)
     gran = torch.zeros(int(k.harp_sytrd_ll_gran_words()), dtype=torch.int64, device=dev)
-    d = torch.empty(n, dtype=torch.float64, device=dev)
+    d = torch.zeros(n, dtype=torch.float64, device=dev)
     e = torch.zeros(max(n, 1), dtype=torch.float64, device=dev)
     Vt = torch.zeros((n, n), dtype=torch.float64, device=dev) if vectors else None
     tau = torch.zeros(n, dtype=torch.float64, device=dev) if vectors else None
     st = k.harp_sytrd_ll(A.data_ptr(), n, n, d.data_ptr(), e.data_ptr(), _lib.ptr(Vt), n, _lib.ptr(tau),
                          ws.data_ptr(), gran.data_ptr(), _lib.stream_ptr(dev))
     _lib.check(st, "sytrd_ll")
-    if int(ws[2].item()):
-        if not _LL_WARNED[0]:
-            warnings.warn("chip-wide tridiagonalisation timed out (workgroups not co-resident); "
-                          "using the one-XCD reduction")
-            _LL_WARNED[0] = True
+    if not check:
+        return d, e, Vt, tau, ws
+    if not _ll_ok(ws):
         return None
     return d, e, Vt, tau
 
@@ -227,11 +241,12 @@ def eigh(C: torch.Tensor, native: bool | None = None):
     dev = C.device
     k = _lib.kernels()
     if VARIANT == "ll":
-        r = sytrd_ll(C)
+        r = sytrd_ll(C, check=False)
         if r is not None:
-            d, e, Vt, tau = r
-            lam, Z = eigh_tridiag(d, e[:max(n - 1, 0)])
-            return lam, back_transform(Vt, tau, Z)
+            d, e, Vt, tau, ws = r
+            out = _dc_and_back_transform(d, e[:max(n - 1, 0)], Vt, tau)
+            if _ll_ok(ws):  # one sync, after the D&C and back-transform are queued
+                return out
     nb = int(k.harp_eig_workgroups(n, int(os.environ.get("HARP_EIG_NB", NB_DEFAULT))))
     if nb < 1:
         return torch.linalg.eigh(C)
@@ -250,8 +265,58 @@ def eigh(C: torch.Tensor, native: bool | None = None):
         warnings.warn(f"one-XCD reduction did not run cooperatively (claims {claims}/{nb}, error {err}); "
                       "using torch.linalg.eigh")
         return torch.linalg.eigh(C)
-    lam, Z = eigh_tridiag(d, e[:max(n - 1, 0)])
-    return lam, back_transform(Vt, tau, Z)
+    return _dc_and_back_transform(d, e[:max(n - 1, 0)], Vt, tau)
+
+
+_SIDE: dict = {}
+
+
+def _dc_and_back_transform(d, e, Vt, tau):
+    """D&C eigenvectors Z of the tridiagonal, X = Q Z. The WY factor M = V T of Q depends only
+    on the reflectors, so it is formed on a side stream while the D&C runs (the D&C's lower
+    tree levels fill a fraction of the chip); what is left after the D&C is two GEMMs."""
+    dev = d.device
+    cur = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        wy = wy_factor(Vt, tau)
+    Vt.record_stream(side)
+    tau.record_stream(side)
+    lam, Z = eigh_tridiag(d, e)
+    cur.wait_stream(side)
+    if wy is None:
+        return lam, Z
+    Vm, Mt = wy
+    Mt.record_stream(cur)
+    Vm.record_stream(cur)
+    return lam, apply_wy(Vm, Mt, Z)
+
+
+def wy_factor(Vt: torch.Tensor, tau: torch.Tensor):
+    """Compact-WY factor of H_0 H_1 ... H_{n-3} (``Vt`` row c = v_c): Q = I - V T V^T with
+    T^-1 = diag(1/tau) + striu(V^T V); returns (V^T, M^T) with M = V T (one GEMM and one
+    triangular solve), or None for n <= 2 (Q = I). A reflector with tau = 0 is the
+    identity (its column of V is zeroed, no host sync)."""
+    n = Vt.shape[1]
+    m = n - 2
+    if m <= 0:
+        return None
+    t = tau[:m]
+    live = t != 0
+    Vm = Vt[:m] * live.to(Vt.dtype).unsqueeze(1)  # V^T, m x n
+    Tinv = torch.triu(Vm @ Vm.t(), 1)
+    Tinv.diagonal().copy_(torch.where(live, 1.0 / torch.where(live, t, torch.ones_like(t)), torch.ones_like(t)))
+    # M^T = T^T V^T = Tinv^-T V^T: a lower-triangular solve with n right-hand sides
+    Mt = torch.linalg.solve_triangular(Tinv.t(), Vm, upper=False)
+    return Vm, Mt
+
+
+def apply_wy(Vm: torch.Tensor, Mt: torch.Tensor, Z: torch.Tensor) -> torch.Tensor:
+    """X = Q Z = Z - M (V^T Z) for the factor of :func:`wy_factor`."""
+    return torch.addmm(Z, Mt.t(), Vm @ Z, alpha=-1.0)
 
 
 def back_transform(Vt: torch.Tensor, tau: torch.Tensor, Z: torch.Tensor) -> torch.Tensor:

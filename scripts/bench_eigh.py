@@ -5,6 +5,7 @@ after 3 warm-ups, on the PCA correlation matrix shape (uniform data, spectrum ar
 
     python scripts/bench_eigh.py [n]
 """
+import ctypes
 import json
 import statistics
 import sys
@@ -96,7 +97,14 @@ def main():
     rec["sytrd_fused_ms"] = timed(fused)
     lam, Z = E.eigh_tridiag(d, e[:n - 1])
     rec["dc_ms"] = timed(lambda: E.eigh_tridiag(d, e[:n - 1]))
+    st = (ctypes.c_longlong * 9)()
+    E._lib.check(k.harp_dc_prep_stamps(ctypes.cast(st, ctypes.c_void_p)), "dc_prep_stamps")
+    rec["dc_top_prep_cycles"] = [st[i + 1] - st[i] for i in range(8)]
     rec["back_transform_ms"] = timed(lambda: E.back_transform(Vt, tau, Z))
+    rec["wy_factor_ms"] = timed(lambda: E.wy_factor(Vt, tau))
+    Vm, Mt = E.wy_factor(Vt, tau)
+    rec["apply_wy_ms"] = timed(lambda: E.apply_wy(Vm, Mt, Z))
+    rec["wy_vs_back_transform"] = float((E.apply_wy(Vm, Mt, Z) - E.back_transform(Vt, tau, Z)).abs().max())
     for var in ("ll", "fused"):
         E.VARIANT = var
         rec[f"eigh_{var}_ms"] = timed(lambda: E.eigh(C))

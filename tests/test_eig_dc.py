@@ -75,3 +75,22 @@ def test_back_transform_recovers_eigenvectors():
     Xv = EIG.back_transform(torch.from_numpy(Vt), torch.from_numpy(tau), torch.from_numpy(Z)).numpy()
     assert np.abs(Xv.T @ Xv - np.eye(n)).max() <= 1e-12
     assert np.abs(A @ Xv - Xv * w).max() <= 1e-12 * np.linalg.norm(A, 2)
+
+
+def test_wy_factor_matches_back_transform():
+    """The side-stream split (M = V T formed before the D&C, then two GEMMs) equals the
+    one-shot compact-WY back-transform, including a tau = 0 (identity) reflector."""
+    rng = np.random.default_rng(2)
+    n = 48
+    X = rng.standard_normal((n, n))
+    A = X + X.T
+    d, e, Vt, tau = _householder_tridiag(A)
+    tau[5] = 0.0
+    Vt[5] = rng.standard_normal(n)  # ignored: tau = 0
+    w, Z = eigh_tridiag(d, e)
+    Vt_t, tau_t, Z_t = (torch.from_numpy(a) for a in (Vt, tau, Z))
+    ref = EIG.back_transform(Vt_t, tau_t, Z_t)
+    Vm, Mt = EIG.wy_factor(Vt_t, tau_t)
+    got = EIG.apply_wy(Vm, Mt, Z_t)
+    assert torch.allclose(got, ref, rtol=0, atol=1e-13)
+    assert EIG.wy_factor(Vt_t[:2, :2], tau_t[:2]) is None
