@@ -23,6 +23,8 @@
 //   decode_replace: LDS = 0, scatter slot entries, LDS -> row                      (1 write)
 //   decode_add    : atomic adds of the slot entries into the row (several peers may
 //                   push into one owner row within one launch)
+//   merge         : owner table held as slots itself: canonical slot += pushed delta slots,
+//                   re-encoded in place (no dense table, no encode pass for the pull)
 // Received payloads are bounds-checked (nnz clamped to the slot, topics < K).
 #include "common.h"
 
@@ -327,6 +329,214 @@ __global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_copy_slots_kernel(
   }
 }
 
+// Owner-side merge for a table held in slot form (sparse owner table): canonical slot u :=
+// slot u + every delta slot pushed for its row (src_idx[src_ptr[u] .. src_ptr[u + 1])),
+// written back in place without zero counts (the form the samplers and copy_slots read;
+// topic order within a slot is free). One wave per row, grid-stride over a row list. Rows
+// come in two classes the host fixes once from the slot capacities (static bounds):
+//  * rows with at most 64 / 256 / 512 entries (old + pushed; a word's handful of tokens is the
+//    common case at an 8-rank share): 16 / 32 / 64 lanes and a 128 / 512 / 1024-entry
+//    open-addressing LDS hash per row, four / two / one rows per wave, so a wave overlaps
+//    several rows' chains of dependent slot loads;
+//  * big rows: a K-int LDS accumulator plus a K-bit bitmap of the touched topics, re-zeroed
+//    only where touched (ascending output).
+// Dense canonical rows (cap < 0) take the deltas as atomic adds. overflow |= 1: a row
+// exceeded its capacity; |= 2: a count went negative.
+// row classes by entry bound: (G lanes, S hash entries) per row
+constexpr int kTinyBound = 64, kSmallBound = 256, kHashBound = 512;  // (16, 128), (32, 512), (64, 1024)
+
+// every (topic, value) of the canonical slot (sparse) and of the row's delta slots
+template <class F>
+__device__ __forceinline__ void merge_entries(const unsigned char* slot, int c, int q0, int q1,
+                                              const int* __restrict__ src_idx, const unsigned char* __restrict__ in,
+                                              const long* __restrict__ in_off, const int* __restrict__ in_cap, int K,
+                                              int lane, F&& f, int stride = 64) {
+  if (c >= 0) {
+    int nnz = *(const int*)slot;
+    nnz = nnz < 0 ? 0 : (nnz > c ? c : nnz);
+    const int* ocn = slot_counts(slot);
+    const unsigned short* otp = slot_topics(slot, c);
+    for (int e = lane; e < nnz; e += stride) {
+      const int t = otp[e];
+      if (t < K) f(t, ocn[e]);
+    }
+  }
+  for (int q = q0; q < q1; ++q) {
+    const int si = src_idx[q];
+    const unsigned char* ds = in + in_off[si];
+    const int dc = in_cap[si];
+    if (dc < 0) {
+      for (int t = lane; t < K; t += stride) {
+        const int v = ((const int*)ds)[t];
+        if (v) f(t, v);
+      }
+    } else {
+      int nz = *(const int*)ds;
+      nz = nz < 0 ? 0 : (nz > dc ? dc : nz);
+      const int* dcn = slot_counts(ds);
+      const unsigned short* dtp = slot_topics(ds, dc);
+      for (int e = lane; e < nz; e += stride) {
+        const int t = dtp[e], v = dcn[e];
+        if (v && t < K) f(t, v);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void hash_add(int* hk, int* hv, int slots, int t, int v, bool& over) {
+  unsigned h = ((unsigned)t * 2654435761u) >> 16;
+  for (int probe = 0;; ++probe) {
+    h &= (unsigned)(slots - 1);
+    if (probe == slots) {  // table full: the host's row bound was wrong (never loops)
+      over = true;
+      return;
+    }
+    const int k = atomicCAS(&hk[h], -1, t);
+    if (k == -1 || k == t) {
+      atomicAdd(&hv[h], v);
+      return;
+    }
+    ++h;
+  }
+}
+
+// G lanes per row (256 / G rows per workgroup), an S-entry LDS hash per row (S >= 2 x the
+// class bound); the G-lane groups of one wave run different rows, so the wave overlaps
+// their dependent slot loads
+template <int G, int S>
+__global__ __launch_bounds__(256) void rowcodec_merge_group_kernel(
+    unsigned char* __restrict__ canon, const long* __restrict__ c_off, const int* __restrict__ c_cap,
+    const int* __restrict__ rows, int nrows, const int* __restrict__ src_ptr, const int* __restrict__ src_idx,
+    const unsigned char* __restrict__ in, const long* __restrict__ in_off, const int* __restrict__ in_cap, int K,
+    int* __restrict__ overflow) {
+  constexpr int R = 256 / G;
+  __shared__ int keys[R][S];
+  __shared__ int vals[R][S];
+  const int grp = threadIdx.x / G, gl = threadIdx.x % G, gshift = (threadIdx.x & 63) / G * G;
+  int* hk = keys[grp];
+  int* hv = vals[grp];
+  for (int i = gl; i < S; i += G) {
+    hk[i] = -1;
+    hv[i] = 0;
+  }
+  bool over = false, neg = false;
+  const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1ull);
+  for (int j = blockIdx.x * R + grp; j < nrows; j += gridDim.x * R) {
+    const int u = rows[j];
+    unsigned char* slot = canon + c_off[u];
+    const int c = c_cap[u];  // >= 0: these classes are sparse rows
+    merge_entries(slot, c, src_ptr[u], src_ptr[u + 1], src_idx, in, in_off, in_cap, K, gl,
+                  [&](int t, int v) { hash_add(hk, hv, S, t, v, over); }, G);
+    int* ocn = (int*)(slot + 4);
+    unsigned short* otp = (unsigned short*)(slot + 4 + 4 * (long)c);
+    const unsigned long long below = (1ull << gl) - 1ull;
+    int base = 0;
+    for (int i0 = 0; i0 < S; i0 += G) {
+      const int i = i0 + gl;
+      const int t = hk[i], v = hv[i];
+      const bool keep = t >= 0 && v != 0;
+      neg |= v < 0;
+      const unsigned long long m = (__ballot(keep) >> gshift) & gmask;  // this row's G lanes
+      if (keep) {
+        const int pos = base + __popcll(m & below);
+        if (pos < c) {
+          ocn[pos] = v;
+          otp[pos] = (unsigned short)t;
+        } else {
+          over = true;
+        }
+      }
+      base += __popcll(m);
+      hk[i] = -1;
+      hv[i] = 0;
+    }
+    if (gl == 0) *(int*)slot = base < c ? base : c;
+  }
+  if (over) atomicOr(overflow, 1);
+  if (neg) atomicOr(overflow, 2);
+}
+
+__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_merge_kernel(
+    unsigned char* __restrict__ canon, const long* __restrict__ c_off, const int* __restrict__ c_cap,
+    const int* __restrict__ rows, int nrows, const int* __restrict__ src_ptr, const int* __restrict__ src_idx,
+    const unsigned char* __restrict__ in, const long* __restrict__ in_off, const int* __restrict__ in_cap, int K,
+    int per_wave, int* __restrict__ overflow) {
+  extern __shared__ int lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, W = blockDim.x >> 6;
+  int* acc = lds + w * per_wave;
+  const int nbw = (K + 31) >> 5;
+  unsigned* bits = (unsigned*)(acc + K);
+  for (int i = lane; i < K + nbw; i += 64) acc[i] = 0;
+  bool over = false, neg = false;
+  for (int j = blockIdx.x * W + w; j < nrows; j += gridDim.x * W) {
+    const int u = rows[j];
+    unsigned char* slot = canon + c_off[u];
+    const int c = c_cap[u];
+    const int q0 = src_ptr[u], q1 = src_ptr[u + 1];
+    if (c < 0) {  // dense canonical row
+      int* row = (int*)slot;
+      merge_entries(slot, c, q0, q1, src_idx, in, in_off, in_cap, K, lane, [&](int t, int v) { atomicAdd(row + t, v); });
+      continue;
+    }
+    merge_entries(slot, c, q0, q1, src_idx, in, in_off, in_cap, K, lane, [&](int t, int v) {
+      atomicAdd(&acc[t], v);
+      atomicOr(&bits[t >> 5], 1u << (t & 31));
+    });
+    int* ocn = (int*)(slot + 4);
+    unsigned short* otp = (unsigned short*)(slot + 4 + 4 * (long)c);
+    // compaction in topic order: lane L scans bitmap word wb + L (32 topics)
+    int base = 0;
+    for (int wb = 0; wb < nbw; wb += 64) {
+      const int wi = wb + lane;
+      const unsigned m = wi < nbw ? bits[wi] : 0u;
+      int mine = 0;
+      for (unsigned mm = m; mm; mm &= mm - 1) {
+        const int v = acc[(wi << 5) + __builtin_ctz(mm)];
+        mine += v != 0;
+        neg |= v < 0;
+      }
+      const float incl = wave_scan_incl((float)mine);  // <= 64 x 32: exact
+      int pos = base + (int)incl - mine;
+      for (unsigned mm = m; mm; mm &= mm - 1) {
+        const int t = (wi << 5) + __builtin_ctz(mm);
+        const int v = acc[t];
+        if (v != 0) {
+          if (pos < c) {
+            ocn[pos] = v;
+            otp[pos] = (unsigned short)t;
+          } else {
+            over = true;
+          }
+          ++pos;
+        }
+        acc[t] = 0;
+      }
+      if (wi < nbw) bits[wi] = 0u;
+      base += (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+    }
+    if (lane == 0) *(int*)slot = base < c ? base : c;
+  }
+  if (__ballot(over) && lane == 0) atomicOr(overflow, 1);
+  if (__ballot(neg) && lane == 0) atomicOr(overflow, 2);
+}
+
+// empty every slot for a kernel to fill: the nnz word of a sparse slot, the whole row of a
+// dense one (the entries past nnz are never read), instead of clearing the whole payload
+__global__ __launch_bounds__(kMaxWaves * 64) void rowcodec_reset_kernel(unsigned char* __restrict__ buf,
+                                                                       const long* __restrict__ off,
+                                                                       const int* __restrict__ cap, int n, int K) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, W = blockDim.x >> 6;
+  for (int j = blockIdx.x * W + w; j < n; j += gridDim.x * W) {
+    unsigned char* slot = buf + off[j];
+    if (cap[j] < 0) {
+      int4* s4 = (int4*)slot;
+      for (int q = lane; q < K / 4; q += 64) s4[q] = make_int4(0, 0, 0, 0);
+    } else if (lane == 0) {
+      *(int*)slot = 0;
+    }
+  }
+}
+
 inline bool bad_shape(long ld, int K) { return K <= 0 || (K & 3) || ld < K || (ld & 3) || 4L * K > kLdsBudget; }
 // waves (rows) per workgroup so that the LDS rows fit the default dynamic-LDS limit
 inline int waves_for(int K) {
@@ -394,6 +604,61 @@ HARP_EXPORT int harp_rowcodec_decode_add16(unsigned short* dst, long ld, int K, 
   const int wv = waves_for(K);
   const dim3 grid((n + wv - 1) / wv), block(wv * 64);
   rowcodec_decode_add16_kernel<<<grid, block, 0, s>>>(dst, ld, K, rows, n, slot_off, cap, (const unsigned char*)in);
+  return harp_launch_status();
+}
+
+// canonical slots u (canon + c_off[u], cap c_cap[u]) += the delta slots src_idx[src_ptr[u] ..
+// src_ptr[u + 1]) of `in` (in_off / in_cap), re-encoded in place: the rows listed in
+// tiny / small / hash rows (entry bounds: harp_rowcodec_merge_bounds) by the lane-group LDS
+// hash kernels, the rows in big_rows by the dense-accumulator kernel
+// class bounds, smallest first: rows with at most bound[i] entries go to list i
+HARP_EXPORT int harp_rowcodec_merge_bounds(int* out3) {
+  out3[0] = kTinyBound;
+  out3[1] = kSmallBound;
+  out3[2] = kHashBound;
+  return HARP_OK;
+}
+
+HARP_EXPORT int harp_rowcodec_merge(void* canon, const long* c_off, const int* c_cap, const int* tiny_rows,
+                                    int n_tiny, const int* small_rows, int n_small, const int* hash_rows, int n_hash,
+                                    const int* big_rows, int n_big, const int* src_ptr, const int* src_idx,
+                                    const void* in, const long* in_off, const int* in_cap, int K, int* overflow,
+                                    hipStream_t s) {
+  if (n_tiny < 0 || n_small < 0 || n_hash < 0 || n_big < 0 || K <= 0 || (K & 3) || K > 16384 ||
+      misaligned(canon) || misaligned(in) || !overflow)
+    return HARP_EBADARG;
+  auto group = [&](auto kern, const int* rows, int nr, int per_wg) {
+    int grid = (nr + per_wg - 1) / per_wg;
+    if (grid > 16384) grid = 16384;
+    kern<<<dim3((unsigned)grid), dim3(256), 0, s>>>((unsigned char*)canon, c_off, c_cap, rows, nr, src_ptr, src_idx,
+                                                   (const unsigned char*)in, in_off, in_cap, K, overflow);
+  };
+  if (n_tiny > 0) group(rowcodec_merge_group_kernel<16, 128>, tiny_rows, n_tiny, 16);
+  if (n_small > 0) group(rowcodec_merge_group_kernel<32, 512>, small_rows, n_small, 8);
+  if (n_hash > 0) group(rowcodec_merge_group_kernel<64, 1024>, hash_rows, n_hash, 4);
+  if (n_big > 0) {
+    const int per_wave = (K + (K + 31) / 32 + 3) & ~3;  // ints: accumulator + bitmap
+    int wv = kLdsBudget / (4 * per_wave);
+    wv = wv < 1 ? 1 : (wv > kMaxWaves ? kMaxWaves : wv);
+    int grid = (n_big + wv - 1) / wv;
+    if (grid > 4096) grid = 4096;
+    const size_t lds = sizeof(int) * (size_t)per_wave * wv;
+    if (lds > 65536 && hipFuncSetAttribute((const void*)rowcodec_merge_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return HARP_ELAUNCH;
+    rowcodec_merge_kernel<<<dim3((unsigned)grid), dim3(wv * 64), lds, s>>>(
+        (unsigned char*)canon, c_off, c_cap, big_rows, n_big, src_ptr, src_idx, (const unsigned char*)in, in_off,
+        in_cap, K, per_wave, overflow);
+  }
+  return harp_launch_status();
+}
+
+HARP_EXPORT int harp_rowcodec_reset(void* buf, const long* off, const int* cap, int n, int K, hipStream_t s) {
+  if (n < 0 || K <= 0 || (K & 3) || misaligned(buf)) return HARP_EBADARG;
+  if (n == 0) return HARP_OK;
+  int grid = (n + kMaxWaves - 1) / kMaxWaves;
+  if (grid > 8192) grid = 8192;
+  rowcodec_reset_kernel<<<dim3((unsigned)grid), dim3(kMaxWaves * 64), 0, s>>>((unsigned char*)buf, off, cap, n, K);
   return harp_launch_status();
 }
 

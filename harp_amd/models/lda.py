@@ -57,6 +57,7 @@ class LDAConfig:
     min_bound: int = 0        # with a budget: retune it every iteration so the trained percentage lands
     max_bound: int = 0        # in [min_bound, max_bound] (dymoro.BudgetTuner); 0 / 0: the budget stays fixed
     deterministic: bool = False  # GPU: one wave samples in order (bit-reproducible; tests / debugging only)
+    owner_slots: bool = True  # fused rows: the owner holds its table as the canonical pull slots (merge on push)
     fused_rows: bool = True   # push-pull over sparse rows, GPU dense sampler: sample straight from the pull
                               # payload into the push payload (no dense local table, no decode / re-encode)
 
@@ -520,13 +521,21 @@ class LDAPushPullMapper(LDACollectiveMapper):
             self.glob = PackedTable(owned, gbuf, table_id=1, combiner=self.sum)
             self.glob.static_layout = True
             self.before = self.want_pt = None
-            self.ps.push(self.pull_buf, self._glob_rows(), delta=False)  # initial counts into an empty model
             # fused rows: the dense sampler reads the pull payload and writes the push payload
             # itself, so the dense local table is only the initial-count source
             # (the sparse doc-span sampler too: the doc-order lists replace the doc table)
             self.fused = (cfg.fused_rows and dev.type == "cuda" and L._lib.use_native(self.tz)
                           and ((not self.sparse and K <= 1024)
                                or (self.sparse and self.ndk is None and L.SPAN and K <= L.MAX_TOPICS)))
+            # fused rows + owner slots: the owner's table is held as the canonical slots the
+            # pull sends, so a sweep has no pull encode and the push is a slot merge (the dense
+            # table is filled only for the likelihood / checkpoints, _sync_glob)
+            if self.fused and cfg.owner_slots:
+                self.ps.use_owner_slots()
+                self.ps.push_initial(self.pull_buf)
+                self._glob_stale = True
+            else:
+                self.ps.push(self.pull_buf, self._glob_rows(), delta=False)  # initial counts into an empty model
             if self.fused:
                 self.slots = self.ps.row_slots()
                 self.pull_buf = None
@@ -588,6 +597,12 @@ class LDAPushPullMapper(LDACollectiveMapper):
     def _glob_rows(self) -> torch.Tensor:
         return self.glob.buffer.view(-1, self.Kp)
 
+    def _sync_glob(self) -> None:
+        """Dense owner table from the owner slots (owner-slot mode keeps it stale while sampling)."""
+        if self.ps is not None and self.ps.owner_slots and getattr(self, "_glob_stale", False):
+            self.ps.owner_to_dense(self._glob_rows())
+            self._glob_stale = False
+
     @property
     def comm_mode(self) -> str:
         return "local" if self.local_server else ("sparse" if self.ps is not None else "dense")
@@ -627,6 +642,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
                                  deterministic=cfg.deterministic, doc_index=self.doc_index)
                  if n else torch.zeros(self.Kp, dtype=torch.int32, device=self.device))
             self._timed_ps("push", lambda: self.ps.push_payload(self._glob_rows()), push_b)
+            self._glob_stale = True
             if self.get_num_workers() > 1:
                 with self.metrics.time_collective("allreduce", "lda", "topic-delta", self.Kp * 8, self.device):
                     d = reduce_partials(self.comm, {"d": d}, dtype=torch.float64)["d"].round().to(torch.int32)
@@ -673,6 +689,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         """Exact invariant (test / debug; dense [vocab, K_pad] scratch): the word-topic
         counts rebuilt from every worker's (word, z) equal the server table at each owner,
         and the topic sums equal their column sums. Collective; same answer on all ranks."""
+        self._sync_glob()
         Kp, B, P = self.Kp, self.B, self.get_num_workers()
         nblocks = math.ceil(self.vocab / B)
         flat = self.token_words() * Kp + self.tz.long()
@@ -691,6 +708,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         cfg = self.cfg
         K = cfg.num_topics
         wp = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self._sync_glob()
         for p in self.glob.get_partitions():  # each block counted once, at its owner
             wp += L.loglik_terms(RC.widen(p.get()), cfg.beta, K)
         dp = self._doc_loglik()
@@ -723,6 +741,7 @@ class LDAPushPullMapper(LDACollectiveMapper):
         tabs = {"tz": blob_table(self.tz), "nk": blob_table(self.nk)}
         if self.ndk is not None:
             tabs["ndk"] = blob_table(self.ndk)
+        self._sync_glob()
         ids = self.glob.sorted_ids()
         if ids:
             tabs["glob"] = tensor_table(torch.stack([RC.widen(self.glob[b]) for b in ids]), ids)
@@ -738,12 +757,16 @@ class LDAPushPullMapper(LDACollectiveMapper):
             g = tabs["glob"]
             for j, b in enumerate(g.ids):
                 self.glob[b].copy_(g.buffer[j].to(self.device))  # (into a narrow table: uint16 bit patterns)
+            if self.ps is not None and self.ps.owner_slots:
+                self.ps.owner_from_dense(self._glob_rows())
+                self._glob_stale = False
         return it
 
     def print_word_model(self, folder: str, next_it: int = 0) -> str:
         """Word rows of the global-table blocks this rank owns (``wordID topic:count ...``)."""
         from ..utils.model_io import write_topic_counts
 
+        self._sync_glob()
         ids, rows = [], []
         for b in self.glob.sorted_ids():
             lo = b * self.B

@@ -33,6 +33,12 @@ _lib.register({
                                    _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
     "harp_rowcodec_copy_slots": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                                  _lib.c_int, _lib.c_int, _lib.c_void_p],
+    "harp_rowcodec_merge": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                            _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                            _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
+                            _lib.c_void_p],
+    "harp_rowcodec_merge_bounds": [_lib.c_void_p],
+    "harp_rowcodec_reset": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p],
 })
 
 ALIGN = 16
@@ -105,7 +111,7 @@ def _dense_rows(buf: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, K: int)
         cnt = w32[(ro + 4 + 4 * e) // 4]
         top = w16[(ro + 4 + 4 * rc + 2 * e) // 2].to(torch.int64) & 0xFFFF
         ok = top < K
-        out[rows[ok], top[ok]] = cnt[ok]
+        out.index_put_((rows[ok], top[ok]), cnt[ok], accumulate=True)  # repeated topics add up
     return out
 
 
@@ -231,3 +237,89 @@ def copy_slots(inp: torch.Tensor, src_off: torch.Tensor, out: torch.Tensor, dst_
     for a, d, b in zip(src_off.tolist(), dst_off.tolist(), sz.tolist()):
         out[d:d + b] = inp[a:a + b]
     return out
+
+
+# csrc/rowcodec.hip kTinyBound / kSmallBound / kHashBound: rows with at most this many entries
+# merge in an LDS hash, 4 / 2 / 1 rows per wave; larger rows in a K-wide accumulator
+MERGE_BOUNDS = (64, 256, 512)
+
+
+def merge_classes(c_cap: torch.Tensor, src_ptr: torch.Tensor, src_idx: torch.Tensor, in_cap: torch.Tensor,
+                  K: int) -> Tuple[torch.Tensor, ...]:
+    """(tiny, small, hash, big) row lists (int32) for :func:`merge` from the static slot
+    capacities: a row's entry bound is its canonical capacity plus its delta slots' (K for a
+    dense slot)."""
+    n = c_cap.numel()
+    dsz = torch.where(in_cap < 0, torch.full_like(in_cap, K), in_cap).to(torch.int64)
+    per = dsz[src_idx.long()] if src_idx.numel() else torch.zeros(0, dtype=torch.int64, device=c_cap.device)
+    owner = torch.repeat_interleave(torch.arange(n, device=c_cap.device), (src_ptr[1:] - src_ptr[:-1]).long())
+    bound = torch.where(c_cap < 0, torch.full_like(c_cap, K), c_cap).to(torch.int64)
+    bound = bound.index_add(0, owner, per)
+    cls = torch.full_like(bound, 3)
+    for i, b in reversed(list(enumerate(MERGE_BOUNDS))):
+        cls = torch.where((bound <= b) & (c_cap >= 0), torch.full_like(cls, i), cls)
+    return tuple(torch.nonzero(cls == i).flatten().to(torch.int32).contiguous() for i in range(4))
+
+
+def merge(canon: torch.Tensor, c_off: torch.Tensor, c_cap: torch.Tensor, src_ptr: torch.Tensor,
+          src_idx: torch.Tensor, inp: torch.Tensor, in_off: torch.Tensor, in_cap: torch.Tensor, K: int,
+          overflow: torch.Tensor, classes: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
+    """Owner table held as slots (no dense table): canonical slot u := slot u + the delta
+    slots ``src_idx[src_ptr[u]:src_ptr[u + 1]]`` of ``inp``, written back in place without
+    zero counts (unique topics, in no fixed order; a dense slot stays dense). ``classes``:
+    :func:`merge_classes` (computed here when omitted). ``overflow`` |= 1 when a row exceeds
+    its capacity, |= 2 when a count goes negative."""
+    n = c_cap.numel()
+    if n == 0:
+        return canon
+    if K <= 0 or K % 4 or K > MAX_K:
+        raise ValueError(f"rowcodec merge needs 0 < K <= {MAX_K}, K % 4 == 0 (got {K})")
+    if _lib.use_native(canon):
+        for t in (c_off, c_cap, src_ptr, src_idx, inp, in_off, in_cap, overflow):
+            assert t.device == canon.device and t.is_contiguous()
+        assert c_off.dtype == torch.int64 and in_off.dtype == torch.int64
+        assert c_cap.dtype == torch.int32 and in_cap.dtype == torch.int32
+        assert src_ptr.dtype == torch.int32 and src_idx.dtype == torch.int32 and src_ptr.numel() == n + 1
+        tr, sr, hr, br = classes if classes is not None else merge_classes(c_cap, src_ptr, src_idx, in_cap, K)
+        st = _lib.kernels().harp_rowcodec_merge(canon.data_ptr(), c_off.data_ptr(), c_cap.data_ptr(), tr.data_ptr(),
+                                                tr.numel(), sr.data_ptr(), sr.numel(), hr.data_ptr(), hr.numel(),
+                                                br.data_ptr(), br.numel(), src_ptr.data_ptr(),
+                                                src_idx.data_ptr(), inp.data_ptr(), in_off.data_ptr(),
+                                                in_cap.data_ptr(), K, overflow.data_ptr(),
+                                                _lib.stream_ptr(canon.device))
+        _lib.check(st, "rowcodec_merge")
+        return canon
+    # CPU oracle: dense rows, add, re-encode
+    rows = _dense_rows(canon, c_off.long(), c_cap.long(), K)
+    if src_idx.numel():
+        d = _dense_rows(inp, in_off.long(), in_cap.long(), K)
+        owner = torch.repeat_interleave(torch.arange(n), (src_ptr[1:] - src_ptr[:-1]).long())
+        rows.index_add_(0, owner, d[src_idx.long()])
+    if bool((rows < 0).any()):
+        overflow.view(-1)[0] |= 2
+    flag = torch.zeros_like(overflow)
+    encode(rows, K, torch.arange(n, dtype=torch.int32), c_off, c_cap, canon, flag)
+    overflow |= flag
+    return canon
+
+
+def reset_slots(buf: torch.Tensor, off: torch.Tensor, cap: torch.Tensor, K: int) -> torch.Tensor:
+    """Empty every slot for a kernel to fill (nnz = 0, dense rows zeroed) without clearing
+    the whole payload."""
+    n = cap.numel()
+    if n == 0:
+        return buf
+    if _lib.use_native(buf):
+        for t in (off, cap):
+            assert t.device == buf.device and t.is_contiguous()
+        assert off.dtype == torch.int64 and cap.dtype == torch.int32
+        _lib.check(_lib.kernels().harp_rowcodec_reset(buf.data_ptr(), off.data_ptr(), cap.data_ptr(), n, K,
+                                                      _lib.stream_ptr(buf.device)), "rowcodec_reset")
+        return buf
+    w32 = buf.view(torch.int32)
+    o, c = off.long(), cap.long()
+    w32[o[c >= 0] // 4] = 0
+    d = torch.nonzero(c < 0).flatten()
+    if d.numel():
+        w32[(o[d] // 4)[:, None] + torch.arange(K, device=buf.device)[None, :]] = 0
+    return buf

@@ -132,9 +132,15 @@ class SparseRowPS:
         self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.n_rows = int(ids.numel())
         self._pulled = False
+        self._owner = None  # owner table held as canonical slots (use_owner_slots)
 
     def _encode_pull(self, glob_rows: torch.Tensor) -> None:
         s = self.pull_send
+        if self._owner is not None:  # owner slots: the canonical slots are the rows
+            if not self._owner["alias"]:
+                urows, coff, ucap, cbuf, src_off = self._dedup
+                RC.copy_slots(cbuf, src_off, s.buf, s.off, s.cap, self.K)
+            return
         if self._dedup is None:
             RC.encode(glob_rows, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
             return
@@ -178,7 +184,10 @@ class SparseRowPS:
         else:
             RC.encode(local, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
         self._exchange(s, r)
-        RC.decode(glob_rows, self.K, r.rows, r.off, r.cap, r.buf, add=True)
+        if self._owner is not None:
+            self._merge_pushed()
+        else:
+            RC.decode(glob_rows, self.K, r.rows, r.off, r.cap, r.buf, add=True)
 
     # -- fused rows (the sampler reads pull slots and writes push slots itself) -----------
     def row_slots(self):
@@ -211,17 +220,86 @@ class SparseRowPS:
         return r.buf
 
     def push_payload_buffer(self) -> torch.Tensor:
-        """The push payload, zeroed (empty sparse slots, zero dense slots) for a kernel to fill."""
-        buf = self.push_send.buf
-        buf[:self.push_send.nbytes].zero_()
-        return buf
+        """The push payload with every slot emptied (nnz 0, dense slots zero) for a kernel to fill."""
+        s = self.push_send
+        RC.reset_slots(s.buf, s.off, s.cap, self.K)
+        return s.buf
 
     def push_payload(self, glob_rows: torch.Tensor) -> None:
         """The push of a payload a kernel filled (:meth:`push_payload_buffer`): one
         all-to-all, owners add the slots (repeated topics in a slot add up)."""
         s, r = self.push_send, self.push_recv
         self._exchange(s, r)
-        RC.decode(glob_rows, self.K, r.rows, r.off, r.cap, r.buf, add=True)
+        if self._owner is not None:
+            self._merge_pushed()
+        else:
+            RC.decode(glob_rows, self.K, r.rows, r.off, r.cap, r.buf, add=True)
+
+    # -- owner table held as slots ---------------------------------------------------------
+    def use_owner_slots(self) -> None:
+        """Hold the owner's share of the table as CANONICAL SLOTS instead of dense rows: one
+        slot per owned row that any requester uses (capacity min(K, the word's global tokens),
+        so it always fits), ascending topics without zeros. The pull then needs no encode (one
+        rank: the slots ARE the pull payload; otherwise a slot copy per requester, or none
+        when every row has one requester) and the push is a per-row merge of the canonical
+        slot with the pushed delta slots (``ops.rowcodec.merge``) instead of scattered atomic
+        adds into a dense table. Dense rows for the likelihood / checkpoints come from
+        :meth:`owner_to_dense`. Call before the first push; the slots start empty."""
+        s, r = self.pull_send, self.push_recv
+        if self._dedup is None:  # every owned row has one slot in the pull payload: alias it
+            crow, coff, ccap, cbuf = s.rows, s.off, s.cap, s.buf
+            alias = True
+        else:
+            crow, coff, ccap, cbuf, _ = self._dedup
+            alias = False
+        cbuf.zero_()
+        n = crow.numel()
+        # CSR: received push slots grouped by their canonical row
+        if r.rows.numel() and n:
+            srt, perm = torch.sort(crow.long())
+            pos = torch.searchsorted(srt, r.rows.long())
+            if bool((pos >= n).any()) or not bool(torch.equal(srt[pos.clamp(max=n - 1)], r.rows.long())):
+                raise RuntimeError("sparse push/pull: a pushed row has no canonical slot")
+            ci = perm[pos]
+            order = torch.argsort(ci, stable=True)
+            cnt = torch.bincount(ci, minlength=n)
+        else:
+            order = torch.zeros(0, dtype=torch.int64, device=self.device)
+            cnt = torch.zeros(n, dtype=torch.int64, device=self.device)
+        ptr = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+        ptr[1:] = torch.cumsum(cnt, 0)
+        self._owner = {"rows": crow, "off": coff, "cap": ccap, "buf": cbuf, "alias": alias,
+                       "src_ptr": ptr.to(torch.int32).contiguous(), "src_idx": order.to(torch.int32).contiguous()}
+        self._owner["classes"] = RC.merge_classes(ccap, self._owner["src_ptr"], self._owner["src_idx"], r.cap,
+                                                  self.K)
+
+    @property
+    def owner_slots(self) -> bool:
+        return self._owner is not None
+
+    def _merge_pushed(self) -> None:
+        o, r = self._owner, self.push_recv
+        RC.merge(o["buf"], o["off"], o["cap"], o["src_ptr"], o["src_idx"], r.buf, r.off, r.cap, self.K,
+                 self.overflow, o["classes"])
+
+    def push_initial(self, local: torch.Tensor) -> None:
+        """Initial counts (the rows themselves, not a delta) into the empty owner slots."""
+        s, r = self.push_send, self.push_recv
+        RC.encode(local, self.K, s.rows, s.off, s.cap, s.buf, self.overflow)
+        self._exchange(s, r)
+        self._merge_pushed()
+
+    def owner_to_dense(self, glob_rows: torch.Tensor) -> torch.Tensor:
+        """Dense owner rows from the canonical slots (rows nobody uses are zero)."""
+        o = self._owner
+        glob_rows.zero_()
+        RC.decode(glob_rows, self.K, o["rows"], o["off"], o["cap"], o["buf"], add=True)
+        return glob_rows
+
+    def owner_from_dense(self, glob_rows: torch.Tensor) -> None:
+        """Canonical slots from dense owner rows (checkpoint restore)."""
+        o = self._owner
+        RC.encode(glob_rows, self.K, o["rows"], o["off"], o["cap"], o["buf"], self.overflow)
 
     def check_overflow(self) -> None:
         if int(self.overflow.item()):

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--slices", type=int, default=0, help="rotation: word slices per worker (0: LDAConfig default)")
     ap.add_argument("--local-server", default="on", choices=["on", "off"],
                     help="push_pull at P=1: off runs the pull / push collectives even on one rank")
+    ap.add_argument("--owner-slots", default="on", choices=["on", "off"],
+                    help="push_pull, fused rows: owner table held as canonical slots (merge on push)")
     a = ap.parse_args()
     import torch
 
@@ -43,7 +45,8 @@ def main():
     toks = synthetic_corpus(nd, V, 1000, a.len, seed=3, device=comm.device)
     gen = time.perf_counter() - t0
     cfg = LDAConfig(num_topics=a.topics, alpha=50.0 / a.topics, beta=0.01, iterations=a.warmup + a.iters,
-                    sparse_comm=a.sparse_comm, local_server=a.local_server == "on", fused_rows=a.fused_rows == "on")
+                    sparse_comm=a.sparse_comm, local_server=a.local_server == "on", fused_rows=a.fused_rows == "on",
+                    owner_slots=a.owner_slots == "on")
     if a.max_chunk:
         cfg.max_chunk = a.max_chunk
     if a.slices:

@@ -118,6 +118,94 @@ def test_rowcodec_copy_slots_gpu(cuda):
     assert torch.equal(dec.cpu(), src[req])
 
 
+def _write_slots(buf, off, cap, rows_entries, K):
+    """Slots with arbitrary (topic, value) entries -- repeats allowed, as the fused sampler
+    appends them -- or dense rows (cap < 0)."""
+    w32, w16 = buf.view(torch.int32), buf.view(torch.int16)
+    for o, c, ent in zip(off.tolist(), cap.tolist(), rows_entries):
+        if c < 0:
+            row = torch.zeros(K, dtype=torch.int32)
+            for t, v in ent:
+                row[t] += v
+            w32[o // 4:o // 4 + K] = row
+            continue
+        assert len(ent) <= c
+        w32[o // 4] = len(ent)
+        for e, (t, v) in enumerate(ent):
+            w32[(o + 4 + 4 * e) // 4] = v
+            w16[(o + 4 + 4 * c + 2 * e) // 2] = t
+
+
+@pytest.mark.parametrize("K", [256, 1024, 10000])
+def test_rowcodec_merge_matches_oracle(cuda, K):
+    """Owner-slot merge (csrc/rowcodec.hip rowcodec_merge_kernel): canonical slots plus
+    pushed delta slots with repeated topics (sparse and dense, several per row, none for
+    some rows) equal the CPU oracle, in canonical form (unique topics, no zeros); all four
+    row classes (16 / 32 / 64-lane LDS hashes, dense accumulator) are exercised."""
+    g = torch.Generator().manual_seed(K)
+    n = 700
+    base = torch.zeros((n, K), dtype=torch.int32)
+    tok = torch.randint(1, 400, (n,), generator=g)
+    tok[::3] = torch.randint(1, 12, (tok[::3].numel(),), generator=g)  # tiny rows
+    tok[1::3] = torch.randint(30, 120, (tok[1::3].numel(),), generator=g)  # small rows
+    tok[::97] = 3 * K  # some rows with dense canonical slots
+    for r in range(n):
+        t = torch.randint(0, K, (int(tok[r]),), generator=g)
+        base[r].index_add_(0, t, torch.ones_like(t, dtype=torch.int32))
+    caps = RC.slot_caps(tok, K).to(torch.int32)
+    off, nb = RC.layout(caps.long(), K)
+    canon = torch.zeros(nb, dtype=torch.uint8)
+    ov = torch.zeros(1, dtype=torch.int32)
+    RC.encode(base, K, torch.arange(n, dtype=torch.int32), off, caps, canon, ov)
+    owners, ents, dtok = [], [], []
+    cur = base.clone()
+    for r in range(n):
+        for _ in range(int(torch.randint(0, 3, (1,), generator=g))):
+            moves = int(torch.randint(1, 12, (1,), generator=g))
+            ent = []
+            for _ in range(moves):  # a token leaves a topic it holds and joins another (repeats allowed)
+                src = int(torch.nonzero(cur[r]).flatten()[int(torch.randint(0, int((cur[r] > 0).sum()), (1,), generator=g))])
+                dst = int(torch.randint(0, K, (1,), generator=g))
+                cur[r, src] -= 1
+                cur[r, dst] += 1
+                ent += [(src, -1), (dst, 1)]
+            owners.append(r)
+            ents.append(ent)
+            dtok.append(len(ent) if len(ent) % 3 else 10 * K)  # every third: a dense delta slot
+    dcap = RC.slot_caps(torch.tensor(dtok), K).to(torch.int32)
+    doff, dnb = RC.layout(dcap.long(), K)
+    dbuf = torch.zeros(max(dnb, 16), dtype=torch.uint8)
+    _write_slots(dbuf, doff, dcap, ents, K)
+    cnt = torch.bincount(torch.tensor(owners), minlength=n)
+    ptr = torch.zeros(n + 1, dtype=torch.int32)
+    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    idx = torch.arange(len(owners), dtype=torch.int32)  # owners are ascending already
+    ref = RC.merge(canon.clone(), off, caps, ptr, idx, dbuf, doff, dcap, K, torch.zeros(1, dtype=torch.int32))
+    classes = RC.merge_classes(caps, ptr, idx, dcap, K)
+    assert all(c.numel() > 0 for c in classes), [c.numel() for c in classes]
+    gbuf = canon.to(cuda)
+    gov = torch.zeros(1, dtype=torch.int32, device=cuda)
+    RC.merge(gbuf, off.to(cuda), caps.to(cuda), ptr.to(cuda), idx.to(cuda), dbuf.to(cuda), doff.to(cuda),
+             dcap.to(cuda), K, gov)
+    torch.cuda.synchronize()
+    assert int(gov) == 0
+    got = torch.zeros((n, K), dtype=torch.int32)
+    RC.decode(got, K, torch.arange(n, dtype=torch.int32), off, caps, gbuf.cpu())
+    assert torch.equal(got, cur)
+    w32, w16 = gbuf.cpu().view(torch.int32), gbuf.cpu().view(torch.int16)
+    for r in range(0, n, 7):  # canonical form
+        o, c = int(off[r]), int(caps[r])
+        if c < 0:
+            continue
+        nz = int(w32[o // 4])
+        top = w16[(o + 4 + 4 * c) // 2:(o + 4 + 4 * c) // 2 + nz].to(torch.int64) & 0xFFFF
+        cn = w32[(o + 4) // 4:(o + 4) // 4 + nz]
+        assert nz == int((cur[r] != 0).sum()) and top.unique().numel() == nz and bool((cn != 0).all())
+    refd = torch.zeros_like(got)
+    RC.decode(refd, K, torch.arange(n, dtype=torch.int32), off, caps, ref)
+    assert torch.equal(refd, cur)
+
+
 def test_rowcodec_overflow_flag_gpu(cuda):
     K = 256
     src = torch.ones((10, K), dtype=torch.int32, device=cuda)
@@ -129,13 +217,14 @@ def test_rowcodec_overflow_flag_gpu(cuda):
     assert int(ov.item()) == 1
 
 
-def _lda_pp(cuda, toks, mode, local, seed, det, fused=True):
+def _lda_pp(cuda, toks, mode, local, seed, det, fused=True, owner=True):
     from harp_amd.models.lda import LDAConfig, LDAPushPullMapper
     from harp_amd.parallel.comm import Communicator
     from harp_amd.runtime.mapper import KeyValReader
 
     cfg = LDAConfig(num_topics=64, alpha=0.1, beta=0.01, iterations=12, print_interval=6, block_words=512,
-                    sparse_comm=mode, local_server=local, seed=seed, deterministic=det, fused_rows=fused)
+                    sparse_comm=mode, local_server=local, seed=seed, deterministic=det, fused_rows=fused,
+                    owner_slots=owner)
     m = LDAPushPullMapper(Communicator(device=cuda), cfg, 3000, 4000, toks)
     m.run(KeyValReader([]))
     return m
@@ -157,18 +246,21 @@ def test_lda_push_pull_sparse_rows_gpu(cuda):
 
     toks = synthetic_corpus(3000, 4000, 20, 50, seed=2)
     n = toks[0].numel()
+    cases = (("off", False, True, True), ("on", False, True, True), ("on", False, True, False), ("on", False, False, True),
+             ("off", True, True, True))
     for seed in range(2):
-        for mode, local, fused in (("off", False, True), ("on", False, True), ("on", False, False), ("off", True, True)):
-            m = _lda_pp(cuda, toks, mode, local, seed, det=False, fused=fused)
+        for mode, local, fused, owner in cases:
+            m = _lda_pp(cuda, toks, mode, local, seed, det=False, fused=fused, owner=owner)
             assert m.comm_mode == {("off", False): "dense", ("on", False): "sparse", ("off", True): "local"}[(mode, local)]
             assert m.result["fused_rows"] == (mode == "on" and fused)
+            assert (m.ps is not None and m.ps.owner_slots) == (mode == "on" and fused and owner)
             assert m.check_counts(), (mode, local, seed)
             assert int(m.nk.sum()) == n
             ll = [v for _, v in m.result["loglik"]]
             assert ll[-1] > ll[0]
     ref = None
-    for mode, local, fused in (("off", False, True), ("on", False, True), ("on", False, False), ("off", True, True)):
-        m = _lda_pp(cuda, toks, mode, local, 3, det=True, fused=fused)
+    for mode, local, fused, owner in cases:
+        m = _lda_pp(cuda, toks, mode, local, 3, det=True, fused=fused, owner=owner)
         assert m.check_counts()
         got = (m.tz.cpu(), m.ndk.cpu(), [v for _, v in m.result["loglik"]])
         if ref is None:

@@ -46,7 +46,7 @@ def test_codec_roundtrip_cpu():
     assert int(ov) == 1
 
 
-def _ps_worker(comm):
+def _ps_worker(comm, owner_slots=False):
     from harp_amd.parallel.sparse_ps import SparseRowPS
 
     P, me = comm.world_size, comm.rank
@@ -64,7 +64,11 @@ def _ps_worker(comm):
     for i in range(want.numel()):
         t = torch.randint(0, K, (int(toks[i]),), generator=g)
         local[i].index_add_(0, t, torch.ones_like(t, dtype=torch.int32))
-    ps.push(local, glob, delta=False)
+    if owner_slots:
+        ps.use_owner_slots()
+        ps.push_initial(local)
+    else:
+        ps.push(local, glob, delta=False)
     pulled = torch.zeros_like(local)
     ps.pull(glob, pulled)
     # a "sweep": move some tokens between topics, push the delta
@@ -78,13 +82,18 @@ def _ps_worker(comm):
             cur[i, b] += 1
     ps.push(cur, glob, delta=True)
     ps.check_overflow()
+    if owner_slots:
+        assert not glob.any()  # the owner table lives in the slots until asked for
+        ps.owner_to_dense(glob)
     return {"want": want, "local": local, "pulled": pulled, "delta": cur - pulled, "glob": glob, "owned": owned,
             "bytes": ps.bytes_per_call(), "dedup": ps._dedup is not None}
 
 
+@pytest.mark.parametrize("owner_slots", [False, True])
 @pytest.mark.parametrize("P", [1, 2, 3])
-def test_sparse_ps_push_pull(P):
-    res = launch(_ps_worker, P, timeout=300)
+def test_sparse_ps_push_pull(P, owner_slots):
+    """Owner slots (the table held as canonical slots, pushes merged) give the same rows."""
+    res = launch(_ps_worker, P, args=(owner_slots,), timeout=300)
     V, B = 300, 16
     tot0 = torch.zeros((V, K), dtype=torch.int32)
     dtot = torch.zeros((V, K), dtype=torch.int32)
@@ -127,3 +136,58 @@ def test_lda_sparse_rows_bit_identical_to_dense(P):
         if d["glob"] is not None:
             assert torch.equal(d["glob"], s["glob"])
         assert d["loglik"] == s["loglik"]
+
+
+def test_merge_oracle_cpu():
+    """rowcodec.merge (CPU oracle): canonical slot + several delta slots (repeated topics,
+    sparse and dense) -> ascending topics without zeros; overflow and negative flags."""
+    g = torch.Generator().manual_seed(3)
+    n = 6
+    base = torch.zeros((n, K), dtype=torch.int32)
+    for r in range(n):
+        t = torch.randint(0, K, (5 + 4 * r,), generator=g)
+        base[r].index_add_(0, t, torch.ones_like(t, dtype=torch.int32))
+    caps = RC.slot_caps(base.sum(1) + 8, K).to(torch.int32)
+    off, nb = RC.layout(caps.long(), K)
+    canon = torch.zeros(nb, dtype=torch.uint8)
+    ov = torch.zeros(1, dtype=torch.int32)
+    RC.encode(base, K, torch.arange(n, dtype=torch.int32), off, caps, canon, ov)
+    # deltas: rows 0, 2, 2, 5 (row 2 twice), moves of counts between topics
+    owners = [0, 2, 2, 5]
+    delta = torch.zeros((len(owners), K), dtype=torch.int32)
+    for j, r in enumerate(owners):
+        src = int(torch.nonzero(base[r]).flatten()[j])  # distinct topics for the two row-2 deltas
+        delta[j, src] -= 1
+        delta[j, (src + 7 + j) % K] += 1
+    dcap = RC.slot_caps(torch.full((len(owners),), 4), K).to(torch.int32)
+    doff, dnb = RC.layout(dcap.long(), K)
+    dbuf = torch.zeros(dnb, dtype=torch.uint8)
+    RC.encode(delta, K, torch.arange(len(owners), dtype=torch.int32), doff, dcap, dbuf, ov)
+    ptr = torch.tensor([0, 1, 1, 3, 3, 3, 4], dtype=torch.int32)
+    idx = torch.tensor([0, 1, 2, 3], dtype=torch.int32)
+    RC.merge(canon, off, caps, ptr, idx, dbuf, doff, dcap, K, ov)
+    want = base.clone()
+    want.index_add_(0, torch.tensor(owners), delta)
+    got = torch.zeros_like(want)
+    RC.decode(got, K, torch.arange(n, dtype=torch.int32), off, caps, canon)
+    assert torch.equal(got, want) and int(ov) == 0
+    neg = torch.zeros_like(delta[:1])
+    neg[0, int(torch.nonzero(base[1] == 0)[0])] = -1
+    RC.encode(neg, K, torch.zeros(1, dtype=torch.int32), doff[:1], dcap[:1], dbuf, ov)
+    RC.merge(canon, off, caps, torch.tensor([0, 0, 1, 1, 1, 1, 1], dtype=torch.int32),
+             torch.zeros(1, dtype=torch.int32), dbuf, doff, dcap, K, ov)
+    assert int(ov) & 2
+
+
+def test_reset_slots_cpu():
+    """reset_slots empties every slot (nnz 0, dense rows zero) and leaves entry bytes alone."""
+    caps = torch.tensor([3, -1, 0, 5], dtype=torch.int32)
+    off, nb = RC.layout(caps.long(), K)
+    buf = torch.full((nb,), 7, dtype=torch.uint8)
+    RC.reset_slots(buf, off, caps, K)
+    w32 = buf.view(torch.int32)
+    for o, c in zip(off.tolist(), caps.tolist()):
+        if c < 0:
+            assert not w32[o // 4:o // 4 + K].any()
+        else:
+            assert int(w32[o // 4]) == 0 and (c == 0 or int(buf[o + 4]) == 7)
