@@ -822,6 +822,12 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
                           : wdelta == 2 ? (int*)(smem + (ldelta ? 2 : 1) * Kp) : nullptr;
   __shared__ float s_bs[512];  // per-64-topic block sums of qw (Kp <= 32768)
   __shared__ float s_q;
+  // fused rows into a sparse push slot without an LDS delta row (wdelta == 0): each wave keeps
+  // its moves in a list and writes them as (-1, z), (+1, nz) entries with ONE slot
+  // reservation per kMvList moves (one returning atomic per move had stalled the wave for a
+  // global round trip twice per moved token)
+  constexpr int kMvList = 64;
+  __shared__ unsigned s_mvl[WAVES][kMvList];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
@@ -902,6 +908,29 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       if (__ballot(over) && lane == 0) ps.overflow[0] = 1;
     };
     auto flush_wd = [&]() { flush_row(s_wd, lane, 64); };  // this wave's word-row moves
+    const bool mvlist = fused && qcap >= 0 && wdelta == 0;
+    int nmv = 0;  // moves in this wave's list (wave-uniform)
+    auto flush_mv = [&]() {
+      if (nmv == 0) return;
+      int base = 0;
+      if (lane == 0) base = atomicAdd((int*)qslot, 2 * nmv);
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (lane < nmv) {
+        const unsigned m = s_mvl[wv][lane];
+        int* cnt = (int*)(qslot + 4);
+        unsigned short* top = (unsigned short*)(qslot + 4 + 4 * (long)qcap);
+        const int pos = base + 2 * lane;
+        if (pos + 1 < qcap) {
+          cnt[pos] = -1;
+          top[pos] = (unsigned short)(m & 0xFFFFu);
+          cnt[pos + 1] = 1;
+          top[pos + 1] = (unsigned short)(m >> 16);
+        } else {
+          ps.overflow[0] = 1;
+        }
+      }
+      nmv = 0;
+    };
     int ntok = 0;
     if (!fused) {
       for (int t = threadIdx.x; t < Kp; t += 64 * WAVES) {
@@ -1139,6 +1168,8 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           } else if (wdelta == 2) {
             atomicSub(&s_wd[z], 1);
             atomicAdd(&s_wd[nz], 1);
+          } else if (mvlist) {
+            s_mvl[wv][nmv] = (unsigned)z | ((unsigned)nz << 16);
           } else {
             put_move(z, -1);
             put_move(nz, 1);
@@ -1155,6 +1186,10 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
       // one wave are separate threads to the compiler, so order them explicitly
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (mvlist && nz != z && ++nmv == kMvList) {
+        flush_mv();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next list writes follow the reads
+      }
       if (wdelta == 1 && !fused && ++ntok % WFLUSH == 0) {
         flush_wd();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next adds follow the reset
@@ -1176,6 +1211,10 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       dd1 = dd2;
       zz1 = zz2;
       pp1 = pp2;
+    }
+    if (mvlist) {
+      flush_mv();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
     if (wdelta == 1) {
       flush_wd();

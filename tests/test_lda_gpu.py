@@ -48,6 +48,27 @@ def test_sparse_sampler_keeps_no_dense_doc_table(cuda, strategy):
     assert len(ll) == 1 and ll[0] < 0
 
 
+@pytest.mark.parametrize("owner", [True, False])
+def test_sparse_fused_push_list_counts_exact(cuda, owner):
+    """K > 4096 push-pull with fused rows: the sparse sampler writes its word-row moves into
+    the push slots from per-wave move lists (one slot reservation per 64 moves) and the
+    owner merges / decode-adds them; the exact invariant (server rows == counts rebuilt from
+    the final topics) holds with owner slots on and off."""
+    from harp_amd.models.lda import LDAPushPullMapper
+    from harp_amd.runtime.mapper import KeyValReader
+
+    toks = synthetic_corpus(1500, 3000, 20, 60, seed=12)
+    K = 6000
+    cfg = LDAConfig(num_topics=K, alpha=50.0 / K, beta=0.01, iterations=4, print_interval=2, block_words=512,
+                    sparse_comm="on", local_server=False, owner_slots=owner)
+    m = LDAPushPullMapper(Communicator(device=cuda), cfg, 1500, 3000, toks)
+    m.run(KeyValReader([]))
+    assert m.sparse and m.result["fused_rows"] and m.ps.owner_slots == owner
+    assert m.check_counts()
+    ll = [v for _, v in m.result["loglik"]]
+    assert ll[-1] > ll[0]
+
+
 def test_sparse_sampler_doc_spans_match_doc_ids(cuda, monkeypatch):
     """The span form of the sparse sampler (per-token doc_off | length << 40 instead of doc
     ids -> doc_off) takes the same trajectory as the id form in the one-wave deterministic
