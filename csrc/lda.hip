@@ -822,12 +822,16 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
                           : wdelta == 2 ? (int*)(smem + (ldelta ? 2 : 1) * Kp) : nullptr;
   __shared__ float s_bs[512];  // per-64-topic block sums of qw (Kp <= 32768)
   __shared__ float s_q;
-  // fused rows into a sparse push slot without an LDS delta row (wdelta == 0): each wave keeps
-  // its moves in a list and writes them as (-1, z), (+1, nz) entries with ONE slot
+  // no LDS delta row (wdelta == 0, K > 4096): each wave keeps its moves in a list and writes
+  // them out together -- into a sparse push slot as (-1, z), (+1, nz) entries with ONE slot
   // reservation per kMvList moves (one returning atomic per move had stalled the wave for a
-  // global round trip twice per moved token)
-  constexpr int kMvList = 64;
-  __shared__ unsigned s_mvl[WAVES][kMvList];
+  // global round trip twice per moved token: K = 10,000 push-pull 68.7 -> 55.7 ms), into a
+  // dense slot / the global word row and the topic-sum deltas as 64-lane atomics (every
+  // kMvFlush moves when other workgroups read the global row: at most that many moves late)
+  constexpr int kMvList = 64, kMvFlush = 16;
+  // wdelta == 0: the move lists [WAVES][kMvList] in the dynamic LDS after s_qw
+  unsigned* s_mvl_base = (unsigned*)(smem + Kp);
+  auto s_mvl_at = [&](int w, int i) -> unsigned& { return s_mvl_base[w * kMvList + i]; };
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
@@ -908,25 +912,40 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       if (__ballot(over) && lane == 0) ps.overflow[0] = 1;
     };
     auto flush_wd = [&]() { flush_row(s_wd, lane, 64); };  // this wave's word-row moves
-    const bool mvlist = fused && qcap >= 0 && wdelta == 0;
+    const bool mvlist = wdelta == 0;
+    const int mv_cap = fused ? kMvList : kMvFlush;
     int nmv = 0;  // moves in this wave's list (wave-uniform)
     auto flush_mv = [&]() {
       if (nmv == 0) return;
+      const bool sparse_slot = fused && qcap >= 0;
       int base = 0;
-      if (lane == 0) base = atomicAdd((int*)qslot, 2 * nmv);
-      base = __builtin_amdgcn_readfirstlane(base);
+      if (sparse_slot) {
+        if (lane == 0) base = atomicAdd((int*)qslot, 2 * nmv);
+        base = __builtin_amdgcn_readfirstlane(base);
+      }
       if (lane < nmv) {
-        const unsigned m = s_mvl[wv][lane];
-        int* cnt = (int*)(qslot + 4);
-        unsigned short* top = (unsigned short*)(qslot + 4 + 4 * (long)qcap);
-        const int pos = base + 2 * lane;
-        if (pos + 1 < qcap) {
-          cnt[pos] = -1;
-          top[pos] = (unsigned short)(m & 0xFFFFu);
-          cnt[pos + 1] = 1;
-          top[pos + 1] = (unsigned short)(m >> 16);
+        const unsigned m = s_mvl_at(wv, lane);
+        const int zo = (int)(m & 0xFFFFu), zn = (int)(m >> 16);
+        if (sparse_slot) {
+          int* cnt = (int*)(qslot + 4);
+          unsigned short* top = (unsigned short*)(qslot + 4 + 4 * (long)qcap);
+          const int pos = base + 2 * lane;
+          if (pos + 1 < qcap) {
+            cnt[pos] = -1;
+            top[pos] = (unsigned short)zo;
+            cnt[pos + 1] = 1;
+            top[pos + 1] = (unsigned short)zn;
+          } else {
+            ps.overflow[0] = 1;
+          }
         } else {
-          ps.overflow[0] = 1;
+          int* row = fused ? (int*)qslot : wrow;
+          atomicSub(row + zo, 1);
+          atomicAdd(row + zn, 1);
+        }
+        if (!ldelta) {
+          atomicSub(nk_delta + zo, 1);
+          atomicAdd(nk_delta + zn, 1);
         }
       }
       nmv = 0;
@@ -1169,7 +1188,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
             atomicSub(&s_wd[z], 1);
             atomicAdd(&s_wd[nz], 1);
           } else if (mvlist) {
-            s_mvl[wv][nmv] = (unsigned)z | ((unsigned)nz << 16);
+            s_mvl_at(wv, nmv) = (unsigned)z | ((unsigned)nz << 16);
           } else {
             put_move(z, -1);
             put_move(nz, 1);
@@ -1177,7 +1196,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
           if (ldelta) {
             atomicSub(&s_nkd[z], 1);
             atomicAdd(&s_nkd[nz], 1);
-          } else {  // K > 4096: the moves spread over enough topics (per-XCD copies measured no gain)
+          } else if (!mvlist) {  // (with the move list: flushed with it)
             atomicSub(nk_delta + z, 1);
             atomicAdd(nk_delta + nz, 1);
           }
@@ -1186,7 +1205,7 @@ __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
       // the next token's LDS reads (all lanes) must follow lane 0's row update: lanes of
       // one wave are separate threads to the compiler, so order them explicitly
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (mvlist && nz != z && ++nmv == kMvList) {
+      if (mvlist && nz != z && ++nmv == mv_cap) {
         flush_mv();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // lane 0's next list writes follow the reads
       }
@@ -1355,7 +1374,9 @@ constexpr int kSparseMaxK = 32768;
 int sparse_wdelta(int Kp) { return Kp <= 1024 ? 1 : Kp <= 4096 ? 2 : 0; }
 size_t sparse_lds_bytes(int Kp, int waves) {
   const int wd = sparse_wdelta(Kp);
-  return (Kp <= 4096 ? 8 : 4) * (size_t)Kp + (wd == 1 ? 4 * (size_t)Kp * waves : wd == 2 ? 4 * (size_t)Kp : 0);
+  // wd == 0: s_qw and the move lists (64 per wave)
+  return (Kp <= 4096 ? 8 : 4) * (size_t)Kp +
+         (wd == 1 ? 4 * (size_t)Kp * waves : wd == 2 ? 4 * (size_t)Kp : 4 * 64 * (size_t)waves);
 }
 
 template <int WAVES, class DT, bool SPAN = false>

@@ -48,6 +48,40 @@ def test_sparse_sampler_keeps_no_dense_doc_table(cuda, strategy):
     assert len(ll) == 1 and ll[0] < 0
 
 
+def test_sparse_move_list_flush_exact(cuda):
+    """K > 4096 (no LDS delta row): the sparse sampler's per-wave move lists flush word-row
+    moves into the global table and the topic-sum deltas as 64-lane atomics; after two
+    sweeps the table, the topic sums and the doc lists equal a recount."""
+    from harp_amd.ops import lda as L
+
+    K = 6000
+    g = torch.Generator(device=cuda).manual_seed(5)
+    nd, V, n = 2000, 400, 150000
+    tdoc = torch.randint(0, nd, (n,), generator=g, device=cuda, dtype=torch.int32)
+    tword = torch.randint(0, V, (n,), generator=g, device=cuda, dtype=torch.int32)
+    order = torch.argsort(tword.long() * nd + tdoc.long())
+    tdoc, tword = tdoc[order].contiguous(), tword[order].contiguous()
+    tz = torch.randint(0, K, (n,), generator=g, device=cuda, dtype=torch.int32)
+    Kp = L.padded_topics(K)
+    nwk = torch.zeros((V, Kp), dtype=torch.int32, device=cuda)
+    nk = torch.zeros(Kp, dtype=torch.int32, device=cuda)
+    L.count(None, tword, tz, None, nwk, nk)
+    di = L.DocIndex.build(tdoc, tz, nd)
+    chunks = L.build_chunks(tword, 4096)
+    before = tz.clone()
+    for sweep in range(2):
+        d = L.cgs_sample(tdoc, tword, tz, chunks, None, nwk, nk, K, 50.0 / K, 0.01, V * 0.01, 21 + sweep, di)
+        nk += d
+    torch.cuda.synchronize()
+    assert int((tz != before).sum()) > n // 4
+    r_nwk = torch.zeros_like(nwk)
+    r_nk = torch.zeros_like(nk)
+    L.count(None, tword, tz, None, r_nwk, r_nk)
+    assert torch.equal(r_nwk, nwk)
+    assert torch.equal(r_nk, nk)
+    assert torch.equal(di.zdoc[di.tpos].int() & 0xFFFF, tz)
+
+
 @pytest.mark.parametrize("owner", [True, False])
 def test_sparse_fused_push_list_counts_exact(cuda, owner):
     """K > 4096 push-pull with fused rows: the sparse sampler writes its word-row moves into
