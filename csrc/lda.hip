@@ -793,6 +793,9 @@ __global__ void lda_count_kernel(const int* __restrict__ tdoc, const int* __rest
 // SPAN: tspan[i] = doc_off[doc of token i] | (doc length << 40), precomputed per token, so the
 // next token's doc range needs no dependent doc_off load (no doc-topic table, no doc ids)
 template <int WAVES, class DT, bool SPAN = false>
+// (16-wave workgroups forced to 64 VGPRs for eight waves per SIMD measured slower at K = 10,000:
+// 57.2 vs 54.6 ms rotation, with a worse likelihood from more concurrent chunk tokens;
+// profiles/r6_sparse/waves_*.log)
 __global__ __launch_bounds__(64 * WAVES) void lda_cgs_sparse_kernel(
     const int* __restrict__ tdoc, const long* __restrict__ tspan, const int* __restrict__ tword, int* __restrict__ tz,
     const long* __restrict__ chunk_start, long nchunks, const int* __restrict__ order, int* __restrict__ work,
