@@ -403,11 +403,22 @@ __device__ __forceinline__ void hash_add(int* hk, int* hv, int slots, int t, int
 // G lanes per row (256 / G rows per workgroup), an S-entry LDS hash per row (S >= 2 x the
 // class bound); the G-lane groups of one wave run different rows, so the wave overlaps
 // their dependent slot loads
+// Per-row merge metadata, built once on the host from the static layouts (32 B per row):
+// canonical slot offset, first delta slot offset, capacities, and the row's range of delta
+// slots (the first one is inlined; more, at P > 1, come from qoff / qcap in CSR order). A row's
+// loads are then independent of each other, so the next row's are issued under this one.
+struct MergeMeta {
+  long off, doff;
+  int cap, dcap, q0, q1;
+};
+
+// G lanes per row (256 / G rows per workgroup), an S-entry LDS hash per row (S >= 2 x the
+// class bound); the G-lane groups of one wave run different rows, so the wave overlaps
+// their slot loads, and each group loads the next row's metadata under the current row
 template <int G, int S>
 __global__ __launch_bounds__(256) void rowcodec_merge_group_kernel(
-    unsigned char* __restrict__ canon, const long* __restrict__ c_off, const int* __restrict__ c_cap,
-    const int* __restrict__ rows, int nrows, const int* __restrict__ src_ptr, const int* __restrict__ src_idx,
-    const unsigned char* __restrict__ in, const long* __restrict__ in_off, const int* __restrict__ in_cap, int K,
+    unsigned char* __restrict__ canon, const MergeMeta* __restrict__ meta, int nrows,
+    const long* __restrict__ qoff, const int* __restrict__ qcap, const unsigned char* __restrict__ in, int K,
     int* __restrict__ overflow) {
   constexpr int R = 256 / G;
   __shared__ int keys[R][S];
@@ -421,14 +432,44 @@ __global__ __launch_bounds__(256) void rowcodec_merge_group_kernel(
   }
   bool over = false, neg = false;
   const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1ull);
-  for (int j = blockIdx.x * R + grp; j < nrows; j += gridDim.x * R) {
-    const int u = rows[j];
-    unsigned char* slot = canon + c_off[u];
-    const int c = c_cap[u];  // >= 0: these classes are sparse rows
-    merge_entries(slot, c, src_ptr[u], src_ptr[u + 1], src_idx, in, in_off, in_cap, K, gl,
-                  [&](int t, int v) { hash_add(hk, hv, S, t, v, over); }, G);
+  auto add = [&](int t, int v) { hash_add(hk, hv, S, t, v, over); };
+  // one delta slot's entries (sparse or dense)
+  auto delta = [&](const unsigned char* ds, int dc) {
+    if (dc < 0) {
+      for (int t = gl; t < K; t += G) {
+        const int v = ((const int*)ds)[t];
+        if (v) add(t, v);
+      }
+    } else {
+      int nz = *(const int*)ds;
+      nz = nz < 0 ? 0 : (nz > dc ? dc : nz);
+      const int* dcn = slot_counts(ds);
+      const unsigned short* dtp = slot_topics(ds, dc);
+      for (int e = gl; e < nz; e += G) {
+        const int t = dtp[e], v = dcn[e];
+        if (v && t < K) add(t, v);
+      }
+    }
+  };
+  const int stride = gridDim.x * R;
+  int j = blockIdx.x * R + grp;
+  MergeMeta m{0, 0, 0, 0, 0, 0};
+  if (j < nrows) m = meta[j];
+  for (; j < nrows; j += stride) {
+    MergeMeta mn{0, 0, 0, 0, 0, 0};
+    if (j + stride < nrows) mn = meta[j + stride];  // in flight during this row
+    unsigned char* slot = canon + m.off;
+    const int c = m.cap;  // >= 0: these classes are sparse rows
+    int nnz = *(const int*)slot;
+    nnz = nnz < 0 ? 0 : (nnz > c ? c : nnz);
     int* ocn = (int*)(slot + 4);
     unsigned short* otp = (unsigned short*)(slot + 4 + 4 * (long)c);
+    for (int e = gl; e < nnz; e += G) {
+      const int t = otp[e];
+      if (t < K) add(t, ocn[e]);
+    }
+    if (m.q1 > m.q0) delta(in + m.doff, m.dcap);
+    for (int q = m.q0 + 1; q < m.q1; ++q) delta(in + qoff[q], qcap[q]);
     const unsigned long long below = (1ull << gl) - 1ull;
     int base = 0;
     for (int i0 = 0; i0 < S; i0 += G) {
@@ -436,9 +477,9 @@ __global__ __launch_bounds__(256) void rowcodec_merge_group_kernel(
       const int t = hk[i], v = hv[i];
       const bool keep = t >= 0 && v != 0;
       neg |= v < 0;
-      const unsigned long long m = (__ballot(keep) >> gshift) & gmask;  // this row's G lanes
+      const unsigned long long mk = (__ballot(keep) >> gshift) & gmask;  // this row's G lanes
       if (keep) {
-        const int pos = base + __popcll(m & below);
+        const int pos = base + __popcll(mk & below);
         if (pos < c) {
           ocn[pos] = v;
           otp[pos] = (unsigned short)t;
@@ -446,11 +487,12 @@ __global__ __launch_bounds__(256) void rowcodec_merge_group_kernel(
           over = true;
         }
       }
-      base += __popcll(m);
+      base += __popcll(mk);
       hk[i] = -1;
       hv[i] = 0;
     }
     if (gl == 0) *(int*)slot = base < c ? base : c;
+    m = mn;
   }
   if (over) atomicOr(overflow, 1);
   if (neg) atomicOr(overflow, 2);
@@ -619,23 +661,28 @@ HARP_EXPORT int harp_rowcodec_merge_bounds(int* out3) {
   return HARP_OK;
 }
 
-HARP_EXPORT int harp_rowcodec_merge(void* canon, const long* c_off, const int* c_cap, const int* tiny_rows,
-                                    int n_tiny, const int* small_rows, int n_small, const int* hash_rows, int n_hash,
-                                    const int* big_rows, int n_big, const int* src_ptr, const int* src_idx,
-                                    const void* in, const long* in_off, const int* in_cap, int K, int* overflow,
-                                    hipStream_t s) {
+HARP_EXPORT int harp_rowcodec_merge_meta_bytes() { return (int)sizeof(MergeMeta); }
+
+// meta_tiny / meta_small / meta_hash: MergeMeta rows of each lane-group class (qoff / qcap:
+// every delta slot's offset / capacity in CSR order, for rows with more than one); big_rows:
+// the rest, by the dense-accumulator kernel (c_off, c_cap, src_ptr, src_idx, in_off, in_cap)
+HARP_EXPORT int harp_rowcodec_merge(void* canon, const void* in, const void* meta_tiny, int n_tiny,
+                                    const void* meta_small, int n_small, const void* meta_hash, int n_hash,
+                                    const long* qoff, const int* qcap, const int* big_rows, int n_big,
+                                    const long* c_off, const int* c_cap, const int* src_ptr, const int* src_idx,
+                                    const long* in_off, const int* in_cap, int K, int* overflow, hipStream_t s) {
   if (n_tiny < 0 || n_small < 0 || n_hash < 0 || n_big < 0 || K <= 0 || (K & 3) || K > 16384 ||
       misaligned(canon) || misaligned(in) || !overflow)
     return HARP_EBADARG;
-  auto group = [&](auto kern, const int* rows, int nr, int per_wg) {
+  auto group = [&](auto kern, const void* meta, int nr, int per_wg) {
     int grid = (nr + per_wg - 1) / per_wg;
     if (grid > 16384) grid = 16384;
-    kern<<<dim3((unsigned)grid), dim3(256), 0, s>>>((unsigned char*)canon, c_off, c_cap, rows, nr, src_ptr, src_idx,
-                                                   (const unsigned char*)in, in_off, in_cap, K, overflow);
+    kern<<<dim3((unsigned)grid), dim3(256), 0, s>>>((unsigned char*)canon, (const MergeMeta*)meta, nr, qoff, qcap,
+                                                   (const unsigned char*)in, K, overflow);
   };
-  if (n_tiny > 0) group(rowcodec_merge_group_kernel<16, 128>, tiny_rows, n_tiny, 16);
-  if (n_small > 0) group(rowcodec_merge_group_kernel<32, 512>, small_rows, n_small, 8);
-  if (n_hash > 0) group(rowcodec_merge_group_kernel<64, 1024>, hash_rows, n_hash, 4);
+  if (n_tiny > 0) group(rowcodec_merge_group_kernel<16, 128>, meta_tiny, n_tiny, 16);
+  if (n_small > 0) group(rowcodec_merge_group_kernel<32, 512>, meta_small, n_small, 8);
+  if (n_hash > 0) group(rowcodec_merge_group_kernel<64, 1024>, meta_hash, n_hash, 4);
   if (n_big > 0) {
     const int per_wave = (K + (K + 31) / 32 + 3) & ~3;  // ints: accumulator + bitmap
     int wv = kLdsBudget / (4 * per_wave);

@@ -33,10 +33,11 @@ _lib.register({
                                    _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
     "harp_rowcodec_copy_slots": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                                  _lib.c_int, _lib.c_int, _lib.c_void_p],
-    "harp_rowcodec_merge": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
-                            _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
-                            _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p,
-                            _lib.c_void_p],
+    "harp_rowcodec_merge": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_int,
+                            _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int,
+                            _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                            _lib.c_int, _lib.c_void_p, _lib.c_void_p],
+    "harp_rowcodec_merge_meta_bytes": [],
     "harp_rowcodec_merge_bounds": [_lib.c_void_p],
     "harp_rowcodec_reset": [_lib.c_void_p, _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_int, _lib.c_void_p],
 })
@@ -261,13 +262,46 @@ def merge_classes(c_cap: torch.Tensor, src_ptr: torch.Tensor, src_idx: torch.Ten
     return tuple(torch.nonzero(cls == i).flatten().to(torch.int32).contiguous() for i in range(4))
 
 
+def merge_plan(c_off: torch.Tensor, c_cap: torch.Tensor, src_ptr: torch.Tensor, src_idx: torch.Tensor,
+               in_off: torch.Tensor, in_cap: torch.Tensor, K: int) -> dict:
+    """The static part of :func:`merge` (layouts never change while sampling): the row classes
+    and, for the lane-group classes, one 32-byte metadata row per canonical row (csrc/rowcodec.hip
+    ``MergeMeta``: slot offsets, capacities, the first delta slot inlined, the delta range), so
+    the kernels issue a row's loads together and the next row's under the current one."""
+    tiny, small, hsh, big = merge_classes(c_cap, src_ptr, src_idx, in_cap, K)
+    dev = c_cap.device
+    q0, q1 = src_ptr[:-1].long(), src_ptr[1:].long()
+    has = q1 > q0
+    if src_idx.numel():
+        first = src_idx.long()[q0.clamp(max=src_idx.numel() - 1)]
+        doff = torch.where(has, in_off.long()[first], torch.zeros_like(q0))
+        dcap = torch.where(has, in_cap.long()[first], torch.zeros_like(q0))
+    else:
+        doff = dcap = torch.zeros_like(q0)
+
+    def meta(rows: torch.Tensor) -> torch.Tensor:
+        r = rows.long()
+        m = torch.empty((r.numel(), 4), dtype=torch.int64, device=dev)
+        m[:, 0] = c_off.long()[r]
+        m[:, 1] = doff[r]
+        m[:, 2] = (c_cap.long()[r] & 0xFFFFFFFF) | (dcap[r] << 32)
+        m[:, 3] = (q0[r] & 0xFFFFFFFF) | (q1[r] << 32)
+        return m.contiguous()
+
+    si = src_idx.long()
+    return {"meta": [meta(tiny), meta(small), meta(hsh)], "big": big,
+            "qoff": in_off.long()[si].contiguous() if si.numel() else torch.zeros(1, dtype=torch.int64, device=dev),
+            "qcap": in_cap[si].to(torch.int32).contiguous() if si.numel() else torch.zeros(1, dtype=torch.int32,
+                                                                                          device=dev)}
+
+
 def merge(canon: torch.Tensor, c_off: torch.Tensor, c_cap: torch.Tensor, src_ptr: torch.Tensor,
           src_idx: torch.Tensor, inp: torch.Tensor, in_off: torch.Tensor, in_cap: torch.Tensor, K: int,
-          overflow: torch.Tensor, classes: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
+          overflow: torch.Tensor, plan: Optional[dict] = None) -> torch.Tensor:
     """Owner table held as slots (no dense table): canonical slot u := slot u + the delta
     slots ``src_idx[src_ptr[u]:src_ptr[u + 1]]`` of ``inp``, written back in place without
-    zero counts (unique topics, in no fixed order; a dense slot stays dense). ``classes``:
-    :func:`merge_classes` (computed here when omitted). ``overflow`` |= 1 when a row exceeds
+    zero counts (unique topics, in no fixed order; a dense slot stays dense). ``plan``:
+    :func:`merge_plan` (built here when omitted). ``overflow`` |= 1 when a row exceeds
     its capacity, |= 2 when a count goes negative."""
     n = c_cap.numel()
     if n == 0:
@@ -280,13 +314,15 @@ def merge(canon: torch.Tensor, c_off: torch.Tensor, c_cap: torch.Tensor, src_ptr
         assert c_off.dtype == torch.int64 and in_off.dtype == torch.int64
         assert c_cap.dtype == torch.int32 and in_cap.dtype == torch.int32
         assert src_ptr.dtype == torch.int32 and src_idx.dtype == torch.int32 and src_ptr.numel() == n + 1
-        tr, sr, hr, br = classes if classes is not None else merge_classes(c_cap, src_ptr, src_idx, in_cap, K)
-        st = _lib.kernels().harp_rowcodec_merge(canon.data_ptr(), c_off.data_ptr(), c_cap.data_ptr(), tr.data_ptr(),
-                                                tr.numel(), sr.data_ptr(), sr.numel(), hr.data_ptr(), hr.numel(),
-                                                br.data_ptr(), br.numel(), src_ptr.data_ptr(),
-                                                src_idx.data_ptr(), inp.data_ptr(), in_off.data_ptr(),
-                                                in_cap.data_ptr(), K, overflow.data_ptr(),
-                                                _lib.stream_ptr(canon.device))
+        if plan is None:
+            plan = merge_plan(c_off, c_cap, src_ptr, src_idx, in_off, in_cap, K)
+        (mt, ms, mh), br = plan["meta"], plan["big"]
+        st = _lib.kernels().harp_rowcodec_merge(canon.data_ptr(), inp.data_ptr(), mt.data_ptr(), mt.shape[0],
+                                                ms.data_ptr(), ms.shape[0], mh.data_ptr(), mh.shape[0],
+                                                plan["qoff"].data_ptr(), plan["qcap"].data_ptr(), br.data_ptr(),
+                                                br.numel(), c_off.data_ptr(), c_cap.data_ptr(), src_ptr.data_ptr(),
+                                                src_idx.data_ptr(), in_off.data_ptr(), in_cap.data_ptr(), K,
+                                                overflow.data_ptr(), _lib.stream_ptr(canon.device))
         _lib.check(st, "rowcodec_merge")
         return canon
     # CPU oracle: dense rows, add, re-encode

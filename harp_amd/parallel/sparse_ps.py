@@ -270,8 +270,8 @@ class SparseRowPS:
         ptr[1:] = torch.cumsum(cnt, 0)
         self._owner = {"rows": crow, "off": coff, "cap": ccap, "buf": cbuf, "alias": alias,
                        "src_ptr": ptr.to(torch.int32).contiguous(), "src_idx": order.to(torch.int32).contiguous()}
-        self._owner["classes"] = RC.merge_classes(ccap, self._owner["src_ptr"], self._owner["src_idx"], r.cap,
-                                                  self.K)
+        self._owner["plan"] = RC.merge_plan(coff, ccap, self._owner["src_ptr"], self._owner["src_idx"], r.off,
+                                            r.cap, self.K)
 
     @property
     def owner_slots(self) -> bool:
@@ -280,7 +280,7 @@ class SparseRowPS:
     def _merge_pushed(self) -> None:
         o, r = self._owner, self.push_recv
         RC.merge(o["buf"], o["off"], o["cap"], o["src_ptr"], o["src_idx"], r.buf, r.off, r.cap, self.K,
-                 self.overflow, o["classes"])
+                 self.overflow, o["plan"])
 
     def push_initial(self, local: torch.Tensor) -> None:
         """Initial counts (the rows themselves, not a delta) into the empty owner slots."""

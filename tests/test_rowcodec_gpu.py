@@ -183,6 +183,7 @@ def test_rowcodec_merge_matches_oracle(cuda, K):
     ref = RC.merge(canon.clone(), off, caps, ptr, idx, dbuf, doff, dcap, K, torch.zeros(1, dtype=torch.int32))
     classes = RC.merge_classes(caps, ptr, idx, dcap, K)
     assert all(c.numel() > 0 for c in classes), [c.numel() for c in classes]
+    assert int(RC._lib.kernels().harp_rowcodec_merge_meta_bytes()) == 32  # MergeMeta == merge_plan's rows
     gbuf = canon.to(cuda)
     gov = torch.zeros(1, dtype=torch.int32, device=cuda)
     RC.merge(gbuf, off.to(cuda), caps.to(cuda), ptr.to(cuda), idx.to(cuda), dbuf.to(cuda), doff.to(cuda),
