@@ -7,7 +7,7 @@
 export TMPDIR=/tmp
 O=${1:-gpurun_out/r6_rehearsal}
 mkdir -p $O
-for P in 2 3; do
+for P in ${PS:-2 3}; do
   HARP_BENCH_TRACE=1 timeout -k 10 500 python bench.py --gpus $P --backend gloo --steps 3 --warmup 1 --points 2e7 --sgd on --sgd-epochs 3 --extras on --pca-n 1e7 --pca-steps 3 --lda-docs 2e5 --lda-vocab 2e5 --lda-iters 3 --sgd-timeout 300 --extras-timeout 200 > $O/bench_p$P.log 2>&1
   rc=$?; echo "bench P=$P rc=$rc"
   grep '^{' $O/bench_p$P.log | tail -1 | python3 -c '
