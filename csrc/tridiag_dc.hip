@@ -22,8 +22,11 @@
 //  5. dc_gemm_kernel: Q_new[block] = Q[block rows, kept columns] x U (64 x 64 tiles over
 //     LDS, fp64 MFMA, each half's rows over that half's columns only), deflated columns
 //     copied; Q ping-pongs between two buffers.
+//  6. dc_wave_merge_kernel: levels of merges <= 64 rows, steps 1-5 in one wave per merge.
 // Eigenvalues are carried as (origin pole, tau) while the vectors are formed, so every
 // difference d_j - lambda_i is computed as (d_j - d_o) - tau without cancellation.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -64,6 +67,11 @@ __device__ __forceinline__ double block_max_1k(double v, double* red) {
 
 // workgroup barrier for LDS traffic only (__syncthreads() also drains outstanding global loads)
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// LDS ordering within one wave (its lanes run in lockstep: no barrier)
+__device__ __forceinline__ void lds_sync_wave() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // merge holding position c (merges sorted by lo, nm of them)
 __device__ __forceinline__ int find_merge(const int* __restrict__ mg, int nm, int c) {
@@ -82,6 +90,14 @@ __device__ long long g_prep_t[10];
 #define PREP_MARK(i) \
   do {                                                                                   \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_prep_t[i] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+// phase stamps of block 0 of the last dc_wave_merge_kernel launch (harp_dc_wave_stamps)
+__device__ long long g_wave_t[8];
+__device__ int g_wave_it;
+#define WAVE_MARK(i) \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_wave_t[i] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
 struct DcWs {
@@ -651,6 +667,7 @@ __global__ __launch_bounds__(256) void dc_vectors_kernel(const int* __restrict__
 constexpr int TM = 64, TK = 64, kFetch = TK * TM / 256, kPA = TM + 16, kPB = TK + 4;
 constexpr size_t kGemmTileLds = sizeof(double) * (size_t)(TK * kPA + TM * kPB);
 typedef double dc_d4 __attribute__((ext_vector_type(4)));
+typedef double dc_d2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void dc_gemm_kernel(const double* __restrict__ Q, double* __restrict__ Qn, long ldq,
                                                       const int* __restrict__ mg, DcWs w, int rtm) {
   extern __shared__ double gsm[];
@@ -759,11 +776,451 @@ __global__ __launch_bounds__(256) void dc_copyback_kernel(const double* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 6. Levels whose merges have at most kWaveMerge rows: ONE wave per merge does all of steps
+// 1-5 in a single launch (lane = row / sorted position): the merge's block of Q staged in LDS,
+// register bitonic sort over the wave, deflation by ballots (+ the one-lane walk when a
+// rotation applies), one LANE per secular root (sequential sums over k <= 64), Loewner z-hat,
+// U in LDS, and the block product written straight back to Q (no Qb round trip). The six
+// launches of the level kernels cost ~50 us per level at these sizes (dc_kernels_after.txt)
+// for work of a few microseconds.
+constexpr int kWaveMerge = 64, kWaveMergeDefault = 64;
+
+
+__device__ __forceinline__ double quad_sum_d(double v) {
+  v += dpp_mov_d<0xB1>(v);  // quad_perm [1,0,3,2]
+  return v + dpp_mov_d<0x4E>(v);  // quad_perm [2,3,0,1]: the same bits in all four lanes
+}
+__device__ __forceinline__ double quad_prod_d(double v) {
+  v *= dpp_mov_d<0xB1>(v);
+  return v * dpp_mov_d<0x4E>(v);
+}
+
+// Root i of the secular equation by the four lanes of a quad (part = lane & 3 holds the terms
+// j = part + 4 q, q < NT, in registers); the quad's sums are bit-identical in its lanes, so
+// its control flow is uniform. Same iteration as secular_solve.
+template <int NT>
+__device__ int secular_quad(int i, int part, int k, double rho, const double* dd, const double* zz, int& o_out,
+                            double& tau_out) {
+  const double irho = 1.0 / rho;
+  double dr[NT], z2r[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const int j = part + 4 * q;
+    dr[q] = j < k ? dd[j] : 1e300;  // absent terms: z^2 = 0 over a finite pole, an exact 0
+    z2r[q] = j < k ? zz[j] * zz[j] : 0.0;
+  }
+  int o;
+  double lo_t, hi_t;
+  const double ddi = dd[i];
+  if (i < k - 1) {
+    const double mid = 0.5 * (dd[i + 1] - ddi);
+    double f = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) f += z2r[q] / ((dr[q] - ddi) - mid);
+    f = quad_sum_d(f) + irho;
+    if (f >= 0.0) {
+      o = i;
+      lo_t = 0.0;
+      hi_t = mid;
+    } else {
+      o = i + 1;
+      lo_t = -mid;
+      hi_t = 0.0;
+    }
+  } else {
+    double z2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) z2 += z2r[q];
+    o = i;
+    lo_t = 0.0;
+    hi_t = rho * quad_sum_d(z2);
+  }
+  const double dor = dd[o];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) dr[q] -= dor;
+  const double D1o = ddi - dor, D2o = i < k - 1 ? dd[i + 1] - dor : 0.0;
+  double tau = 0.5 * (lo_t + hi_t);
+  int it = 0;
+  for (; it < 64; ++it) {
+    double psi = 0.0, phi = 0.0, dpsi = 0.0, dphi = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {  // branch-free: the split j <= i as selects
+      const bool left = part + 4 * q <= i;
+      const double r = rcp_nr(dr[q] - tau);
+      const double t = z2r[q] * r;
+      const double tl = left ? t : 0.0, tg = left ? 0.0 : t;
+      psi += tl;
+      dpsi = fma(tl, r, dpsi);
+      phi += tg;
+      dphi = fma(tg, r, dphi);
+    }
+    psi = quad_sum_d(psi);
+    phi = quad_sum_d(phi);
+    dpsi = quad_sum_d(dpsi);
+    dphi = quad_sum_d(dphi);
+    const double f = irho + psi + phi;
+    const double erretm = 2.0 * kEps * (irho + fabs(psi) + fabs(phi));
+    if (fabs(f) <= erretm || hi_t - lo_t <= 2.0 * kEps * fmax(fabs(lo_t), fabs(hi_t))) break;
+    if (f < 0.0) lo_t = tau;
+    else hi_t = tau;
+    const double D1 = D1o - tau;
+    const double b1 = dpsi * D1 * D1;
+    double cc = irho + (psi - b1 / D1);
+    double eta = 0.0;
+    bool ok = false;
+    if (i < k - 1) {
+      const double D2 = D2o - tau;
+      const double b2 = dphi * D2 * D2;
+      cc += phi - b2 / D2;
+      const double B = cc * (D1 + D2) + b1 + b2;
+      const double C = D1 * D2 * f;
+      const double sq = sqrt(fmax(B * B - 4.0 * cc * C, 0.0));
+      double r1 = 0.0, r2 = 0.0;
+      int nr = 0;
+      if (cc != 0.0) {
+        const double q = 0.5 * (B + copysign(sq, B));
+        if (q != 0.0) {
+          r1 = q / cc;
+          r2 = C / q;
+          nr = 2;
+        }
+      } else if (B != 0.0) {
+        r1 = C / B;
+        nr = 1;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // straight-line: candidate q valid when q < nr
+        const double cand = q == 0 ? r1 : r2;
+        const double nt = tau + cand;
+        const bool good = q < nr && isfinite(nt) && nt > lo_t && nt < hi_t && (!ok || fabs(cand) < fabs(eta));
+        eta = good ? cand : eta;
+        ok = ok || good;
+      }
+    } else {
+      cc += phi;
+      if (cc != 0.0) {
+        const double cand = D1 + b1 / cc;
+        const double nt = tau + cand;
+        if (isfinite(nt) && nt > lo_t && nt < hi_t) {
+          eta = cand;
+          ok = true;
+        }
+      }
+    }
+    if (!ok) {
+      tau = 0.5 * (lo_t + hi_t);
+    } else {
+      tau += eta;
+      if (fabs(eta) <= 2.0 * kEps * fabs(tau)) break;
+    }
+  }
+  o_out = o;
+  tau_out = tau;
+  return it;
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void dc_wave_merge_kernel(double* __restrict__ Q, long ldq, double* __restrict__ D,
+                                                             const double* __restrict__ e, const int* __restrict__ mg,
+                                                             int S) {
+  constexpr int NT = NC / 4;  // secular / Loewner / U terms per lane (quad per root), GEMM columns per wave
+  extern __shared__ double sm[];
+  double* Ut = sm;            // [S][NC] U row-major: Ut[j NC + c] = U(j, c), NC >= S a power of 2
+  double* sQ = Ut + S * NC;   // [S][S] the merge's block of Q: sQ[c S + r] = Q(lo + r, lo + c)
+  double* sd = sQ + S * S;    // [64] each: sorted d, z (walk scratch), secular d, z, tau, z-hat,
+  double* sz = sd + 64;       // rotation cosines and sines
+  double* dd = sz + 64;
+  double* zz = dd + 64;
+  double* st = zz + 64;
+  double* zh = st + 64;
+  double* rc = zh + 64;
+  double* rsn = rc + 64;
+  int* keep = (int*)(rsn + 64);  // [64] each: survivors, halves bits, secular origin, block
+  int* hm = keep + 64;           // column of secular / deflated position, rotation columns
+  int* org = hm + 64;
+  int* cs = org + 64;
+  int* rp = cs + 64;
+  int* rq = rp + 64;
+  __shared__ int s_nrot, s_k;
+  __shared__ double s_rho;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lo = mg[3 * blockIdx.x], mid = mg[3 * blockIdx.x + 1], hi = mg[3 * blockIdx.x + 2];
+  const int s = hi - lo, s1 = mid - lo;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const double beta = e[mid - 1];
+  const double sgn = beta < 0.0 ? -1.0 : 1.0;
+  WAVE_MARK(0);
+  {  // stage the block: up to 16 loads in flight per thread (one round trip for s <= 64)
+    const int tot = s * s;
+    for (int q0 = 0; q0 < tot; q0 += 256 * 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int q = q0 + 256 * u + tid;
+        v[u] = q < tot ? Q[(long)(lo + q / s) * ldq + lo + q % s] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int q = q0 + 256 * u + tid;
+        if (q < tot) sQ[(q / s) * S + q % s] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  WAVE_MARK(1);
+  if (wv == 0) {  // sort, deflation, rotations: wave 0, lane = sorted position
+    // z: the left block's last row, the right block's first row (sign of beta folded in)
+    double zr = 0.0, key = __builtin_inf();
+    int id = lane;
+    if (lane < s) {
+      zr = lane < s1 ? sQ[lane * S + s1 - 1] : sgn * sQ[lane * S + s1];
+      key = D[lo + lane];
+    }
+    // bitonic sort of (d, index) across the wave, in registers; lanes >= s are +inf
+    const int p2 = s <= 2 ? 2 : 1 << (32 - __builtin_clz(s - 1));  // lanes >= p2 are already in place
+    for (int kk = 2; kk <= p2; kk <<= 1) {
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        const double ok = __shfl_xor(key, j);
+        const int oi = __shfl_xor(id, j);
+        const bool oless = ok < key || (ok == key && oi < id);
+        if ((((lane & j) == 0) == ((lane & kk) == 0)) ? oless : !oless) {
+          key = ok;
+          id = oi;
+        }
+      }
+    }
+    double dv = key, zv = __shfl(zr, id);
+    const int srcv = id;
+    int hv = id < s1 ? 1 : 2;
+    const bool in = lane < s;
+    const double nz2 = wave_sum_d_dpp(in ? zv * zv : 0.0);
+    const double dmax = wave_max_d(in ? fabs(dv) : 0.0);
+    const double rho = fabs(beta) * nz2;
+    zv *= nz2 > 0.0 ? 1.0 / sqrt(nz2) : 0.0;
+    const double zmax = wave_max_d(in ? fabs(zv) : 0.0);
+    const double tol = 8.0 * kEps * fmax(dmax, rho * zmax);
+    int nrot = 0;
+    if (rho > 0.0) {
+      // does a pair of consecutive survivors pass the rotation test (the level kernels' pre-check)?
+      const bool sv = in && rho * fabs(zv) > tol;
+      const unsigned long long msv = __ballot(sv);
+      const unsigned long long pb = msv & below;
+      const int p = pb ? 63 - __builtin_clzll(pb) : 0;
+      const double zp = __shfl(zv, p), dp = __shfl(dv, p);
+      bool pass = false;
+      if (sv && pb) {
+        const double t2 = hypot(zv, zp);
+        pass = fabs((dv - dp) * (zv / t2) * (zp / t2)) <= tol;
+      }
+      const unsigned long long mpass = __ballot(pass);
+      if (mpass) {
+        // dependent walk (one lane, the level kernels' order) over the survivors in LDS; a
+        // pair whose first member was not rotated into sees its original values (mpass bits)
+        sd[lane] = dv;
+        sz[lane] = zv;
+        hm[lane] = hv;
+        if (sv) keep[__popcll(pb)] = lane;
+        lds_sync_wave();
+        if (lane == 0) {
+          const int ns = __popcll(msv);
+          int nr = 0, i = 1;
+          bool chain = false;
+          while (i < ns) {
+            const int pj = keep[i - 1], j = keep[i];
+            if (!chain && !((mpass >> j) & 1ull)) {
+              ++i;
+              continue;
+            }
+            double ss = sz[pj], cc = sz[j];
+            const double t2 = hypot(cc, ss);
+            const double t = sd[j] - sd[pj];
+            cc /= t2;
+            ss = -ss / t2;
+            if (fabs(t * cc * ss) <= tol) {
+              sz[j] = t2;
+              sz[pj] = 0.0;
+              hm[j] |= hm[pj];
+              hm[pj] |= 4;
+              rp[nr] = pj;
+              rq[nr] = j;
+              rc[nr] = cc;
+              rsn[nr] = ss;
+              ++nr;
+              const double tt = sd[pj] * cc * cc + sd[j] * ss * ss;
+              sd[j] = sd[pj] * ss * ss + sd[j] * cc * cc;
+              sd[pj] = tt;
+              chain = true;
+            } else {
+              chain = false;
+            }
+            ++i;
+          }
+          s_nrot = nr;
+        }
+        lds_sync_wave();
+        nrot = s_nrot;
+        dv = sd[lane];
+        zv = sz[lane];
+        hv = hm[lane];
+      }
+    }
+    // kept = survivors not rotated away (in sorted order), deflated = the rest (in sorted order)
+    const bool dj = in && (rho == 0.0 || rho * fabs(zv) <= tol || (hv & 4));
+    const bool kp = in && !dj;
+    const unsigned long long mk = __ballot(kp), md = __ballot(dj);
+    const int k = __popcll(mk);
+    if (nrot && lane < s) {  // rotations on the block's columns (sorted positions -> source columns)
+      for (int q = 0; q < nrot; ++q) {
+        const int xc = __shfl(srcv, rp[q]), yc = __shfl(srcv, rq[q]);
+        const double xv = sQ[xc * S + lane], yv = sQ[yc * S + lane];
+        sQ[xc * S + lane] = rc[q] * xv + rsn[q] * yv;
+        sQ[yc * S + lane] = rc[q] * yv - rsn[q] * xv;
+      }
+    }
+    if (kp) {
+      const int t = __popcll(mk & below);
+      dd[t] = dv;
+      zz[t] = zv;
+      cs[t] = srcv;
+    }
+    if (dj) {
+      const int t = k + __popcll(md & below);
+      cs[t] = srcv;
+      D[lo + t] = dv;
+    }
+    if (lane == 0) {
+      s_k = k;
+      s_rho = rho;
+    }
+  }
+  __syncthreads();
+  WAVE_MARK(2);
+  const int k = s_k;
+  const double rho = s_rho;
+  const int i4 = tid >> 2, part = tid & 3;
+  WAVE_MARK(3);
+  int its = 0;
+  if (i4 < k) {  // secular root i4 by a quad
+    int o;
+    double tau;
+    its = secular_quad<NT>(i4, part, k, rho, dd, zz, o, tau);
+    if (part == 0) {
+      org[i4] = o;
+      st[i4] = tau;
+      D[lo + i4] = dd[o] + tau;
+    }
+  }
+  if (blockIdx.x == 0 && wv == 0) {  // iterations of the slowest of roots 0-15 (harp_dc_wave_stamps)
+    const int mx = (int)wave_max_d((double)its);
+    if (lane == 0) g_wave_it = mx;
+  }
+  __syncthreads();
+  WAVE_MARK(4);
+  if (i4 < k) {  // Loewner z-hat of position i4 by a quad
+    const double dl = dd[i4];
+    double pr = 1.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int i = part + 4 * q;
+      if (i < k) {
+        const double num = (dd[org[i]] - dl) + st[i];
+        pr *= i == i4 ? num / rho : num / (dd[i] - dl);
+      }
+    }
+    pr = quad_prod_d(pr);
+    if (part == 0) zh[i4] = copysign(sqrt(fmax(pr, 0.0)), zz[i4]);
+  }
+  __syncthreads();
+  WAVE_MARK(5);
+  if (i4 < k) {  // column i4 of U, normalised, by a quad
+    const double dor = dd[org[i4]], tau = st[i4];
+    double u[NT];
+    double s2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int j = part + 4 * q;
+      u[q] = j < k ? zh[j] / ((dd[j] - dor) - tau) : 0.0;
+      s2 = fma(u[q], u[q], s2);
+    }
+    const double inv = 1.0 / sqrt(quad_sum_d(s2));
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int j = part + 4 * q;
+      if (j < k) Ut[j * NC + i4] = u[q] * inv;
+    }
+  }
+  __syncthreads();
+  WAVE_MARK(6);
+  // Q(lo + r, lo + c) = sum_j sQ(r, cs[j]) U(j, c) for c < k, sQ(r, cs[c]) for c >= k: lane = row,
+  // wave wv owns columns wv NT .. wv NT + NT - 1 (accumulators in registers; U rows are
+  // wave-uniform LDS reads)
+  if (lane < s) {
+    double* qo = Q + (long)lo * ldq + lo + lane;
+    const int c0 = wv * NT;
+    if (c0 < k) {
+      double acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = 0.0;
+      for (int j = 0; j < k; ++j) {
+        const double qv = sQ[cs[j] * S + lane];
+        const double* u = Ut + j * NC + c0;
+#pragma unroll
+        for (int t = 0; t < NT; t += 2) {
+          const dc_d2 uv = *(const dc_d2*)(u + t);
+          acc[t] = fma(qv, uv.x, acc[t]);
+          acc[t + 1] = fma(qv, uv.y, acc[t + 1]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (c0 + t < k) qo[(long)(c0 + t) * ldq] = acc[t];
+    }
+    for (int c = k + wv; c < s; c += 4) qo[(long)c * ldq] = sQ[cs[c] * S + lane];
+  }
+  WAVE_MARK(7);
+}
+
+int wave_merge_nc(int S) { return S <= 8 ? 8 : S <= 16 ? 16 : S <= 32 ? 32 : 64; }
+
+size_t wave_merge_lds(int S) {
+  return sizeof(double) * ((size_t)S * S + (size_t)S * wave_merge_nc(S) + 8 * 64) + sizeof(int) * 6 * 64;
+}
+
+template <int NC>
+int launch_wave_merge(double* Q, long ldq, double* D, const double* e, const int* mg, int nm, int S, hipStream_t st) {
+  const size_t lds = wave_merge_lds(S);
+  if (lds > 65536 && hipFuncSetAttribute((const void*)dc_wave_merge_kernel<NC>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return HARP_ELAUNCH;
+  dc_wave_merge_kernel<NC><<<dim3((unsigned)nm), dim3(256), lds, st>>>(Q, ldq, D, e, mg, S);
+  return harp_launch_status();
+}
+
+// largest merge of the levels on dc_wave_merge_kernel: HARP_DC_WAVE_MERGE (0 = every level on
+// the level kernels; A/B and tests), at most kWaveMerge
+int wave_merge_max() {
+  static const int m = [] {
+    const char* v = getenv("HARP_DC_WAVE_MERGE");
+    const int x = v ? atoi(v) : kWaveMergeDefault;
+    return x < 0 ? 0 : x > kWaveMerge ? kWaveMerge : x;
+  }();
+  return m;
+}
+
 size_t prep_lds(int smax) { return (size_t)smax * (2 * sizeof(double) + 4 * sizeof(int)); }
 
 }  // namespace
 
 HARP_EXPORT int harp_dc_max_n() { return kMaxN; }
+HARP_EXPORT int harp_dc_wave_stamps(long long* out) {
+  int it = 0;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), sizeof(long long) * 8) != hipSuccess ||
+      hipMemcpyFromSymbol(&it, HIP_SYMBOL(g_wave_it), sizeof(int)) != hipSuccess)
+    return HARP_ELAUNCH;
+  out[8] = it;
+  return HARP_OK;
+}
 
 HARP_EXPORT int harp_dc_prep_stamps(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prep_t), sizeof(long long) * 9) == hipSuccess ? HARP_OK : HARP_ELAUNCH;
@@ -813,6 +1270,15 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
     if (smax < 2 || smax > n) return HARP_EBADARG;
     w.ldu = smax;
     const int* mg = merges + 3 * m0;
+    if (smax <= wave_merge_max()) {
+      const int nc = wave_merge_nc(smax);
+      const int s_ = nc == 8    ? launch_wave_merge<8>(Q, n, dmod, e, mg, nm, smax, st)
+                     : nc == 16 ? launch_wave_merge<16>(Q, n, dmod, e, mg, nm, smax, st)
+                     : nc == 32 ? launch_wave_merge<32>(Q, n, dmod, e, mg, nm, smax, st)
+                                : launch_wave_merge<64>(Q, n, dmod, e, mg, nm, smax, st);
+      if (s_ != HARP_OK) return s_;
+      continue;
+    }
     const size_t lds = prep_lds(smax);
     // set per launch (a host-side attribute call, no process-wide cache to race on)
     if (lds > 65536 && hipFuncSetAttribute((const void*)dc_prep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

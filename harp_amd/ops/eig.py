@@ -36,6 +36,7 @@ _lib.register({
                          _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
     "harp_dc_max_n": [],
     "harp_dc_prep_stamps": [_lib.c_void_p],
+    "harp_dc_wave_stamps": [_lib.c_void_p],
     "harp_dc_ws_doubles": [_lib.c_int],
     # dmod, e, n, Q, merges, level_off, level_smax, nlevels, ws, stream
     "harp_dc_tridiag": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,

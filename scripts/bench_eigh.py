@@ -100,6 +100,11 @@ def main():
     st = (ctypes.c_longlong * 9)()
     E._lib.check(k.harp_dc_prep_stamps(ctypes.cast(st, ctypes.c_void_p)), "dc_prep_stamps")
     rec["dc_top_prep_cycles"] = [st[i + 1] - st[i] for i in range(8)]
+    sw = (ctypes.c_longlong * 9)()
+    E._lib.check(k.harp_dc_wave_stamps(ctypes.cast(sw, ctypes.c_void_p)), "dc_wave_stamps")
+    # block 0 of the last one-wave merge level: stage, sort+deflate, scatter, secular, Loewner, U, GEMM
+    rec["dc_wave_phase_cycles"] = [sw[i + 1] - sw[i] for i in range(7)]
+    rec["dc_wave_secular_max_iters"] = sw[8]
     rec["back_transform_ms"] = timed(lambda: E.back_transform(Vt, tau, Z))
     rec["wy_factor_ms"] = timed(lambda: E.wy_factor(Vt, tau))
     Vm, Mt = E.wy_factor(Vt, tau)

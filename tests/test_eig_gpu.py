@@ -1,5 +1,6 @@
 """One-XCD symmetric eigensolver (csrc/eig.hip: cooperative Householder tridiagonalisation +
 multisection) vs torch.linalg.eigvalsh (rocSOLVER) in fp64."""
+import os
 import time
 
 import pytest
@@ -114,8 +115,13 @@ def _tridiag_cases():
     d = np.ones(n)
     d[::2] = 2.0
     yield "decoupled", d, np.zeros(n - 1)
-    for m in (1, 2, 3, 17, 4096):
+    for m in (1, 2, 3, 17, 64, 65, 4096):
         yield f"n{m}", rng.standard_normal(m), rng.standard_normal(m - 1)
+    # every merge on the one-wave path (n <= 64), with rotations (cluster) and zero couplings
+    yield "cluster64", 1 + 1e-9 * rng.standard_normal(64), 1e-9 * rng.standard_normal(63)
+    e = rng.standard_normal(63)
+    e[::4] = 0.0
+    yield "split64", np.repeat(rng.standard_normal(16), 4), e
 
 
 @pytest.mark.parametrize("case", list(_tridiag_cases()), ids=lambda c: c[0])
@@ -134,6 +140,33 @@ def test_dc_tridiag_kernels(cuda, case):
     res = float((T @ V - V * w).abs().max()) / nt
     ev = float((w - torch.linalg.eigvalsh(T)).abs().max()) / nt
     assert orth <= 1e-12 and res <= 1e-12 and ev <= 1e-12, (orth, res, ev)
+
+
+def test_dc_level_kernels_only(cuda):
+    """HARP_DC_WAVE_MERGE=0 (read once per process, so in a child process): every level on
+    the level kernels, the path the one-wave merge kernel replaces for merges <= 64 rows."""
+    import subprocess
+    import sys
+
+    code = (
+        "import numpy as np, torch\n"
+        "from harp_amd.ops import eig as EIG\n"
+        "rng = np.random.default_rng(1)\n"
+        "for n in (64, 1000):\n"
+        "    for tag in ('randn', 'cluster'):\n"
+        "        sc = 1.0 if tag == 'randn' else 1e-9\n"
+        "        d = torch.from_numpy(1 + sc * rng.standard_normal(n)).cuda()\n"
+        "        e = torch.from_numpy(sc * rng.standard_normal(n - 1)).cuda()\n"
+        "        w, V = EIG.eigh_tridiag(d, e)\n"
+        "        T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)\n"
+        "        nt = float(torch.linalg.matrix_norm(T, 2))\n"
+        "        I = torch.eye(n, dtype=torch.float64, device='cuda')\n"
+        "        assert float((V.t() @ V - I).abs().max()) <= 1e-12\n"
+        "        assert float((T @ V - V * w).abs().max()) / nt <= 1e-12\n"
+        "print('ok')\n")
+    env = dict(os.environ, HARP_DC_WAVE_MERGE="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
 def test_eigh_correlation_matrix(cuda):
