@@ -12,4 +12,5 @@ for m in 64 32 16 8 0; do HARP_DC_WAVE_MERGE=$m timeout -k 10 200 python scripts
 for f in 64 32 16 8 0; do python -c "import json,sys; r=json.load(open(sys.argv[1])); print(sys.argv[1], r['dc_ms'], r['eigh_ll_ms'], r['dc_wave_phase_cycles'], r['dc_wave_secular_max_iters'])" "$out/bench_$f.json"; done
 timeout -k 10 300 rocprofv3 --kernel-trace -d "$out/prof" -o run -- python3 scripts/bench_eigh.py 1000 > "$out/prof.log" 2>&1 || { tail -5 "$out/prof.log"; exit 1; }
 python scripts/dc_level_summary.py "$out/prof/run_results.db" > "$out/dc_levels.txt" && cat "$out/dc_levels.txt"
+python scripts/eigh_timeline.py "$out/prof/run_results.db" > "$out/eigh_timeline.txt" && tail -50 "$out/eigh_timeline.txt"
 rm -rf "$out/prof"
