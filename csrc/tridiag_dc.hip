@@ -138,39 +138,90 @@ __global__ __launch_bounds__(1024) void dc_prep_kernel(double* __restrict__ Q, l
   }
   __syncthreads();
   PREP_MARK(1);
-  // sort (value, index) pairs ascending, ties by index, in place in LDS: bitonic network in
-  // the all-ascending (flip) form, where a comparator always keeps the smaller key at the
-  // lower position -- so the positions past s act as +inf and are never touched (no padding
-  // storage). log2(P2) (log2(P2) + 1) / 2 barrier stages instead of s compares per thread.
-  for (int j = tid; j < s; j += T) src[j] = j;
+  // sort (value, index) pairs ascending, ties by index. Each half is the output of a child
+  // merge: its kept roots ascending, then its deflated values ascending -- at most one descent
+  // per half, so the input is at most four sorted runs and every element's sorted position is
+  // its offset in its run plus a binary-search count in each other run (a few dependent LDS
+  // reads per thread). Any other input (not produced here) takes the bitonic network.
+  __shared__ int s_nb[2], s_pb[2];
+  if (tid < 2) {
+    s_nb[tid] = 0;
+    s_pb[tid] = tid == 0 ? s1 : s;
+  }
   __syncthreads();
-  int P2 = 1;
-  while (P2 < s) P2 <<= 1;
-  auto cmpswap = [&](int i, int l) {
-    if (l >= s) return;
-    const double a = sd[i], b = sd[l];
-    const int ai = src[i], bi = src[l];
-    if (b < a || (b == a && bi < ai)) {
-      sd[i] = b;
-      sd[l] = a;
-      src[i] = bi;
-      src[l] = ai;
+  for (int j = tid; j < s; j += T) {
+    if (j != 0 && j != s1 && sd[j] < sd[j - 1]) {
+      const int h = j >= s1;
+      atomicAdd(&s_nb[h], 1);
+      s_pb[h] = j;
     }
-  };
-  for (int lp = 1; (1 << lp) <= P2; ++lp) {  // blocks of p = 2^lp (shifts, no integer divides)
-    const int hm1 = (1 << (lp - 1)) - 1;
-    for (int c = tid; c < (P2 >> 1); c += T) {  // flip: i <-> mirror within the block of p
-      const int base = (c >> (lp - 1)) << lp, o = c & hm1;
-      cmpswap(base + o, base + (1 << lp) - 1 - o);
+  }
+  __syncthreads();
+  if (s_nb[0] <= 1 && s_nb[1] <= 1) {
+    const int rb[5] = {0, s_pb[0], s1, s_pb[1], s};
+    for (int j = tid; j < s; j += T) {
+      const double v = sd[j];
+      int r = 0;
+      while (j >= rb[r + 1]) ++r;
+      int pos = j - rb[r];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q == r) continue;
+        // runs before r hold smaller indices (a tie counts), runs after r larger ones (it does not)
+        int a = rb[q], b = rb[q + 1];
+        const int base = a;
+        while (a < b) {
+          const int m = (a + b) >> 1;
+          const double x = sd[m];
+          if (x < v || (q < r && x == v)) a = m + 1;
+          else b = m;
+        }
+        pos += a - base;
+      }
+      keep[pos] = __double2loint(v);
+      defl[pos] = __double2hiint(v);
+      hm[pos] = j;
     }
-    lds_sync();
-    for (int lq = lp - 2; lq >= 0; --lq) {  // half-cleaners at distance q = 2^lq
-      const int qm1 = (1 << lq) - 1;
-      for (int c = tid; c < (P2 >> 1); c += T) {
-        const int i = ((c >> lq) << (lq + 1)) + (c & qm1);
-        cmpswap(i, i + (1 << lq));
+    __syncthreads();
+    for (int j = tid; j < s; j += T) {
+      sd[j] = __hiloint2double(defl[j], keep[j]);
+      src[j] = hm[j];
+    }
+    __syncthreads();
+  } else {
+    // bitonic network in the all-ascending (flip) form, in place in LDS: a comparator always
+    // keeps the smaller key at the lower position, so the positions past s act as +inf and
+    // are never touched (no padding storage)
+    for (int j = tid; j < s; j += T) src[j] = j;
+    __syncthreads();
+    int P2 = 1;
+    while (P2 < s) P2 <<= 1;
+    auto cmpswap = [&](int i, int l) {
+      if (l >= s) return;
+      const double a = sd[i], b = sd[l];
+      const int ai = src[i], bi = src[l];
+      if (b < a || (b == a && bi < ai)) {
+        sd[i] = b;
+        sd[l] = a;
+        src[i] = bi;
+        src[l] = ai;
+      }
+    };
+    for (int lp = 1; (1 << lp) <= P2; ++lp) {  // blocks of p = 2^lp (shifts, no integer divides)
+      const int hm1 = (1 << (lp - 1)) - 1;
+      for (int c = tid; c < (P2 >> 1); c += T) {  // flip: i <-> mirror within the block of p
+        const int base = (c >> (lp - 1)) << lp, o = c & hm1;
+        cmpswap(base + o, base + (1 << lp) - 1 - o);
       }
       lds_sync();
+      for (int lq = lp - 2; lq >= 0; --lq) {  // half-cleaners at distance q = 2^lq
+        const int qm1 = (1 << lq) - 1;
+        for (int c = tid; c < (P2 >> 1); c += T) {
+          const int i = ((c >> lq) << (lq + 1)) + (c & qm1);
+          cmpswap(i, i + (1 << lq));
+        }
+        lds_sync();
+      }
     }
   }
   PREP_MARK(2);
