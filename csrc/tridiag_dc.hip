@@ -483,6 +483,28 @@ __device__ __forceinline__ double rcp_nr(double x) {
   return fma(r, fma(-x, r, 1.0), r);
 }
 
+// Initial tau of root i < k - 1 (LAPACK dlaed4's two-pole start): f0 is the secular function
+// at the gap's midpoint, c = f0 without the two nearest poles' terms, and the root of
+// c + z_i^2 / (d_i - l) + z_{i+1}^2 / (d_{i+1} - l) in the half f0's sign selects (origin d_i:
+// tau in (0, mid); origin d_{i+1}: tau in (-mid, 0)); the bracket's midpoint if that is not
+// strictly inside it. Saves the first iterations of the rational steps from the midpoint.
+__device__ __forceinline__ double secular_init(double f0, double mid, double zi2, double zj2, bool left, double lo_t,
+                                               double hi_t) {
+  const double del = 2.0 * mid;
+  const double c = f0 + (zi2 - zj2) / mid;
+  double tau;
+  if (left) {
+    const double a = c * del + zi2 + zj2, b = zi2 * del;
+    const double sq = sqrt(fabs(a * a - 4.0 * b * c));
+    tau = a > 0.0 ? 2.0 * b / (a + sq) : (a - sq) / (2.0 * c);
+  } else {
+    const double a = c * del - zi2 - zj2, b = zj2 * del;
+    const double sq = sqrt(fabs(a * a + 4.0 * b * c));
+    tau = a < 0.0 ? 2.0 * b / (a - sq) : -(a + sq) / (2.0 * c);
+  }
+  return (isfinite(tau) && tau > lo_t && tau < hi_t) ? tau : 0.5 * (lo_t + hi_t);
+}
+
 template <bool kReg>
 __device__ __forceinline__ void secular_solve(int i, int k, int lane, double rho, const double* __restrict__ dd,
                                               const double* __restrict__ zz, int& o_out, double& tau_out) {
@@ -497,7 +519,8 @@ __device__ __forceinline__ void secular_solve(int i, int k, int lane, double rho
     }
   }
   int o;
-  double lo_t, hi_t;
+  double lo_t, hi_t, tau0 = 0.0;
+  bool init = false;
   const double ddi = dd[i];
   if (i < k - 1) {
     const double mid = 0.5 * (dd[i + 1] - ddi);
@@ -519,6 +542,8 @@ __device__ __forceinline__ void secular_solve(int i, int k, int lane, double rho
       lo_t = -mid;
       hi_t = 0.0;
     }
+    tau0 = secular_init(f, mid, zz[i] * zz[i], zz[i + 1] * zz[i + 1], f >= 0.0, lo_t, hi_t);
+    init = true;
   } else {
     double z2 = 0.0;
     if (kReg) {
@@ -537,7 +562,7 @@ __device__ __forceinline__ void secular_solve(int i, int k, int lane, double rho
     for (int q = 0; q < kSecR; ++q) dr[q] -= dor;
   }
   const double D1o = ddi - dor, D2o = i < k - 1 ? dd[i + 1] - dor : 0.0;
-  double tau = 0.5 * (lo_t + hi_t);
+  double tau = init ? tau0 : 0.5 * (lo_t + hi_t);
   for (int it = 0; it < 64; ++it) {
     double psi = 0.0, phi = 0.0, dpsi = 0.0, dphi = 0.0;
     if (kReg) {
@@ -862,7 +887,8 @@ __device__ int secular_quad(int i, int part, int k, double rho, const double* dd
     z2r[q] = j < k ? zz[j] * zz[j] : 0.0;
   }
   int o;
-  double lo_t, hi_t;
+  double lo_t, hi_t, tau0 = 0.0;
+  bool init = false;
   const double ddi = dd[i];
   if (i < k - 1) {
     const double mid = 0.5 * (dd[i + 1] - ddi);
@@ -879,6 +905,8 @@ __device__ int secular_quad(int i, int part, int k, double rho, const double* dd
       lo_t = -mid;
       hi_t = 0.0;
     }
+    tau0 = secular_init(f, mid, zz[i] * zz[i], zz[i + 1] * zz[i + 1], f >= 0.0, lo_t, hi_t);
+    init = true;
   } else {
     double z2 = 0.0;
 #pragma unroll
@@ -891,7 +919,7 @@ __device__ int secular_quad(int i, int part, int k, double rho, const double* dd
 #pragma unroll
   for (int q = 0; q < NT; ++q) dr[q] -= dor;
   const double D1o = ddi - dor, D2o = i < k - 1 ? dd[i + 1] - dor : 0.0;
-  double tau = 0.5 * (lo_t + hi_t);
+  double tau = init ? tau0 : 0.5 * (lo_t + hi_t);
   int it = 0;
   for (; it < 64; ++it) {
     double psi = 0.0, phi = 0.0, dpsi = 0.0, dphi = 0.0;
