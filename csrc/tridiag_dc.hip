@@ -1287,6 +1287,60 @@ int wave_merge_max() {
   return m;
 }
 
+// Inputs of the D&C in one launch (they were ten small torch ops ahead of the first level, ~130
+// us of the critical path after the reduction): dmod = d with |e[p]| subtracted at p and p + 1
+// for every split point p + 1 (the tree splits down to single rows, so every p in [1, n) is a
+// split: dmod[p] = (d[p] - |e[p]|) - |e[p - 1]|, the order of the former two index_add_), Q = I
+// (column-major), the workspace zeroed, perm = the identity (for dc_order_kernel).
+__global__ __launch_bounds__(256) void dc_setup_kernel(const double* __restrict__ d, const double* __restrict__ e, int n,
+                                                       double* __restrict__ dmod, double* __restrict__ Q,
+                                                       double* __restrict__ ws, long wsn, long* __restrict__ perm) {
+  const long nn = (long)n * n;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nn || i < wsn; i += stride) {
+    if (i < nn) Q[i] = i % (n + 1) == 0 ? 1.0 : 0.0;
+    if (i < wsn) ws[i] = 0.0;
+    if (i < n) {
+      const int p = (int)i;
+      double v = d[p];
+      if (p + 1 < n) v -= fabs(e[p]);
+      if (p >= 1) v -= fabs(e[p - 1]);
+      dmod[p] = v;
+      perm[p] = p;
+    }
+  }
+}
+
+// Ascending order of the D&C's eigenvalues (ties by position): rank_j = the number of
+// (d_i, i) < (d_j, j). Workgroup b ranks positions 64 b .. 64 b + 63 with its four waves
+// counting over quarters of all n values (in LDS, n <= kMaxN: 32 KB). perm is the identity
+// from dc_setup_kernel, so a NaN (no strict order, colliding ranks) cannot leave an index
+// unwritten. Replaces a torch argsort + gather (~7 small kernels) after the top merge.
+__global__ __launch_bounds__(256) void dc_order_kernel(const double* __restrict__ dmod, int n, double* __restrict__ w,
+                                                       long* __restrict__ perm) {
+  __shared__ double sv[kMaxN];
+  __shared__ int part[4][64];
+  for (int j = threadIdx.x; j < n; j += 256) sv[j] = dmod[j];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const double v = j < n ? sv[j] : 0.0;
+  const int q = (n + 3) / 4, i0 = wv * q, i1 = i0 + q < n ? i0 + q : n;
+  int r = 0;
+#pragma unroll 8
+  for (int i = i0; i < i1; ++i) {
+    const double x = sv[i];
+    r += (x < v || (x == v && i < j)) ? 1 : 0;
+  }
+  part[wv][lane] = r;
+  __syncthreads();
+  if (wv == 0 && j < n) {
+    r = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    w[r] = v;
+    perm[r] = j;
+  }
+}
+
 size_t prep_lds(int smax) { return (size_t)smax * (2 * sizeof(double) + 4 * sizeof(int)); }
 
 }  // namespace
@@ -1308,6 +1362,29 @@ HARP_EXPORT int harp_dc_prep_stamps(long long* out) {
 // doubles of the workspace for size n: Qb n^2, U n^2, dd/zz/tau/zh/rho/rotc/rots 7 n, sort
 // scratch 3 n; ints (colsrc/org/kcnt/rotp/rotq/jl/jr/kl/kr 9 n) follow as 5 n doubles
 HARP_EXPORT long harp_dc_ws_doubles(int n) { return 2L * n * n + 10L * n + 5L * n + 16; }
+
+// dmod, Q (n x n, column-major) and ws (harp_dc_ws_doubles(n)) for harp_dc_tridiag from the
+// tridiagonal (d, e): see dc_setup_kernel (the tree of ops/tridiag_dc.py tree_levels, which
+// splits every position 1 .. n - 1). e: n - 1 entries (any pointer when n == 1).
+HARP_EXPORT int harp_dc_setup(const double* d, const double* e, int n, double* dmod, double* Q, double* ws,
+                              long* perm, hipStream_t st) {
+  if (n < 1 || n > kMaxN || !d || !dmod || !Q || !ws || !perm || (n > 1 && !e)) return HARP_EBADARG;
+  const long wsn = harp_dc_ws_doubles(n);
+  const long work = wsn > (long)n * n ? wsn : (long)n * n;
+  long blocks = (work + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  dc_setup_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(d, e, n, dmod, Q, ws, wsn, perm);
+  return harp_launch_status();
+}
+
+// w = dmod ascending, perm[r] = the position of the r-th smallest (ties by position), for
+// n <= harp_dc_max_n(): dc_order_kernel. perm: int64 (a torch index), the identity on entry
+// (harp_dc_setup writes it).
+HARP_EXPORT int harp_dc_order(const double* dmod, int n, double* w, long* perm, hipStream_t st) {
+  if (n < 1 || n > kMaxN || !dmod || !w || !perm) return HARP_EBADARG;
+  dc_order_kernel<<<dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st>>>(dmod, n, w, perm);
+  return harp_launch_status();
+}
 
 // Eigen-decomposition of the symmetric tridiagonal (dmod, e): dmod is the diagonal with
 // |e[mid - 1]| already subtracted at d[mid - 1] and d[mid] for every merge (harp_amd/ops/eig.py),

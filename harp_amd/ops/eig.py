@@ -38,6 +38,11 @@ _lib.register({
     "harp_dc_prep_stamps": [_lib.c_void_p],
     "harp_dc_wave_stamps": [_lib.c_void_p],
     "harp_dc_ws_doubles": [_lib.c_int],
+    # dmod, n, w, perm (int64), stream
+    "harp_dc_order": [_lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
+    # d, e, n, dmod, Q, ws, perm, stream
+    "harp_dc_setup": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
+                      _lib.c_void_p, _lib.c_void_p],
     # dmod, e, n, Q, merges, level_off, level_smax, nlevels, ws, stream
     "harp_dc_tridiag": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                         _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
@@ -215,20 +220,22 @@ def eigh_tridiag(d: torch.Tensor, e: torch.Tensor):
         return torch.from_numpy(w).to(d), torch.from_numpy(V).to(d)
     dev = d.device
     k = _lib.kernels()
-    merges, off, smax, nlev, mids = _tree(n, dev)
-    dmod = d.clone().contiguous()
+    merges, off, smax, nlev, _ = _tree(n, dev)
     ec = e.contiguous() if e.numel() else torch.zeros(1, dtype=torch.float64, device=dev)
-    if mids.numel():
-        b = e[mids - 1].abs()
-        dmod.index_add_(0, mids - 1, -b)
-        dmod.index_add_(0, mids, -b)
-    Qt = torch.eye(n, dtype=torch.float64, device=dev)  # column-major Q == row-major Q^T
-    ws = torch.zeros(int(k.harp_dc_ws_doubles(n)), dtype=torch.float64, device=dev)
+    # dmod (d with |e| taken off both sides of every split), Q = I and the zeroed workspace
+    # in one launch (csrc/tridiag_dc.hip dc_setup_kernel; the tree splits every position)
+    dmod = torch.empty(n, dtype=torch.float64, device=dev)
+    Qt = torch.empty((n, n), dtype=torch.float64, device=dev)  # column-major Q == row-major Q^T
+    ws = torch.empty(int(k.harp_dc_ws_doubles(n)), dtype=torch.float64, device=dev)
+    perm = torch.empty(n, dtype=torch.int64, device=dev)  # identity here, the sort order below
+    _lib.check(k.harp_dc_setup(d.contiguous().data_ptr(), ec.data_ptr(), n, dmod.data_ptr(), Qt.data_ptr(),
+                               ws.data_ptr(), perm.data_ptr(), _lib.stream_ptr(dev)), "dc_setup")
     st = k.harp_dc_tridiag(dmod.data_ptr(), ec.data_ptr(), n, Qt.data_ptr(), merges.data_ptr(), off, smax, nlev,
                            ws.data_ptr(), _lib.stream_ptr(dev))
     _lib.check(st, "dc_tridiag")
-    order = torch.argsort(dmod)
-    return dmod[order], Qt[order].t()
+    w = torch.empty(n, dtype=torch.float64, device=dev)
+    _lib.check(k.harp_dc_order(dmod.data_ptr(), n, w.data_ptr(), perm.data_ptr(), _lib.stream_ptr(dev)), "dc_order")
+    return w, Qt.index_select(0, perm).t()
 
 
 def eigh(C: torch.Tensor, native: bool | None = None):
