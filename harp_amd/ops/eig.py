@@ -291,24 +291,24 @@ def _dc_and_back_transform(d, e, Vt, tau):
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         wy = wy_factor(Vt, tau)
-        if wy is not None:  # M^T row-major for the in-place row-major apply below
-            wy = (wy[0], wy[1].contiguous())
+        if wy is not None:  # V and M^T row-major for the in-place row-major apply below
+            wy = (wy[0].t().contiguous(), wy[1].contiguous())
     Vt.record_stream(side)
     tau.record_stream(side)
     lam, Z = eigh_tridiag(d, e)
     cur.wait_stream(side)
     if wy is None:
         return lam, Z
-    Vm, Mt = wy
+    V, Mt = wy
     Mt.record_stream(cur)
-    Vm.record_stream(cur)
+    V.record_stream(cur)
     Zt = Z.t()
     if Zt.is_contiguous():
         # X^T = Z^T - (Z^T V) M^T: row-major GEMMs in place on the fresh Z^T buffer (the
-        # eigenvectors come back as the columns of a transposed view); 0.122 -> ~0.102 ms at
+        # eigenvectors come back as the columns of a transposed view); 0.121 -> ~0.084 ms at
         # n = 1000 against apply_wy (profiles/r6_dcwave/probe_wy_apply.json)
-        return lam, Zt.addmm_(Zt @ Vm.t(), Mt, alpha=-1).t()
-    return lam, apply_wy(Vm, Mt, Z)
+        return lam, Zt.addmm_(Zt @ V, Mt, alpha=-1).t()
+    return lam, apply_wy(V.t(), Mt, Z)
 
 
 def wy_factor(Vt: torch.Tensor, tau: torch.Tensor):

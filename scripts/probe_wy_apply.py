@@ -21,6 +21,7 @@ Vt = torch.triu(torch.randn(n, n, generator=g, device=dev, dtype=torch.float64),
 tau = torch.full((n,), 1.0, device=dev, dtype=torch.float64)
 Vm, Mt = E.wy_factor(Vt, tau)
 Mtc = Mt.contiguous()
+Vc = Vm.t().contiguous()  # V (n x m) row-major
 print("Mt strides", Mt.stride(), "Vm strides", Vm.stride(), file=sys.stderr)
 
 
@@ -48,6 +49,11 @@ def e():  # d with M^T made row-major (off the critical path, on wy_factor's str
     return W.addmm_(Zt @ Vm.t(), Mtc, alpha=-1).t()
 
 
+def g():  # e with V row-major as well
+    W = Zt.clone()
+    return W.addmm_(Zt @ Vc, Mtc, alpha=-1).t()
+
+
 def f():  # a with M^T row-major
     Z = Zt.t()
     return torch.addmm(Z, Mtc.t(), Vm @ Z, alpha=-1)
@@ -56,7 +62,8 @@ def f():  # a with M^T row-major
 ref = a()
 rec = {"n": n}
 for name, fn in (("a_view", a), ("b_zt_v", b), ("c_rowmajor", c), ("d_inplace_incl_clone", d),
-                 ("e_inplace_mt_rowmajor_incl_clone", e), ("f_view_mt_rowmajor", f)):
+                 ("e_inplace_mt_rowmajor_incl_clone", e), ("f_view_mt_rowmajor", f),
+                 ("g_inplace_v_mt_rowmajor_incl_clone", g)):
     out = fn()
     err = float((out - ref).abs().max() / ref.abs().max())
     for _ in range(3):
