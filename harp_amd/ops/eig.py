@@ -290,9 +290,7 @@ def _dc_and_back_transform(d, e, Vt, tau):
         side = _SIDE[dev] = torch.cuda.Stream(dev)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        wy = wy_factor(Vt, tau)
-        if wy is not None:  # V and M^T row-major for the in-place row-major apply below
-            wy = (wy[0].t().contiguous(), wy[1].contiguous())
+        wy = wy_factor(Vt, tau, rowmajor=True)  # V and M^T row-major for the apply below
     Vt.record_stream(side)
     tau.record_stream(side)
     lam, Z = eigh_tridiag(d, e)
@@ -311,11 +309,14 @@ def _dc_and_back_transform(d, e, Vt, tau):
     return lam, apply_wy(V.t(), Mt, Z)
 
 
-def wy_factor(Vt: torch.Tensor, tau: torch.Tensor):
+def wy_factor(Vt: torch.Tensor, tau: torch.Tensor, rowmajor: bool = False):
     """Compact-WY factor of H_0 H_1 ... H_{n-3} (``Vt`` row c = v_c): Q = I - V T V^T with
     T^-1 = diag(1/tau) + striu(V^T V); returns (V^T, M^T) with M = V T (one GEMM and one
     triangular solve), or None for n <= 2 (Q = I). A reflector with tau = 0 is the
-    identity (its column of V is zeroed, no host sync)."""
+    identity (its column of V is zeroed, no host sync). ``rowmajor``: returns (V, M^T) both
+    contiguous (V n x m), the operands of the in-place row-major apply in
+    :func:`_dc_and_back_transform`; V^T V is then formed from two row-major operands (rocBLAS
+    picks a faster kernel for that form)."""
     n = Vt.shape[1]
     m = n - 2
     if m <= 0:
@@ -323,10 +324,13 @@ def wy_factor(Vt: torch.Tensor, tau: torch.Tensor):
     t = tau[:m]
     live = t != 0
     Vm = Vt[:m] * live.to(Vt.dtype).unsqueeze(1)  # V^T, m x n
-    Tinv = torch.triu(Vm @ Vm.t(), 1)
+    V = Vm.t().contiguous() if rowmajor else None
+    Tinv = torch.triu(Vm @ (V if rowmajor else Vm.t()), 1)
     Tinv.diagonal().copy_(torch.where(live, 1.0 / torch.where(live, t, torch.ones_like(t)), torch.ones_like(t)))
     # M^T = T^T V^T = Tinv^-T V^T: a lower-triangular solve with n right-hand sides
     Mt = torch.linalg.solve_triangular(Tinv.t(), Vm, upper=False)
+    if rowmajor:
+        return V, Mt.contiguous()
     return Vm, Mt
 
 
