@@ -1391,9 +1391,11 @@ HARP_EXPORT int harp_dc_order(const double* dmod, int n, double* w, long* perm, 
 // overwritten by the (unsorted) eigenvalues. Q: n x n column-major, = I on entry, holds the
 // eigenvectors on exit (columns in the order of dmod). merges: (lo, mid, hi) int32 triples
 // of all levels, bottom level first; level_off[l] .. level_off[l + 1]: level l's merges
-// (host array), level_smax[l]: its largest block. ws: harp_dc_ws_doubles(n) doubles, zeroed.
+// (host array), level_smax[l]: its largest block, level_full[l] (host, may be null): its
+// merges cover all n rows. ws: harp_dc_ws_doubles(n) doubles, zeroed.
 HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q, const int* merges,
-                                const int* level_off, const int* level_smax, int nlevels, double* ws, hipStream_t st) {
+                                const int* level_off, const int* level_smax, const int* level_full, int nlevels,
+                                double* ws, hipStream_t st) {
   if (n < 1 || n > kMaxN || !dmod || !Q || !ws || (nlevels > 0 && (!merges || !level_off || !level_smax)))
     return HARP_EBADARG;
   const long nn = (long)n * n;
@@ -1419,6 +1421,10 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
   w.jr = ip + 6 * n;
   w.kl = ip + 7 * n;
   w.kr = ip + 8 * n;
+  // a level whose merges cover every row writes its products to the other buffer and the two
+  // swap roles (no copy-back); Q's off-block entries are zero in both buffers throughout
+  double* cur = Q;
+  double* oth = Qb;
   for (int l = 0; l < nlevels; ++l) {
     const int m0 = level_off[l], nm = level_off[l + 1] - m0;
     const int smax = level_smax[l];
@@ -1428,10 +1434,10 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
     const int* mg = merges + 3 * m0;
     if (smax <= wave_merge_max()) {
       const int nc = wave_merge_nc(smax);
-      const int s_ = nc == 8    ? launch_wave_merge<8>(Q, n, dmod, e, mg, nm, smax, st)
-                     : nc == 16 ? launch_wave_merge<16>(Q, n, dmod, e, mg, nm, smax, st)
-                     : nc == 32 ? launch_wave_merge<32>(Q, n, dmod, e, mg, nm, smax, st)
-                                : launch_wave_merge<64>(Q, n, dmod, e, mg, nm, smax, st);
+      const int s_ = nc == 8    ? launch_wave_merge<8>(cur, n, dmod, e, mg, nm, smax, st)
+                     : nc == 16 ? launch_wave_merge<16>(cur, n, dmod, e, mg, nm, smax, st)
+                     : nc == 32 ? launch_wave_merge<32>(cur, n, dmod, e, mg, nm, smax, st)
+                                : launch_wave_merge<64>(cur, n, dmod, e, mg, nm, smax, st);
       if (s_ != HARP_OK) return s_;
       continue;
     }
@@ -1441,7 +1447,7 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
                                            (int)lds) != hipSuccess)
       return HARP_ELAUNCH;
     const int threads = smax >= 512 ? 1024 : smax >= 128 ? 256 : 64;
-    dc_prep_kernel<<<dim3((unsigned)nm), dim3(threads), lds, st>>>(Q, n, dmod, e, mg, w);
+    dc_prep_kernel<<<dim3((unsigned)nm), dim3(threads), lds, st>>>(cur, n, dmod, e, mg, w);
     const unsigned wg = (unsigned)((n + 3) / 4);
     dc_secular_kernel<<<dim3(wg), dim3(256), 0, st>>>(mg, nm, n, dmod, w);
     dc_loewner_kernel<<<dim3(wg), dim3(256), 0, st>>>(mg, nm, n, w);
@@ -1451,12 +1457,20 @@ HARP_EXPORT int harp_dc_tridiag(double* dmod, const double* e, int n, double* Q,
     if (glds > 65536 && hipFuncSetAttribute((const void*)dc_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)glds) != hipSuccess)
       return HARP_ELAUNCH;
-    dc_gemm_kernel<<<dim3((unsigned)(rtm * tiles), (unsigned)nm), dim3(256), glds, st>>>(Q, Qb, n, mg, w, rtm);
-    const long per = (long)smax * smax;
-    const unsigned cb = (unsigned)((per + 256 * 4 - 1) / (256 * 4));
-    dc_copyback_kernel<<<dim3(cb, (unsigned)nm), dim3(256), 0, st>>>(Qb, Q, n, mg);
+    dc_gemm_kernel<<<dim3((unsigned)(rtm * tiles), (unsigned)nm), dim3(256), glds, st>>>(cur, oth, n, mg, w, rtm);
+    if (level_full && level_full[l]) {
+      double* t = cur;
+      cur = oth;
+      oth = t;
+    } else {
+      const long per = (long)smax * smax;
+      const unsigned cb = (unsigned)((per + 256 * 4 - 1) / (256 * 4));
+      dc_copyback_kernel<<<dim3(cb, (unsigned)nm), dim3(256), 0, st>>>(oth, cur, n, mg);
+    }
     const int s_ = harp_launch_status();
     if (s_ != HARP_OK) return s_;
   }
+  if (cur != Q && hipMemcpyAsync(Q, cur, sizeof(double) * nn, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return HARP_ELAUNCH;
   return harp_launch_status();
 }

@@ -43,9 +43,9 @@ _lib.register({
     # d, e, n, dmod, Q, ws, perm, stream
     "harp_dc_setup": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                       _lib.c_void_p, _lib.c_void_p],
-    # dmod, e, n, Q, merges, level_off, level_smax, nlevels, ws, stream
+    # dmod, e, n, Q, merges, level_off, level_smax, level_full, nlevels, ws, stream
     "harp_dc_tridiag": [_lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
-                        _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
+                        _lib.c_void_p, _lib.c_void_p, _lib.c_int, _lib.c_void_p, _lib.c_void_p],
     # A, lda, n, d, e, w, nb_max, ws, wsd, stream
     "harp_eig_sym_fused": [_lib.c_void_p, _lib.c_long, _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p,
                            _lib.c_int, _lib.c_void_p, _lib.c_void_p, _lib.c_void_p],
@@ -185,7 +185,8 @@ _TREES: dict = {}
 
 def _tree(n: int, device: torch.device):
     """Cached D&C tree of size n: (merges int32 device [3 m], level offsets, level max
-    block sizes (ctypes int arrays), split points int64 device)."""
+    block sizes (ctypes int arrays), split points int64 device, per-level "covers all n
+    rows" flags (ctypes int array))."""
     key = (n, str(device))
     t = _TREES.get(key)
     if t is None:
@@ -194,16 +195,18 @@ def _tree(n: int, device: torch.device):
         from .tridiag_dc import tree_levels
 
         levels = tree_levels(n)
-        flat, off, smax = [], [0], []
+        flat, off, smax, full = [], [0], [], []
         for lev in levels:
             lev = sorted(lev)
             for m in lev:
                 flat += list(m)
             off.append(off[-1] + len(lev))
             smax.append(max(hi - lo for lo, _, hi in lev))
+            full.append(int(sum(hi - lo for lo, _, hi in lev) == n))  # buffers swap, no copy-back
         merges = torch.tensor(flat if flat else [0, 0, 0], dtype=torch.int32, device=device)
         mids = torch.tensor([m[1] for lev in levels for m in lev], dtype=torch.int64, device=device)
-        t = (merges, (ctypes.c_int * len(off))(*off), (ctypes.c_int * max(1, len(smax)))(*smax), len(levels), mids)
+        t = (merges, (ctypes.c_int * len(off))(*off), (ctypes.c_int * max(1, len(smax)))(*smax), len(levels), mids,
+             (ctypes.c_int * max(1, len(full)))(*full))
         _TREES[key] = t
     return t
 
@@ -220,7 +223,7 @@ def eigh_tridiag(d: torch.Tensor, e: torch.Tensor):
         return torch.from_numpy(w).to(d), torch.from_numpy(V).to(d)
     dev = d.device
     k = _lib.kernels()
-    merges, off, smax, nlev, _ = _tree(n, dev)
+    merges, off, smax, nlev, _, full = _tree(n, dev)
     ec = e.contiguous() if e.numel() else torch.zeros(1, dtype=torch.float64, device=dev)
     # dmod (d with |e| taken off both sides of every split), Q = I and the zeroed workspace
     # in one launch (csrc/tridiag_dc.hip dc_setup_kernel; the tree splits every position)
@@ -230,7 +233,7 @@ def eigh_tridiag(d: torch.Tensor, e: torch.Tensor):
     perm = torch.empty(n, dtype=torch.int64, device=dev)  # identity here, the sort order below
     _lib.check(k.harp_dc_setup(d.contiguous().data_ptr(), ec.data_ptr(), n, dmod.data_ptr(), Qt.data_ptr(),
                                ws.data_ptr(), perm.data_ptr(), _lib.stream_ptr(dev)), "dc_setup")
-    st = k.harp_dc_tridiag(dmod.data_ptr(), ec.data_ptr(), n, Qt.data_ptr(), merges.data_ptr(), off, smax, nlev,
+    st = k.harp_dc_tridiag(dmod.data_ptr(), ec.data_ptr(), n, Qt.data_ptr(), merges.data_ptr(), off, smax, full, nlev,
                            ws.data_ptr(), _lib.stream_ptr(dev))
     _lib.check(st, "dc_tridiag")
     w = torch.empty(n, dtype=torch.float64, device=dev)
