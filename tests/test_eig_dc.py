@@ -37,9 +37,31 @@ def test_dc_reference_matches_lapack(case):
 
 
 def test_tree_covers_every_split_once():
+    # csrc/tridiag_dc.hip dc_setup_kernel takes |e| off both sides of EVERY position 1 .. n - 1
     for n in (1, 2, 3, 7, 64, 1000):
         mids = [m[1] for lev in tree_levels(n) for m in lev]
         assert sorted(mids) == list(range(1, n))
+
+
+def test_tree_level_metadata():
+    """ops.eig._tree's host arrays for harp_dc_tridiag: level offsets, largest block, and the
+    "covers all n rows" flags that let a level swap the two Q buffers (no copy-back)."""
+    import torch
+
+    from harp_amd.ops.eig import _tree
+
+    for n in (2, 17, 64, 65, 1000, 4096):
+        levels = tree_levels(n)
+        merges, off, smax, nlev, _, full = _tree(n, torch.device("cpu"))
+        assert nlev == len(levels) and merges.numel() == 3 * sum(len(lev) for lev in levels)
+        for li, lev in enumerate(levels):
+            assert off[li + 1] - off[li] == len(lev)
+            assert smax[li] == max(hi - lo for lo, _, hi in lev)
+            assert full[li] == int(sum(hi - lo for lo, _, hi in lev) == n)
+            # merges of one level are disjoint row blocks
+            spans = sorted((lo, hi) for lo, _, hi in lev)
+            assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+        assert full[nlev - 1] == 1  # the top merge covers everything
 
 
 def _householder_tridiag(A):
